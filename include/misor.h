@@ -1,0 +1,163 @@
+/*
+ * misor.h -- C ABI of libmisor: MI355X-native red-black SOR for the 2D
+ * pressure Poisson equation and the 2D Navier-Stokes step kernels around it.
+ *
+ * This is the drop-in boundary for the reference's L4 solver layer.  The
+ * reference has no FFI: its C `main` calls plain functions declared in
+ * solver.h.  Each entry point below replaces one of them (cited per function);
+ * the host programs in practical-parallel-algorithms-with-mpi_amd/host/ keep
+ * the reference's own names (initSolver, solveRB, computeFG, ...) as thin
+ * wrappers over these calls, see INTEGRATION.md.
+ *
+ * Conventions
+ *  - Plain C: pointers, sizes, scalars.  No HIP/torch types in signatures.
+ *  - Host arrays exchanged with the library use the reference layout:
+ *    (ni+2) x (nj+2) doubles, row-major, i fastest, A(i,j) = a[j*(ni+2)+i]
+ *    (assignment-4/src/solver.c:16), where (ni,nj) is the LOCAL block of this
+ *    rank (= (imax,jmax) on one GPU).
+ *  - Every function returns MISOR_OK (0) or a negative MISOR_E* code;
+ *    misor_last_error() describes the last failure of the calling thread.
+ *    The reference prints and exit(EXIT_FAILURE)s instead (allocate.c:18-35,
+ *    parameter.c:32-35); the host wrappers map a non-zero return to exactly
+ *    that.
+ *  - Device fields live in HBM for the lifetime of the grid; nothing is
+ *    copied across the boundary except by misor_upload / misor_download.
+ */
+#ifndef MISOR_H
+#define MISOR_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MISOR_OK 0
+#define MISOR_EINVAL (-1)   /* bad argument */
+#define MISOR_EHIP (-2)     /* HIP runtime error */
+#define MISOR_ENOMEM (-3)   /* device allocation failed */
+#define MISOR_ECOMM (-4)    /* RCCL error */
+#define MISOR_ESTATE (-5)   /* call not valid in this state */
+
+/* field ids */
+enum { MISOR_P = 0, MISOR_RHS = 1, MISOR_U = 2, MISOR_V = 3, MISOR_F = 4, MISOR_G = 5 };
+
+/* boundary flags, assignment-5/sequential/src/solver.h:11 */
+enum { MISOR_NOSLIP = 1, MISOR_SLIP = 2, MISOR_OUTFLOW = 3, MISOR_PERIODIC = 4 };
+
+/* special boundary condition, selected in the reference by strcmp on the
+ * problem name (assignment-5/sequential/src/solver.c:345,349) */
+enum { MISOR_PROBLEM_NONE = 0, MISOR_PROBLEM_DCAVITY = 1, MISOR_PROBLEM_CANAL = 2 };
+
+/* SOR update form: solveRB (P -= factor*r, factor includes omega,
+ * assignment-4/src/solver.c:189,211) or solveRBA (P -= omega*factor*r,
+ * :250,273) */
+enum { MISOR_SOLVE_RB = 0, MISOR_SOLVE_RBA = 1 };
+
+typedef struct misor_grid misor_grid;
+
+typedef struct {
+    /* global grid and the SOR parameters of Solver
+     * (assignment-4/src/solver.h:11-22, assignment-5/sequential/src/solver.h:13-32) */
+    int imax, jmax;     /* interior cells, whole domain */
+    double dx, dy;      /* xlength/imax, ylength/jmax */
+    double omega, eps;
+    int itermax;
+    int variant;        /* MISOR_SOLVE_RB or MISOR_SOLVE_RBA */
+    int device;         /* HIP device ordinal; -1 = current device */
+    /* 2D domain decomposition (assignment-5/skeleton/src/solver.c:445-473).
+     * nranks = 1 for a single GPU; then the rest is ignored. */
+    int nranks, rank;
+    int dims[2];        /* process grid {x, y}; {0,0} = MPI_Dims_create rule */
+    const void* comm_id; /* MISOR_COMM_ID_BYTES from misor_comm_unique_id() on rank 0 */
+} misor_desc;
+
+#define MISOR_COMM_ID_BYTES 128
+
+/* NS physics parameters (assignment-5/sequential/src/solver.h:13-32) */
+typedef struct {
+    double xlength, ylength;
+    double re, gx, gy, gamma, tau;
+    int bcLeft, bcRight, bcBottom, bcTop;
+    int problem;        /* MISOR_PROBLEM_* */
+} misor_ns_desc;
+
+/* what this rank owns (for uploads/downloads and tests) */
+typedef struct {
+    int ni, nj;         /* local interior cells */
+    int ioff, joff;     /* global index of local cell (0,0) */
+    int coords[2], dims[2];
+    int neighbours[4];  /* left, right, bottom, top rank or -1 */
+    long long pitch;    /* device row pitch in doubles */
+} misor_local;
+
+/* per-grid counters; sweep_ms is summed from HIP events recorded around
+ * every sweep kernel when timing is enabled (misor_enable_timing) */
+typedef struct {
+    long long sweeps;       /* red+black iterations executed on the device */
+    long long launches;     /* sweep kernels launched (incl. early-exited) */
+    double sweep_ms;        /* total device time of sweep kernels (timing on) */
+    long long timed_sweeps; /* launches covered by sweep_ms */
+} misor_stats;
+
+const char* misor_last_error(void);
+const char* misor_version(void);
+
+/* decomposition rule of MPI_Dims_create(n, 2) + sizeOfRank
+ * (assignment-5/skeleton/src/solver.c:30-32,445,472-473); host-only */
+int misor_decompose(int nranks, int rank, int imax, int jmax, const int dims_in[2],
+                    misor_local* out);
+
+/* rank 0 calls this and ships the bytes to the other ranks out of band */
+int misor_comm_unique_id(void* id_out /* MISOR_COMM_ID_BYTES */);
+
+/* replaces the allocation half of initSolver (assignment-4/src/solver.c:83-97,
+ * assignment-5/sequential/src/solver.c:59-91): all six fields, zeroed */
+int misor_create(misor_grid** out, const misor_desc* desc);
+void misor_destroy(misor_grid* g);
+int misor_local_info(const misor_grid* g, misor_local* out);
+
+/* stream the grid's kernels run on (hipStream_t as void*); NULL = own stream */
+int misor_set_stream(misor_grid* g, void* hip_stream);
+int misor_synchronize(misor_grid* g);
+
+int misor_upload(misor_grid* g, int field, const double* host);
+int misor_download(misor_grid* g, int field, double* host);
+/* fill a field (incl. ghosts) with a constant; initSolver of NS (solver.c:92-99) */
+int misor_fill(misor_grid* g, int field, double value);
+
+/* initSolver of assignment-4 (solver.c:99-123): p = sin(4 pi i dx) +
+ * sin(4 pi j dy), rhs = sin(2 pi i dx) for problem 2 else 0, incl. ghosts.
+ * The 1-D sine tables are evaluated on the host with libm exactly as the
+ * reference does, so the fields are bit-identical to it. */
+int misor_poisson_init(misor_grid* g, double xlength, double ylength, int problem);
+
+/* solveRB / solveRBA (assignment-4/src/solver.c:179-299): red-black SOR
+ * with Neumann ghost copy after each iteration, until res < eps^2 or itermax.
+ * *iters = iterations done (the reference prints it, :237), *res = final
+ * residual (sum r^2 / (imax*jmax)).  Either output may be NULL. */
+int misor_solve_rb(misor_grid* g, int* iters, double* res);
+/* the same with an explicit cap that overrides desc.itermax for this call */
+int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res);
+
+/* NS step kernels (assignment-5/sequential/src/solver.c) */
+int misor_ns_setup(misor_grid* g, const misor_ns_desc* ns);
+int misor_compute_timestep(misor_grid* g, double dt_bound, double tau, double* dt_out); /* :219-234 */
+int misor_set_dt(misor_grid* g, double dt);
+int misor_set_boundary_conditions(misor_grid* g);          /* :236-337 */
+int misor_set_special_boundary_condition(misor_grid* g);   /* :339-358 */
+int misor_compute_fg(misor_grid* g);                        /* :360-436 */
+int misor_compute_rhs(misor_grid* g);                       /* :122-138 */
+int misor_normalize_pressure(misor_grid* g);                /* :204-217 */
+int misor_adapt_uv(misor_grid* g);                          /* :438-455 */
+/* max |u| and max |v| over all cells incl. ghosts (maxElement, :193-202) */
+int misor_max_uv(misor_grid* g, double* umax, double* vmax);
+
+int misor_enable_timing(misor_grid* g, int on);
+int misor_get_stats(const misor_grid* g, misor_stats* out);
+int misor_reset_stats(misor_grid* g);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

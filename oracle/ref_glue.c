@@ -1,0 +1,254 @@
+/*
+ * ref_glue.c -- drives the REFERENCE'S OWN compiled functions (oracle/_ref).
+ *
+ * TEST INFRASTRUCTURE ONLY.  oracle/Makefile compiles the reference sources in
+ * place under /root/reference (never copied into this repo) together with this
+ * file into oracle/_ref/libref.so.  This file is ours: it contains no
+ * reference code, only calls into it, so the tests can compare the CPU
+ * restatement (oracle.c) with the reference itself.
+ *
+ * Linked objects (all compiled -O2 -std=c99 -ffp-contract=off):
+ *   assignment-5/sequential/src/{solver,parameter,allocate}.c  (NS + .par)
+ *   assignment-4/src/solver.c  with every global symbol prefixed a4_
+ *   assignment-4/src/parameter.c with every global symbol prefixed a4_
+ * The a4 routines take assignment-4's Solver layout (assignment-4/src/solver.h:11-22),
+ * declared below as A4Solver so both layouts can be used from one library.
+ *
+ * The reference reports iteration counts only on stdout ("%d ",
+ * assignment-4/src/solver.c:176,237), so the calls below redirect fd 1 to a
+ * temporary file and parse it back.
+ */
+#ifndef _GNU_SOURCE
+#define _GNU_SOURCE
+#endif
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include "parameter.h" /* assignment-5/sequential/src/parameter.h */
+#include "solver.h"    /* assignment-5/sequential/src/solver.h    */
+
+typedef struct { /* layout of assignment-4/src/solver.h:11-22 */
+    double dx, dy;
+    double ys;
+    int imax, jmax;
+    int jmaxLocal;
+    int rank;
+    int size;
+    double *p, *rhs;
+    double eps, omega;
+    int itermax;
+} A4Solver;
+
+typedef struct { /* layout of assignment-4/src/parameter.h:10-15 */
+    double xlength, ylength;
+    int imax, jmax;
+    int itermax;
+    double eps, omg;
+} A4Parameter;
+
+void a4_initSolver(A4Solver*, A4Parameter*, int problem);
+void a4_solve(A4Solver*);
+void a4_solveRB(A4Solver*);
+void a4_solveRBA(A4Solver*);
+void a4_writeResult(A4Solver*, char*);
+void a4_initParameter(A4Parameter*);
+void a4_readParameter(A4Parameter*, const char*);
+
+/* ---- stdout capture ---- */
+static int cap_fd = -1, saved_fd = -1;
+static FILE* cap_file;
+
+static void capture_begin(void)
+{
+    fflush(stdout);
+    cap_file = tmpfile();
+    saved_fd = dup(1);
+    cap_fd   = fileno(cap_file);
+    dup2(cap_fd, 1);
+}
+
+/* returns malloc'd text written to stdout since capture_begin */
+static char* capture_end(void)
+{
+    fflush(stdout);
+    dup2(saved_fd, 1);
+    close(saved_fd);
+    long n = ftell(cap_file);
+    if (n < 0) n = 0;
+    rewind(cap_file);
+    char* buf = (char*)malloc((size_t)n + 1);
+    size_t got = fread(buf, 1, (size_t)n, cap_file);
+    buf[got] = '\0';
+    fclose(cap_file);
+    return buf;
+}
+
+/* ---- assignment-4 Poisson ---- */
+
+/* which: 0 = solve (lexicographic), 1 = solveRB, 2 = solveRBA.
+ * p/rhs: (imax+2)(jmax+2) outputs (final p, the rhs used).  If init_p is
+ * non-NULL it replaces the initial p after initSolver.  Returns iterations. */
+int refa4_run(int imax, int jmax, double xlength, double ylength, int itermax,
+              double eps, double omg, int problem, int which, const double* init_p,
+              double* p_out, double* rhs_out)
+{
+    A4Parameter prm;
+    A4Solver s;
+    a4_initParameter(&prm);
+    prm.imax = imax;
+    prm.jmax = jmax;
+    prm.xlength = xlength;
+    prm.ylength = ylength;
+    prm.itermax = itermax;
+    prm.eps = eps;
+    prm.omg = omg;
+    a4_initSolver(&s, &prm, problem);
+    size_t n = (size_t)(imax + 2) * (size_t)(jmax + 2);
+    if (init_p) memcpy(s.p, init_p, n * sizeof(double));
+    capture_begin();
+    if (which == 0) a4_solve(&s);
+    else if (which == 1) a4_solveRB(&s);
+    else a4_solveRBA(&s);
+    char* out = capture_end();
+    int it = atoi(out);
+    free(out);
+    if (p_out) memcpy(p_out, s.p, n * sizeof(double));
+    if (rhs_out) memcpy(rhs_out, s.rhs, n * sizeof(double));
+    free(s.p);
+    free(s.rhs);
+    return it;
+}
+
+/* writeResult of assignment-4 on a given field -> file */
+void refa4_write(int imax, int jmax, double* p, const char* path)
+{
+    A4Solver s;
+    memset(&s, 0, sizeof s);
+    s.imax = imax;
+    s.jmax = jmax;
+    s.p = p;
+    a4_writeResult(&s, (char*)path);
+}
+
+/* the a4 .par reader; fills the 7 assignment-4 keys */
+void refa4_read_parameter(const char* path, int* imax, int* jmax, int* itermax,
+                          double* xlength, double* ylength, double* eps, double* omg)
+{
+    A4Parameter prm;
+    a4_initParameter(&prm);
+    a4_readParameter(&prm, path);
+    *imax = prm.imax; *jmax = prm.jmax; *itermax = prm.itermax;
+    *xlength = prm.xlength; *ylength = prm.ylength; *eps = prm.eps; *omg = prm.omg;
+}
+
+/* ---- assignment-5/sequential NS ---- */
+
+/* the a5 .par reader (22 keys, defaults assignment-5/sequential/src/parameter.c:15-27) */
+void refns_read_parameter(const char* path, Parameter* out)
+{
+    initParameter(out);
+    out->name = NULL;
+    readParameter(out, path);
+}
+int refns_parameter_size(void) { return (int)sizeof(Parameter); }
+
+/* Replays assignment-5/sequential/src/main.c:37-60 with the reference's own
+ * functions.  solver 0: the shipped lexicographic solve(); 1: assignment-4's
+ * solveRB on the NS p/rhs (the composed RB-NS oracle).
+ * te < 0 keeps the .par te.  Returns steps; fills iters (cap entries), the
+ * final p/u/v (each (imax+2)(jmax+2)) and *t_out. */
+int refns_run(const char* par, double te, int max_steps, int solver, int* iters,
+              int cap, double* p_out, double* u_out, double* v_out, double* t_out)
+{
+    Parameter prm;
+    Solver s;
+    initParameter(&prm);
+    prm.name = NULL;
+    readParameter(&prm, par);
+    if (te >= 0.0) prm.te = te;
+    initSolver(&s, &prm);
+
+    A4Solver a4;
+    memset(&a4, 0, sizeof a4);
+    a4.dx = s.dx; a4.dy = s.dy; a4.imax = s.imax; a4.jmax = s.jmax;
+    a4.p = s.p; a4.rhs = s.rhs; a4.eps = s.eps; a4.omega = s.omega;
+    a4.itermax = s.itermax;
+
+    double t = 0.0;
+    int nt = 0;
+    while (t <= s.te && (max_steps < 0 || nt < max_steps)) {
+        if (s.tau > 0.0) computeTimestep(&s);
+        setBoundaryConditions(&s);
+        setSpecialBoundaryCondition(&s);
+        computeFG(&s);
+        computeRHS(&s);
+        if (nt % 100 == 0) normalizePressure(&s);
+        int it;
+        if (solver == 1) {
+            capture_begin();
+            a4_solveRB(&a4);
+            char* out = capture_end();
+            it = atoi(out);
+            free(out);
+        } else {
+            /* the shipped solve() prints nothing unless VERBOSE: count by
+             * re-deriving nothing -- report -1 */
+            solve(&s);
+            it = -1;
+        }
+        if (iters && nt < cap) iters[nt] = it;
+        adaptUV(&s);
+        t += s.dt;
+        nt++;
+    }
+    size_t n = (size_t)(s.imax + 2) * (size_t)(s.jmax + 2);
+    if (p_out) memcpy(p_out, s.p, n * sizeof(double));
+    if (u_out) memcpy(u_out, s.u, n * sizeof(double));
+    if (v_out) memcpy(v_out, s.v, n * sizeof(double));
+    if (t_out) *t_out = t;
+    free(s.u); free(s.v); free(s.p); free(s.rhs); free(s.f); free(s.g);
+    free(prm.name);
+    return nt;
+}
+
+/* writeResult of the sequential NS (pressure.dat, velocity.dat in cwd) after
+ * a run -- used to regenerate the committed .dat format */
+int refns_run_and_write(const char* par, double te, int solver)
+{
+    Parameter prm;
+    Solver s;
+    initParameter(&prm);
+    prm.name = NULL;
+    readParameter(&prm, par);
+    if (te >= 0.0) prm.te = te;
+    initSolver(&s, &prm);
+    A4Solver a4;
+    memset(&a4, 0, sizeof a4);
+    a4.dx = s.dx; a4.dy = s.dy; a4.imax = s.imax; a4.jmax = s.jmax;
+    a4.p = s.p; a4.rhs = s.rhs; a4.eps = s.eps; a4.omega = s.omega;
+    a4.itermax = s.itermax;
+    double t = 0.0;
+    int nt = 0;
+    while (t <= s.te) {
+        if (s.tau > 0.0) computeTimestep(&s);
+        setBoundaryConditions(&s);
+        setSpecialBoundaryCondition(&s);
+        computeFG(&s);
+        computeRHS(&s);
+        if (nt % 100 == 0) normalizePressure(&s);
+        if (solver == 1) {
+            capture_begin();
+            a4_solveRB(&a4);
+            free(capture_end());
+        } else {
+            solve(&s);
+        }
+        adaptUV(&s);
+        t += s.dt;
+        nt++;
+    }
+    writeResult(&s);
+    return nt;
+}

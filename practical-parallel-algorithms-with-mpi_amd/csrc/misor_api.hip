@@ -1,0 +1,632 @@
+// misor_api.hip -- the C ABI of include/misor.h: device state, transfers,
+// the solve loop (batched launches with a device-resident convergence flag),
+// the NS step entry points and the 2D decomposition over RCCL.
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "misor_internal.h"
+
+using namespace misor;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIPCHK(x)                                                                         \
+    do {                                                                                  \
+        hipError_t e_ = (x);                                                              \
+        if (e_ != hipSuccess)                                                             \
+            return fail(MISOR_EHIP, "%s: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, \
+                        __LINE__);                                                        \
+    } while (0)
+
+#define NCCLCHK(x)                                                                        \
+    do {                                                                                  \
+        ncclResult_t r_ = (x);                                                            \
+        if (r_ != ncclSuccess)                                                            \
+            return fail(MISOR_ECOMM, "%s: %s (%s:%d)", #x, ncclGetErrorString(r_),        \
+                        __FILE__, __LINE__);                                              \
+    } while (0)
+
+enum { kP0 = 0, kP1 = 1, kRhs = 2, kU = 3, kV = 4, kF = 5, kG = 6, kNumFields = 7 };
+
+// MPI_Dims_create(n, 2): the most balanced factorisation, larger factor first
+void dims_create(int n, int dims[2]) {
+    int best = 1;
+    for (int d = 1; d * d <= n; ++d)
+        if (n % d == 0) best = d;
+    dims[0] = n / best;
+    dims[1] = best;
+}
+
+// sizeOfRank (assignment-5/skeleton/src/solver.c:30-32)
+int size_of_rank(int rank, int size, int n) { return n / size + ((n % size > rank) ? 1 : 0); }
+
+}  // namespace
+
+struct misor_grid {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    misor_desc desc{};
+    misor_local loc{};
+    long long pitch = 0, rows = 0, elems = 0;
+    double* fld[kNumFields] = {};
+    int cur = 0;  // which p buffer holds the current pressure
+
+    // sweep
+    SweepParams sp{};
+    int nbx = 0, nby = 0, nparts = 0;
+    double* partials = nullptr;
+    DevState* st = nullptr;
+    DevState* st_host = nullptr;  // pinned
+    int last_iters = 0;
+
+    // reductions
+    double* red_partials = nullptr;
+    double* red_out = nullptr;   // 4 doubles on device
+    double* red_host = nullptr;  // 4 doubles pinned
+
+    // NS
+    bool ns_ready = false;
+    NsLaunch nl{};
+
+    // multi-GPU
+    bool dist = false;
+    ncclComm_t comm = nullptr;
+
+    // stats
+    bool timing = false;
+    std::vector<hipEvent_t> ev;
+    misor_stats stats{};
+};
+
+extern "C" {
+
+const char* misor_last_error(void) { return g_err.c_str(); }
+const char* misor_version(void) { return "misor 0.1 (gfx950, fp64 red-black SOR)"; }
+
+int misor_decompose(int nranks, int rank, int imax, int jmax, const int dims_in[2],
+                    misor_local* out) {
+    if (!out || nranks < 1 || rank < 0 || rank >= nranks || imax < 2 || jmax < 2)
+        return fail(MISOR_EINVAL, "misor_decompose: bad arguments");
+    int dims[2] = {0, 0};
+    if (dims_in && dims_in[0] > 0 && dims_in[1] > 0) {
+        dims[0] = dims_in[0];
+        dims[1] = dims_in[1];
+        if (dims[0] * dims[1] != nranks)
+            return fail(MISOR_EINVAL, "dims %dx%d != nranks %d", dims[0], dims[1], nranks);
+    } else {
+        dims_create(nranks, dims);
+    }
+    // MPI_Cart_create row-major rank order: coords = (rank / dims[1], rank % dims[1])
+    const int cx = rank / dims[1], cy = rank % dims[1];
+    misor_local L{};
+    L.dims[0] = dims[0];
+    L.dims[1] = dims[1];
+    L.coords[0] = cx;
+    L.coords[1] = cy;
+    L.ni = size_of_rank(cx, dims[0], imax);
+    L.nj = size_of_rank(cy, dims[1], jmax);
+    int io = 0, jo = 0;
+    for (int c = 0; c < cx; ++c) io += size_of_rank(c, dims[0], imax);
+    for (int c = 0; c < cy; ++c) jo += size_of_rank(c, dims[1], jmax);
+    L.ioff = io;
+    L.joff = jo;
+    auto rank_of = [&](int x, int y) { return x * dims[1] + y; };
+    L.neighbours[0] = cx > 0 ? rank_of(cx - 1, cy) : -1;            // left
+    L.neighbours[1] = cx < dims[0] - 1 ? rank_of(cx + 1, cy) : -1;  // right
+    L.neighbours[2] = cy > 0 ? rank_of(cx, cy - 1) : -1;            // bottom
+    L.neighbours[3] = cy < dims[1] - 1 ? rank_of(cx, cy + 1) : -1;  // top
+    if (L.ni < 2 || L.nj < 2) return fail(MISOR_EINVAL, "local block smaller than 2x2");
+    L.pitch = layout_pitch(L.ni);
+    *out = L;
+    return MISOR_OK;
+}
+
+int misor_comm_unique_id(void* id_out) {
+    if (!id_out) return fail(MISOR_EINVAL, "null id");
+    ncclUniqueId id;
+    NCCLCHK(ncclGetUniqueId(&id));
+    static_assert(sizeof(ncclUniqueId) == MISOR_COMM_ID_BYTES, "ncclUniqueId size");
+    memcpy(id_out, &id, sizeof id);
+    return MISOR_OK;
+}
+
+void misor_destroy(misor_grid* g) {
+    if (!g) return;
+    (void)hipSetDevice(g->device);
+    if (g->stream) (void)hipStreamSynchronize(g->stream);
+    for (auto& f : g->fld)
+        if (f) (void)hipFree(f);
+    (void)hipFree(g->partials);
+    (void)hipFree(g->st);
+    (void)hipHostFree(g->st_host);
+    (void)hipFree(g->red_partials);
+    (void)hipFree(g->red_out);
+    (void)hipHostFree(g->red_host);
+    for (auto e : g->ev) (void)hipEventDestroy(e);
+    if (g->comm) ncclCommDestroy(g->comm);
+    if (g->own_stream && g->stream) (void)hipStreamDestroy(g->stream);
+    delete g;
+}
+
+static int pick_rows_per_block(int ni, int nj) {
+    // enough workgroups to fill 256 CUs several times, but long enough row
+    // marches that the two redundant halo rows per block stay cheap
+    const int strips = (ni + kStripCells - 1) / kStripCells;
+    const int nbx = (strips + kWavesX - 1) / kWavesX;
+    const int target_blocks = 2048;
+    int want_nby = (target_blocks + nbx - 1) / nbx;
+    int h = (nj + want_nby - 1) / want_nby;
+    if (h < 4) h = 4;
+    if (h > 128) h = 128;
+    return h;
+}
+
+int misor_create(misor_grid** out, const misor_desc* d) {
+    if (!out || !d) return fail(MISOR_EINVAL, "null argument");
+    *out = nullptr;
+    if (d->imax < 2 || d->jmax < 2) return fail(MISOR_EINVAL, "imax, jmax must be >= 2");
+    if (!(d->dx > 0) || !(d->dy > 0)) return fail(MISOR_EINVAL, "dx, dy must be > 0");
+    const int nranks = d->nranks < 1 ? 1 : d->nranks;
+    misor_local L{};
+    int rc = misor_decompose(nranks, nranks == 1 ? 0 : d->rank, d->imax, d->jmax, d->dims, &L);
+    if (rc) return rc;
+
+    misor_grid* g = new misor_grid();
+    g->desc = *d;
+    g->desc.nranks = nranks;
+    g->loc = L;
+    g->dist = nranks > 1;
+    if (d->device >= 0) {
+        g->device = d->device;
+        if (hipSetDevice(g->device) != hipSuccess) {
+            delete g;
+            return fail(MISOR_EHIP, "hipSetDevice(%d) failed", d->device);
+        }
+    } else {
+        (void)hipGetDevice(&g->device);
+    }
+#define CREATE_FAIL(code, ...)          \
+    do {                                \
+        int c_ = fail(code, __VA_ARGS__); \
+        misor_destroy(g);               \
+        return c_;                      \
+    } while (0)
+    if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess)
+        CREATE_FAIL(MISOR_EHIP, "hipStreamCreate failed");
+    g->own_stream = true;
+
+    g->pitch = layout_pitch(L.ni);
+    g->rows = layout_rows(L.nj);
+    g->elems = g->pitch * g->rows;
+    for (int k = 0; k < kNumFields; ++k) {
+        if (hipMalloc(&g->fld[k], (size_t)g->elems * sizeof(double)) != hipSuccess)
+            CREATE_FAIL(MISOR_ENOMEM, "hipMalloc of %lld doubles failed", g->elems);
+        if (hipMemsetAsync(g->fld[k], 0, (size_t)g->elems * sizeof(double), g->stream) !=
+            hipSuccess)
+            CREATE_FAIL(MISOR_EHIP, "hipMemset failed");
+    }
+
+    // sweep configuration
+    SweepParams& sp = g->sp;
+    sp.pitch = g->pitch;
+    sp.ni = L.ni;
+    sp.nj = L.nj;
+    sp.rows_per_block = pick_rows_per_block(L.ni, L.nj);
+    sp.parity = (L.ioff + L.joff) & 1;
+    sp.ghost_left = L.neighbours[0] < 0;
+    sp.ghost_right = L.neighbours[1] < 0;
+    sp.ghost_bottom = L.neighbours[2] < 0;
+    sp.ghost_top = L.neighbours[3] < 0;
+    const double dx2 = d->dx * d->dx, dy2 = d->dy * d->dy;
+    sp.idx2 = 1.0 / dx2;
+    sp.idy2 = 1.0 / dy2;
+    if (d->variant == MISOR_SOLVE_RBA) {
+        const double factor = 0.5 * (dx2 * dy2) / (dx2 + dy2);  // solver.c:250
+        sp.coef = d->omega * factor;                            // (omega*factor)*r, :273
+    } else {
+        sp.coef = d->omega * 0.5 * (dx2 * dy2) / (dx2 + dy2);  // solver.c:189
+    }
+    g->nparts = sweep_partials(L.ni, L.nj, sp.rows_per_block, &g->nbx, &g->nby);
+    if (hipMalloc(&g->partials, sizeof(double) * g->nparts) != hipSuccess ||
+        hipMalloc(&g->st, sizeof(DevState)) != hipSuccess ||
+        hipHostMalloc(&g->st_host, sizeof(DevState), hipHostMallocDefault) != hipSuccess)
+        CREATE_FAIL(MISOR_ENOMEM, "state allocation failed");
+    const int rb = reduce_blocks(L.ni, L.nj);
+    if (hipMalloc(&g->red_partials, sizeof(double) * 2 * rb) != hipSuccess ||
+        hipMalloc(&g->red_out, sizeof(double) * 4) != hipSuccess ||
+        hipHostMalloc(&g->red_host, sizeof(double) * 4, hipHostMallocDefault) != hipSuccess)
+        CREATE_FAIL(MISOR_ENOMEM, "reduction allocation failed");
+
+    if (g->dist) {
+        if (!d->comm_id) CREATE_FAIL(MISOR_EINVAL, "nranks > 1 needs comm_id");
+        ncclUniqueId id;
+        memcpy(&id, d->comm_id, sizeof id);
+        if (ncclCommInitRank(&g->comm, nranks, id, d->rank) != ncclSuccess)
+            CREATE_FAIL(MISOR_ECOMM, "ncclCommInitRank failed");
+    }
+    if (hipStreamSynchronize(g->stream) != hipSuccess)
+        CREATE_FAIL(MISOR_EHIP, "hipStreamSynchronize failed");
+#undef CREATE_FAIL
+    *out = g;
+    return MISOR_OK;
+}
+
+int misor_local_info(const misor_grid* g, misor_local* out) {
+    if (!g || !out) return fail(MISOR_EINVAL, "null argument");
+    *out = g->loc;
+    return MISOR_OK;
+}
+
+int misor_set_stream(misor_grid* g, void* s) {
+    if (!g) return fail(MISOR_EINVAL, "null grid");
+    HIPCHK(hipSetDevice(g->device));
+    HIPCHK(hipStreamSynchronize(g->stream));
+    if (g->own_stream) HIPCHK(hipStreamDestroy(g->stream));
+    if (s) {
+        g->stream = (hipStream_t)s;
+        g->own_stream = false;
+    } else {
+        HIPCHK(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
+        g->own_stream = true;
+    }
+    g->nl.s = g->stream;
+    return MISOR_OK;
+}
+
+int misor_synchronize(misor_grid* g) {
+    if (!g) return fail(MISOR_EINVAL, "null grid");
+    HIPCHK(hipStreamSynchronize(g->stream));
+    return MISOR_OK;
+}
+
+static double* field_ptr(misor_grid* g, int field) {
+    switch (field) {
+    case MISOR_P: return g->fld[g->cur];
+    case MISOR_RHS: return g->fld[kRhs];
+    case MISOR_U: return g->fld[kU];
+    case MISOR_V: return g->fld[kV];
+    case MISOR_F: return g->fld[kF];
+    case MISOR_G: return g->fld[kG];
+    default: return nullptr;
+    }
+}
+
+static double* origin(misor_grid* g, double* base) {
+    return base + (long long)kYOff * g->pitch + kXOff;  // cell (0,0)
+}
+
+int misor_upload(misor_grid* g, int field, const double* host) {
+    if (!g || !host || !field_ptr(g, field)) return fail(MISOR_EINVAL, "bad upload");
+    HIPCHK(hipSetDevice(g->device));
+    const size_t w = (size_t)(g->loc.ni + 2) * sizeof(double);
+    const size_t h = (size_t)(g->loc.nj + 2);
+    if (field == MISOR_P) {  // both ping-pong buffers: corners and ghosts must agree
+        g->cur = 0;
+        for (int b = 0; b < 2; ++b)
+            HIPCHK(hipMemcpy2DAsync(origin(g, g->fld[kP0 + b]), g->pitch * sizeof(double), host,
+                                    w, w, h, hipMemcpyHostToDevice, g->stream));
+    } else {
+        HIPCHK(hipMemcpy2DAsync(origin(g, field_ptr(g, field)), g->pitch * sizeof(double), host,
+                                w, w, h, hipMemcpyHostToDevice, g->stream));
+    }
+    HIPCHK(hipStreamSynchronize(g->stream));
+    return MISOR_OK;
+}
+
+int misor_download(misor_grid* g, int field, double* host) {
+    if (!g || !host || !field_ptr(g, field)) return fail(MISOR_EINVAL, "bad download");
+    HIPCHK(hipSetDevice(g->device));
+    const size_t w = (size_t)(g->loc.ni + 2) * sizeof(double);
+    const size_t h = (size_t)(g->loc.nj + 2);
+    HIPCHK(hipMemcpy2DAsync(host, w, origin(g, field_ptr(g, field)), g->pitch * sizeof(double), w,
+                            h, hipMemcpyDeviceToHost, g->stream));
+    HIPCHK(hipStreamSynchronize(g->stream));
+    return MISOR_OK;
+}
+
+int misor_fill(misor_grid* g, int field, double value) {
+    if (!g || !field_ptr(g, field)) return fail(MISOR_EINVAL, "bad fill");
+    HIPCHK(hipSetDevice(g->device));
+    // whole padded array: ghosts included, pads too (pads never feed results)
+    if (field == MISOR_P) {
+        g->cur = 0;
+        launch_fill(g->stream, g->fld[kP0], g->elems, value);
+        launch_fill(g->stream, g->fld[kP1], g->elems, value);
+    } else {
+        launch_fill(g->stream, field_ptr(g, field), g->elems, value);
+    }
+    HIPCHK(hipGetLastError());
+    return MISOR_OK;
+}
+
+int misor_poisson_init(misor_grid* g, double xlength, double ylength, int problem) {
+    if (!g) return fail(MISOR_EINVAL, "null grid");
+    HIPCHK(hipSetDevice(g->device));
+    const int ni = g->loc.ni, nj = g->loc.nj;
+    const double PI = 3.14159265358979323846;  // assignment-4/src/solver.c:15
+    const double dx = xlength / g->desc.imax, dy = ylength / g->desc.jmax;
+    // host tables with the reference's exact expressions (solver.c:107,114)
+    std::vector<double> sx(ni + 2), sy(nj + 2), rx(ni + 2);
+    for (int i = 0; i < ni + 2; ++i) {
+        const int gi = g->loc.ioff + i;
+        sx[i] = sin(2.0 * PI * gi * dx * 2.0);
+        rx[i] = sin(2.0 * PI * gi * dx);
+    }
+    for (int j = 0; j < nj + 2; ++j) sy[j] = sin(2.0 * PI * (g->loc.joff + j) * dy * 2.0);
+    double* tab = nullptr;
+    const size_t n = (size_t)(2 * (ni + 2) + (nj + 2));
+    HIPCHK(hipMalloc(&tab, n * sizeof(double)));
+    HIPCHK(hipMemcpyAsync(tab, sx.data(), (ni + 2) * sizeof(double), hipMemcpyHostToDevice,
+                          g->stream));
+    HIPCHK(hipMemcpyAsync(tab + (ni + 2), rx.data(), (ni + 2) * sizeof(double),
+                          hipMemcpyHostToDevice, g->stream));
+    HIPCHK(hipMemcpyAsync(tab + 2 * (ni + 2), sy.data(), (nj + 2) * sizeof(double),
+                          hipMemcpyHostToDevice, g->stream));
+    g->cur = 0;
+    for (int b = 0; b < 2; ++b)
+        launch_poisson_init(g->stream, g->fld[kP0 + b], g->fld[kRhs], tab, tab + 2 * (ni + 2),
+                            tab + (ni + 2), ni, nj, g->pitch, problem);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(g->stream));
+    HIPCHK(hipFree(tab));
+    return MISOR_OK;
+}
+
+// ---------------------------------------------------------------------------
+// solve loop
+// ---------------------------------------------------------------------------
+
+static int ensure_events(misor_grid* g, size_t n) {
+    while (g->ev.size() < n) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreate(&e));
+        g->ev.push_back(e);
+    }
+    return MISOR_OK;
+}
+
+int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
+    if (!g) return fail(MISOR_EINVAL, "null grid");
+    if (g->dist) return fail(MISOR_ESTATE, "decomposed solve not built yet");
+    HIPCHK(hipSetDevice(g->device));
+    const double epssq = g->desc.eps * g->desc.eps;
+    DevState s0{};
+    s0.it = 0;
+    s0.res = 1.0;
+    s0.epssq = epssq;
+    s0.itermax = itermax;
+    s0.done = !((1.0 >= epssq) && (0 < itermax));  // loop test of solver.c:197
+    if (s0.done) {
+        if (iters) *iters = 0;
+        if (res) *res = 1.0;
+        return MISOR_OK;
+    }
+    *g->st_host = s0;
+    HIPCHK(hipMemcpyAsync(g->st, g->st_host, sizeof(DevState), hipMemcpyHostToDevice,
+                          g->stream));
+    const double cells = (double)g->desc.imax * (double)g->desc.jmax;
+    const int cur0 = g->cur;
+    long long launched = 0;
+    int batch = g->last_iters > 8 ? g->last_iters : 8;
+    for (;;) {
+        if (batch > itermax - launched) batch = (int)(itermax - launched);
+        if (batch < 1) batch = 1;
+        if (g->timing) {
+            int rc = ensure_events(g, 2 * (size_t)batch);
+            if (rc) return rc;
+        }
+        for (int b = 0; b < batch; ++b) {
+            const long long k = launched + b;
+            const double* src = g->fld[kP0 + ((cur0 + k) & 1)];
+            double* dst = g->fld[kP0 + ((cur0 + k + 1) & 1)];
+            if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b], g->stream));
+            launch_sweep(g->stream, g->sp, src, dst, g->fld[kRhs], g->partials, g->st, g->nbx,
+                         g->nby);
+            if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b + 1], g->stream));
+            launch_finish(g->stream, g->partials, g->nparts, g->st, cells);
+        }
+        HIPCHK(hipGetLastError());
+        launched += batch;
+        g->stats.launches += batch;
+        HIPCHK(hipMemcpyAsync(g->st_host, g->st, sizeof(DevState), hipMemcpyDeviceToHost,
+                              g->stream));
+        HIPCHK(hipStreamSynchronize(g->stream));
+        if (g->timing) {
+            // launches after convergence exit at once; count only real sweeps
+            const long long real_before = launched - batch;
+            const long long real_end = g->st_host->it;
+            for (int b = 0; b < batch; ++b) {
+                if (real_before + b >= real_end) break;
+                float ms = 0.f;
+                HIPCHK(hipEventElapsedTime(&ms, g->ev[2 * b], g->ev[2 * b + 1]));
+                g->stats.sweep_ms += ms;
+                g->stats.timed_sweeps++;
+            }
+        }
+        if (g->st_host->done) break;
+        if (launched >= itermax) break;  // cannot happen: done covers it
+        batch = batch < 512 ? 2 * batch : 1024;
+    }
+    const int it = g->st_host->it;
+    g->cur = (cur0 + it) & 1;
+    g->last_iters = it;
+    g->stats.sweeps += it;
+    if (iters) *iters = it;
+    if (res) *res = g->st_host->res;
+    return MISOR_OK;
+}
+
+int misor_solve_rb(misor_grid* g, int* iters, double* res) {
+    if (!g) return fail(MISOR_EINVAL, "null grid");
+    return misor_solve_rb_n(g, g->desc.itermax, iters, res);
+}
+
+// ---------------------------------------------------------------------------
+// NS step
+// ---------------------------------------------------------------------------
+
+int misor_ns_setup(misor_grid* g, const misor_ns_desc* ns) {
+    if (!g || !ns) return fail(MISOR_EINVAL, "null argument");
+    NsLaunch& L = g->nl;
+    L.s = g->stream;
+    L.pitch = g->pitch;
+    L.ni = g->loc.ni;
+    L.nj = g->loc.nj;
+    L.prm.dx = g->desc.dx;
+    L.prm.dy = g->desc.dy;
+    L.prm.dt = 0.0;
+    L.prm.xlength = ns->xlength;
+    L.prm.ylength = ns->ylength;
+    L.prm.re = ns->re;
+    L.prm.gx = ns->gx;
+    L.prm.gy = ns->gy;
+    L.prm.gamma = ns->gamma;
+    L.prm.bc_left = ns->bcLeft;
+    L.prm.bc_right = ns->bcRight;
+    L.prm.bc_bottom = ns->bcBottom;
+    L.prm.bc_top = ns->bcTop;
+    L.prm.problem = ns->problem;
+    L.wall_left = g->loc.neighbours[0] < 0;
+    L.wall_right = g->loc.neighbours[1] < 0;
+    L.wall_bottom = g->loc.neighbours[2] < 0;
+    L.wall_top = g->loc.neighbours[3] < 0;
+    L.ioff = g->loc.ioff;
+    L.joff = g->loc.joff;
+    L.imax_g = g->desc.imax;
+    L.jmax_g = g->desc.jmax;
+    g->ns_ready = true;
+    return MISOR_OK;
+}
+
+#define NEED_NS(g)                                                                 \
+    do {                                                                           \
+        if (!(g)) return fail(MISOR_EINVAL, "null grid");                          \
+        if (!(g)->ns_ready) return fail(MISOR_ESTATE, "misor_ns_setup not called"); \
+        HIPCHK(hipSetDevice((g)->device));                                         \
+    } while (0)
+
+int misor_max_uv(misor_grid* g, double* umax, double* vmax) {
+    NEED_NS(g);
+    launch_absmax2(g->nl, g->fld[kU], g->fld[kV], g->red_partials);
+    launch_finish_reduce(g->stream, g->red_partials, reduce_blocks(g->loc.ni, g->loc.nj),
+                         kReduceMax, 2, g->red_out);
+    HIPCHK(hipGetLastError());
+    if (g->dist)
+        NCCLCHK(ncclAllReduce(g->red_out, g->red_out, 2, ncclDouble, ncclMax, g->comm,
+                              g->stream));
+    HIPCHK(hipMemcpyAsync(g->red_host, g->red_out, 2 * sizeof(double), hipMemcpyDeviceToHost,
+                          g->stream));
+    HIPCHK(hipStreamSynchronize(g->stream));
+    if (umax) *umax = g->red_host[0];
+    if (vmax) *vmax = g->red_host[1];
+    return MISOR_OK;
+}
+
+int misor_compute_timestep(misor_grid* g, double dt_bound, double tau, double* dt_out) {
+    double umax = 0, vmax = 0;
+    int rc = misor_max_uv(g, &umax, &vmax);
+    if (rc) return rc;
+    // computeTimestep, assignment-5/sequential/src/solver.c:219-234
+    double dt = dt_bound;
+    const double dx = g->desc.dx, dy = g->desc.dy;
+    if (umax > 0) dt = (dt > dx / umax) ? dx / umax : dt;
+    if (vmax > 0) dt = (dt > dy / vmax) ? dy / vmax : dt;
+    g->nl.prm.dt = dt * tau;
+    if (dt_out) *dt_out = g->nl.prm.dt;
+    return MISOR_OK;
+}
+
+int misor_set_dt(misor_grid* g, double dt) {
+    if (!g) return fail(MISOR_EINVAL, "null grid");
+    g->nl.prm.dt = dt;
+    return MISOR_OK;
+}
+
+int misor_set_boundary_conditions(misor_grid* g) {
+    NEED_NS(g);
+    launch_set_bc(g->nl, g->fld[kU], g->fld[kV]);
+    HIPCHK(hipGetLastError());
+    return MISOR_OK;
+}
+
+int misor_set_special_boundary_condition(misor_grid* g) {
+    NEED_NS(g);
+    launch_special_bc(g->nl, g->fld[kU]);
+    HIPCHK(hipGetLastError());
+    return MISOR_OK;
+}
+
+int misor_compute_fg(misor_grid* g) {
+    NEED_NS(g);
+    launch_compute_fg(g->nl, g->fld[kU], g->fld[kV], g->fld[kF], g->fld[kG]);
+    HIPCHK(hipGetLastError());
+    return MISOR_OK;
+}
+
+int misor_compute_rhs(misor_grid* g) {
+    NEED_NS(g);
+    launch_compute_rhs(g->nl, g->fld[kF], g->fld[kG], g->fld[kRhs]);
+    HIPCHK(hipGetLastError());
+    return MISOR_OK;
+}
+
+int misor_normalize_pressure(misor_grid* g) {
+    NEED_NS(g);
+    double* p = g->fld[g->cur];
+    launch_sum(g->nl, p, g->red_partials);
+    launch_finish_reduce(g->stream, g->red_partials, reduce_blocks(g->loc.ni, g->loc.nj),
+                         kReduceSum, 1, g->red_out);
+    if (g->dist)
+        NCCLCHK(ncclAllReduce(g->red_out, g->red_out, 1, ncclDouble, ncclSum, g->comm,
+                              g->stream));
+    const double cells = (double)(g->desc.imax + 2) * (double)(g->desc.jmax + 2);
+    launch_sub_mean(g->nl, p, g->red_out, cells);
+    HIPCHK(hipGetLastError());
+    return MISOR_OK;
+}
+
+int misor_adapt_uv(misor_grid* g) {
+    NEED_NS(g);
+    launch_adapt_uv(g->nl, g->fld[kF], g->fld[kG], g->fld[g->cur], g->fld[kU], g->fld[kV]);
+    HIPCHK(hipGetLastError());
+    return MISOR_OK;
+}
+
+int misor_enable_timing(misor_grid* g, int on) {
+    if (!g) return fail(MISOR_EINVAL, "null grid");
+    g->timing = on != 0;
+    return MISOR_OK;
+}
+
+int misor_get_stats(const misor_grid* g, misor_stats* out) {
+    if (!g || !out) return fail(MISOR_EINVAL, "null argument");
+    *out = g->stats;
+    return MISOR_OK;
+}
+
+int misor_reset_stats(misor_grid* g) {
+    if (!g) return fail(MISOR_EINVAL, "null grid");
+    g->stats = misor_stats{};
+    return MISOR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,109 @@
+// misor_internal.h -- device layout, grid state and kernel launchers shared by
+// the libmisor translation units.  Not part of the public ABI (include/misor.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdint>
+#include <string>
+
+#include "misor.h"
+
+namespace misor {
+
+// ---------------------------------------------------------------------------
+// HBM layout of every field (p, p', rhs, u, v, f, g)
+//
+// Reference cell (i,j), i in [0, ni+1], j in [0, nj+1] (ghosts included), lives
+// at   base[(j + kYOff) * pitch + (i + kXOff)].
+//  - kXOff = 15 puts the first interior column i = 1 on a 128-byte boundary,
+//    so every wave's 16-byte-per-lane row segment of 128 cells starts a cache
+//    line; the ghost column i = 0 is the last double of the preceding line.
+//  - kYOff = 2 and two spare rows at the top give every sweep block its two
+//    halo rows (j0-2 .. j1+1) without clamping.
+//  - pitch = 32 + round_up(ni, kStripCells * kWavesX): left pad line, the
+//    strips, the right halo pair and pad; a multiple of 16 doubles (128 B).
+// Padding cells are zero and never feed an interior result.
+// ---------------------------------------------------------------------------
+constexpr int kXOff = 15;
+constexpr int kYOff = 2;
+constexpr int kLanes = 64;                 // wavefront
+constexpr int kStripCells = 2 * kLanes;    // 128 columns per wave (2 per lane)
+constexpr int kWavesX = 4;                 // waves per workgroup, side by side
+constexpr int kSweepThreads = kLanes * kWavesX;
+
+inline long long layout_pitch(int ni) {
+    const int w = kStripCells * kWavesX;
+    return 32 + (long long)((ni + w - 1) / w) * w;
+}
+inline long long layout_rows(int nj) { return (long long)nj + 6; }
+
+// Solver state that lives on the device between launches.  Written only by
+// the finish kernel (one workgroup) and read by the next sweep launch.
+struct DevState {
+    int it;        // iterations completed
+    int done;      // 1 once (res >= eps^2 && it < itermax) is false
+    int itermax;   // cap of the current solve call
+    int pad;
+    double res;    // residual of the last iteration
+    double epssq;
+};
+
+struct SweepParams {
+    long long pitch;
+    int ni, nj;          // local interior size
+    int rows_per_block;  // H
+    int parity;          // (ioff + joff) & 1 : global colour of local cell (0,0)
+    int ghost_left, ghost_right, ghost_bottom, ghost_top;  // physical boundary -> Neumann copy
+    double idx2, idy2, coef;  // 1/dx^2, 1/dy^2, factor (RB) or omega*factor (RBA)
+};
+
+struct NsParams {
+    double dx, dy, dt;
+    double xlength, ylength;
+    double re, gx, gy, gamma;
+    int bc_left, bc_right, bc_bottom, bc_top, problem;
+};
+
+// kernel launchers (sor_kernels.hip, ns_kernels.hip)
+void launch_sweep(hipStream_t s, const SweepParams& prm, const double* src, double* dst,
+                  const double* rhs, double* partials, const DevState* st, int nblocks_x,
+                  int nblocks_y);
+void launch_finish(hipStream_t s, const double* partials, int nparts, DevState* st,
+                   double inv_cells);
+int sweep_partials(int ni, int nj, int rows_per_block, int* nbx, int* nby);
+
+void launch_fill(hipStream_t s, double* a, long long count, double v);
+void launch_poisson_init(hipStream_t s, double* p, double* rhs, const double* sx,
+                         const double* sy, const double* rx, int ni, int nj,
+                         long long pitch, int problem);
+
+struct NsLaunch {
+    hipStream_t s;
+    long long pitch;
+    int ni, nj;
+    NsParams prm;
+    // physical-boundary flags (multi-GPU: only edge ranks apply wall BCs)
+    int wall_left, wall_right, wall_bottom, wall_top;
+    int ioff, joff;          // global index of local cell (0,0)
+    int imax_g, jmax_g;      // global interior size
+};
+void launch_set_bc(const NsLaunch& L, double* u, double* v);
+void launch_special_bc(const NsLaunch& L, double* u);
+void launch_compute_fg(const NsLaunch& L, const double* u, const double* v, double* f,
+                       double* g);
+void launch_compute_rhs(const NsLaunch& L, const double* f, const double* g, double* rhs);
+void launch_adapt_uv(const NsLaunch& L, const double* f, const double* g, const double* p,
+                     double* u, double* v);
+// reductions over ALL (ni+2)(nj+2) cells: partial per block, then a finish
+int reduce_blocks(int ni, int nj);
+void launch_absmax2(const NsLaunch& L, const double* u, const double* v, double* partials);
+void launch_sum(const NsLaunch& L, const double* p, double* partials);
+void launch_finish_reduce(hipStream_t s, const double* partials, int n, int op, int width,
+                          double* out);
+// p -= (*sum) / cells over the whole local array (normalizePressure)
+void launch_sub_mean(const NsLaunch& L, double* p, const double* sum, double cells);
+enum { kReduceSum = 0, kReduceMax = 1 };
+
+}  // namespace misor

@@ -1,0 +1,349 @@
+// ns_kernels.hip -- the 2D Navier-Stokes step around the pressure solve,
+// assignment-5/sequential/src/solver.c, on the padded HBM layout of
+// misor_internal.h.  All kernels are HBM-bandwidth bound FP64 stencils or
+// O(perimeter) boundary updates; expression order follows the reference and
+// the file is compiled with -ffp-contract=off, so every per-cell value is
+// bit-identical to the CPU.  Only the two reductions whose result depends on
+// summation order (normalizePressure's mean) differ from the CPU in rounding.
+
+#include "misor_internal.h"
+
+namespace misor {
+
+namespace {
+
+struct Lay {
+    double* a;
+    long long pitch;
+    __device__ __forceinline__ double& operator()(int i, int j) const {
+        return a[(long long)(j + kYOff) * pitch + (i + kXOff)];
+    }
+};
+struct CLay {
+    const double* a;
+    long long pitch;
+    __device__ __forceinline__ double operator()(int i, int j) const {
+        return a[(long long)(j + kYOff) * pitch + (i + kXOff)];
+    }
+};
+
+constexpr int kTx = 64, kTy = 4;
+
+}  // namespace
+
+// ---- setBoundaryConditions, :236-337.  The reference applies left, right,
+// bottom, top in that order and bottom/top read cells that left/right wrote
+// (U(imax,1), ...), so the walls run as two dependent launches:
+// phase 0 = left + right (loop over j), phase 1 = bottom + top (loop over i).
+__global__ void bc_lr_kernel(Lay u, Lay v, int ni, int nj, int bcl, int bcr, int wl, int wr) {
+    const int j = 1 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (j > nj) return;
+    if (wl) {
+        switch (bcl) {
+        case MISOR_NOSLIP: u(0, j) = 0.0; v(0, j) = -v(1, j); break;
+        case MISOR_SLIP: u(0, j) = 0.0; v(0, j) = v(1, j); break;
+        case MISOR_OUTFLOW: u(0, j) = u(1, j); v(0, j) = v(1, j); break;
+        default: break;
+        }
+    }
+    if (wr) {
+        switch (bcr) {
+        case MISOR_NOSLIP: u(ni, j) = 0.0; v(ni + 1, j) = -v(ni, j); break;
+        case MISOR_SLIP: u(ni, j) = 0.0; v(ni + 1, j) = v(ni, j); break;
+        case MISOR_OUTFLOW: u(ni, j) = u(ni - 1, j); v(ni + 1, j) = v(ni, j); break;
+        default: break;
+        }
+    }
+}
+
+__global__ void bc_bt_kernel(Lay u, Lay v, int ni, int nj, int bcb, int bct, int wb, int wt) {
+    const int i = 1 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > ni) return;
+    if (wb) {
+        switch (bcb) {
+        case MISOR_NOSLIP: v(i, 0) = 0.0; u(i, 0) = -u(i, 1); break;
+        case MISOR_SLIP: v(i, 0) = 0.0; u(i, 0) = u(i, 1); break;
+        case MISOR_OUTFLOW: u(i, 0) = u(i, 1); v(i, 0) = v(i, 1); break;
+        default: break;
+        }
+    }
+    if (wt) {
+        switch (bct) {
+        case MISOR_NOSLIP: v(i, nj) = 0.0; u(i, nj + 1) = -u(i, nj); break;
+        case MISOR_SLIP: v(i, nj) = 0.0; u(i, nj + 1) = u(i, nj); break;
+        case MISOR_OUTFLOW: u(i, nj + 1) = u(i, nj); v(i, nj) = v(i, nj - 1); break;
+        default: break;
+        }
+    }
+}
+
+void launch_set_bc(const NsLaunch& L, double* u, double* v) {
+    Lay U{u, L.pitch}, V{v, L.pitch};
+    hipLaunchKernelGGL(bc_lr_kernel, dim3((L.nj + 255) / 256), dim3(256), 0, L.s, U, V, L.ni,
+                       L.nj, L.prm.bc_left, L.prm.bc_right, L.wall_left, L.wall_right);
+    hipLaunchKernelGGL(bc_bt_kernel, dim3((L.ni + 255) / 256), dim3(256), 0, L.s, U, V, L.ni,
+                       L.nj, L.prm.bc_bottom, L.prm.bc_top, L.wall_bottom, L.wall_top);
+}
+
+// ---- setSpecialBoundaryCondition, :339-358
+// dcavity: U(i, jmax+1) = 2 - U(i, jmax) for GLOBAL i = 1 .. imax-1 (not imax)
+// canal:   U(0, j) = y (ylength - y) 4 / ylength^2,  y = dy (j - 1/2)
+__global__ void special_bc_kernel(Lay u, int ni, int nj, int problem, int wt, int wl, int ioff,
+                                  int joff, int imax_global, double dy, double ylength) {
+    const int k = 1 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (problem == MISOR_PROBLEM_DCAVITY) {
+        if (wt && k <= ni && ioff + k < imax_global) u(k, nj + 1) = 2.0 - u(k, nj);
+    } else if (problem == MISOR_PROBLEM_CANAL) {
+        if (wl && k <= nj) {
+            const int jg = joff + k;
+            const double y = dy * (jg - 0.5);
+            u(0, k) = y * (ylength - y) * 4.0 / (ylength * ylength);
+        }
+    }
+}
+
+void launch_special_bc(const NsLaunch& L, double* u) {
+    const int n = L.ni > L.nj ? L.ni : L.nj;
+    hipLaunchKernelGGL(special_bc_kernel, dim3((n + 255) / 256), dim3(256), 0, L.s,
+                       Lay{u, L.pitch}, L.ni, L.nj, L.prm.problem, L.wall_top, L.wall_left,
+                       L.ioff, L.joff, L.imax_g, L.prm.dy, L.prm.ylength);
+}
+
+// ---- computeFG, :360-436 (+ its F/G boundary lines :426-435 on wall ranks)
+__global__ __launch_bounds__(kTx* kTy) void fg_kernel(CLay u, CLay v, Lay f, Lay g, int ni,
+                                                      int nj, double dt, double inverseRe,
+                                                      double inverseDx, double inverseDy,
+                                                      double gamma, double gx, double gy,
+                                                      int wl, int wr, int wb, int wt) {
+    const int i = 1 + blockIdx.x * kTx + threadIdx.x;
+    const int j = 1 + blockIdx.y * kTy + threadIdx.y;
+    if (i > ni || j > nj) return;
+
+    const double uc = u(i, j), ue = u(i + 1, j), uw = u(i - 1, j);
+    const double un = u(i, j + 1), us = u(i, j - 1), unw = u(i - 1, j + 1);
+    const double vc = v(i, j), ve = v(i + 1, j), vw = v(i - 1, j);
+    const double vn = v(i, j + 1), vs = v(i, j - 1), vse = v(i + 1, j - 1);
+
+    const double du2dx = inverseDx * 0.25 * ((uc + ue) * (uc + ue) - (uc + uw) * (uc + uw)) +
+                         gamma * inverseDx * 0.25 *
+                             (fabs(uc + ue) * (uc - ue) + fabs(uc + uw) * (uc - uw));
+    const double duvdy = inverseDy * 0.25 * ((vc + ve) * (uc + un) - (vs + vse) * (uc + us)) +
+                         gamma * inverseDy * 0.25 *
+                             (fabs(vc + ve) * (uc - un) + fabs(vs + vse) * (uc - us));
+    const double du2dx2 = inverseDx * inverseDx * (ue - 2.0 * uc + uw);
+    const double du2dy2 = inverseDy * inverseDy * (un - 2.0 * uc + us);
+    double fv = uc + dt * (inverseRe * (du2dx2 + du2dy2) - du2dx - duvdy + gx);
+
+    const double duvdx = inverseDx * 0.25 * ((uc + un) * (vc + ve) - (uw + unw) * (vc + vw)) +
+                         gamma * inverseDx * 0.25 *
+                             (fabs(uc + un) * (vc - ve) + fabs(uw + unw) * (vc - vw));
+    const double dv2dy = inverseDy * 0.25 * ((vc + vn) * (vc + vn) - (vc + vs) * (vc + vs)) +
+                         gamma * inverseDy * 0.25 *
+                             (fabs(vc + vn) * (vc - vn) + fabs(vc + vs) * (vc - vs));
+    const double dv2dx2 = inverseDx * inverseDx * (ve - 2.0 * vc + vw);
+    const double dv2dy2 = inverseDy * inverseDy * (vn - 2.0 * vc + vs);
+    double gv = vc + dt * (inverseRe * (dv2dx2 + dv2dy2) - duvdx - dv2dy + gy);
+
+    // boundary of F / G (:426-435) overrides the interior value at i = imax / j = jmax
+    if (wr && i == ni) fv = uc;
+    if (wt && j == nj) gv = vc;
+    f(i, j) = fv;
+    g(i, j) = gv;
+    if (wl && i == 1) f(0, j) = uw;
+    if (wb && j == 1) g(i, 0) = vs;
+}
+
+void launch_compute_fg(const NsLaunch& L, const double* u, const double* v, double* f,
+                       double* g) {
+    dim3 grid((L.ni + kTx - 1) / kTx, (L.nj + kTy - 1) / kTy);
+    const NsParams& P = L.prm;
+    hipLaunchKernelGGL(fg_kernel, grid, dim3(kTx, kTy), 0, L.s, CLay{u, L.pitch},
+                       CLay{v, L.pitch}, Lay{f, L.pitch}, Lay{g, L.pitch}, L.ni, L.nj, P.dt,
+                       1.0 / P.re, 1.0 / P.dx, 1.0 / P.dy, P.gamma, P.gx, P.gy, L.wall_left,
+                       L.wall_right, L.wall_bottom, L.wall_top);
+}
+
+// ---- computeRHS, :122-138
+__global__ void rhs_kernel(CLay f, CLay g, Lay rhs, int ni, int nj, double idx, double idy,
+                           double idt) {
+    const int i = 1 + blockIdx.x * kTx + threadIdx.x;
+    const int j = 1 + blockIdx.y * kTy + threadIdx.y;
+    if (i > ni || j > nj) return;
+    rhs(i, j) = idt * ((f(i, j) - f(i - 1, j)) * idx + (g(i, j) - g(i, j - 1)) * idy);
+}
+
+void launch_compute_rhs(const NsLaunch& L, const double* f, const double* g, double* rhs) {
+    dim3 grid((L.ni + kTx - 1) / kTx, (L.nj + kTy - 1) / kTy);
+    hipLaunchKernelGGL(rhs_kernel, grid, dim3(kTx, kTy), 0, L.s, CLay{f, L.pitch},
+                       CLay{g, L.pitch}, Lay{rhs, L.pitch}, L.ni, L.nj, 1.0 / L.prm.dx,
+                       1.0 / L.prm.dy, 1.0 / L.prm.dt);
+}
+
+// ---- adaptUV, :438-455
+__global__ void adapt_kernel(CLay f, CLay g, CLay p, Lay u, Lay v, int ni, int nj, double fx,
+                             double fy) {
+    const int i = 1 + blockIdx.x * kTx + threadIdx.x;
+    const int j = 1 + blockIdx.y * kTy + threadIdx.y;
+    if (i > ni || j > nj) return;
+    const double pc = p(i, j);
+    u(i, j) = f(i, j) - (p(i + 1, j) - pc) * fx;
+    v(i, j) = g(i, j) - (p(i, j + 1) - pc) * fy;
+}
+
+void launch_adapt_uv(const NsLaunch& L, const double* f, const double* g, const double* p,
+                     double* u, double* v) {
+    dim3 grid((L.ni + kTx - 1) / kTx, (L.nj + kTy - 1) / kTy);
+    hipLaunchKernelGGL(adapt_kernel, grid, dim3(kTx, kTy), 0, L.s, CLay{f, L.pitch},
+                       CLay{g, L.pitch}, CLay{p, L.pitch}, Lay{u, L.pitch}, Lay{v, L.pitch},
+                       L.ni, L.nj, L.prm.dt / L.prm.dx, L.prm.dt / L.prm.dy);
+}
+
+// ---- reductions over the cells the reference visits (all (imax+2)(jmax+2),
+// ghosts included).  On a decomposed grid a rank covers its interior plus the
+// ghost rows/columns that lie on the physical boundary, so every global cell is
+// visited exactly once.  Block partials, then one fixed-order finish.
+constexpr int kRedBlocks = 1024;
+constexpr int kRedThreads = 256;
+
+int reduce_blocks(int ni, int nj) {
+    long long cells = (long long)(ni + 2) * (nj + 2);
+    long long b = (cells + kRedThreads - 1) / kRedThreads;
+    return (int)(b < kRedBlocks ? (b < 1 ? 1 : b) : kRedBlocks);
+}
+
+namespace {
+__device__ __forceinline__ double wsum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ double wmax(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double w = __shfl_xor(v, o, 64);
+        v = (v > w) ? v : w;
+    }
+    return v;
+}
+struct Region {
+    int ilo, jlo, w, h;  // first cell and extent
+};
+__host__ Region region_of(const NsLaunch& L) {
+    Region R;
+    R.ilo = L.wall_left ? 0 : 1;
+    R.jlo = L.wall_bottom ? 0 : 1;
+    R.w = (L.wall_right ? L.ni + 1 : L.ni) - R.ilo + 1;
+    R.h = (L.wall_top ? L.nj + 1 : L.nj) - R.jlo + 1;
+    return R;
+}
+}  // namespace
+
+// maxElement (:193-202) for u and v at once: max |x| seeded with DBL_MIN
+__global__ __launch_bounds__(kRedThreads) void absmax2_kernel(CLay u, CLay v, Region R,
+                                                              double* partials) {
+    __shared__ double su[kRedThreads / 64], sv[kRedThreads / 64];
+    double mu = 2.2250738585072014e-308, mv = 2.2250738585072014e-308;  // DBL_MIN
+    const long long n = (long long)R.w * R.h;
+    for (long long k = (long long)blockIdx.x * kRedThreads + threadIdx.x; k < n;
+         k += (long long)gridDim.x * kRedThreads) {
+        const int i = R.ilo + (int)(k % R.w), j = R.jlo + (int)(k / R.w);
+        const double a = fabs(u(i, j)), b = fabs(v(i, j));
+        mu = (mu > a) ? mu : a;
+        mv = (mv > b) ? mv : b;
+    }
+    mu = wmax(mu);
+    mv = wmax(mv);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) { su[w] = mu; sv[w] = mv; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < kRedThreads / 64; ++k) {
+            mu = (mu > su[k]) ? mu : su[k];
+            mv = (mv > sv[k]) ? mv : sv[k];
+        }
+        mu = (su[0] > mu) ? su[0] : mu;
+        mv = (sv[0] > mv) ? sv[0] : mv;
+        partials[2 * blockIdx.x] = mu;
+        partials[2 * blockIdx.x + 1] = mv;
+    }
+}
+
+void launch_absmax2(const NsLaunch& L, const double* u, const double* v, double* partials) {
+    hipLaunchKernelGGL(absmax2_kernel, dim3(reduce_blocks(L.ni, L.nj)), dim3(kRedThreads), 0,
+                       L.s, CLay{u, L.pitch}, CLay{v, L.pitch}, region_of(L), partials);
+}
+
+__global__ __launch_bounds__(kRedThreads) void sum_kernel(CLay p, Region R, double* partials) {
+    __shared__ double sp[kRedThreads / 64];
+    double s = 0.0;
+    const long long n = (long long)R.w * R.h;
+    for (long long k = (long long)blockIdx.x * kRedThreads + threadIdx.x; k < n;
+         k += (long long)gridDim.x * kRedThreads) {
+        const int i = R.ilo + (int)(k % R.w), j = R.jlo + (int)(k / R.w);
+        s += p(i, j);
+    }
+    s = wsum(s);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) sp[w] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int k = 0; k < kRedThreads / 64; ++k) t += sp[k];
+        partials[blockIdx.x] = t;
+    }
+}
+
+void launch_sum(const NsLaunch& L, const double* p, double* partials) {
+    hipLaunchKernelGGL(sum_kernel, dim3(reduce_blocks(L.ni, L.nj)), dim3(kRedThreads), 0, L.s,
+                       CLay{p, L.pitch}, region_of(L), partials);
+}
+
+// fixed-order combination of `n` partial records of `width` doubles
+__global__ __launch_bounds__(256) void finish_reduce_kernel(const double* partials, int n,
+                                                            int op, int width, double* out) {
+    __shared__ double sh[2][256];
+    const int t = threadIdx.x;
+    for (int c = 0; c < width; ++c) {
+        double acc = (op == kReduceSum) ? 0.0 : 2.2250738585072014e-308;
+        for (int k = t; k < n; k += 256) {
+            const double x = partials[(long long)k * width + c];
+            acc = (op == kReduceSum) ? acc + x : ((acc > x) ? acc : x);
+        }
+        sh[c][t] = acc;
+    }
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (t < s) {
+            for (int c = 0; c < width; ++c) {
+                const double a = sh[c][t], b = sh[c][t + s];
+                sh[c][t] = (op == kReduceSum) ? a + b : ((a > b) ? a : b);
+            }
+        }
+        __syncthreads();
+    }
+    if (t < width) out[t] = sh[t][0];
+}
+
+void launch_finish_reduce(hipStream_t s, const double* partials, int n, int op, int width,
+                          double* out) {
+    hipLaunchKernelGGL(finish_reduce_kernel, dim3(1), dim3(256), 0, s, partials, n, op, width,
+                       out);
+}
+
+// normalizePressure's second loop (:214-216): p -= avg over every cell
+__global__ void sub_mean_kernel(Lay p, int ni, int nj, const double* sum, double cells) {
+    const double avg = (*sum) / cells;
+    const long long n = (long long)(ni + 2) * (nj + 2);
+    for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n;
+         k += (long long)gridDim.x * blockDim.x) {
+        const int i = (int)(k % (ni + 2)), j = (int)(k / (ni + 2));
+        p(i, j) = p(i, j) - avg;
+    }
+}
+
+void launch_sub_mean(const NsLaunch& L, double* p, const double* sum, double cells) {
+    hipLaunchKernelGGL(sub_mean_kernel, dim3(reduce_blocks(L.ni, L.nj)), dim3(256), 0, L.s,
+                       Lay{p, L.pitch}, L.ni, L.nj, sum, cells);
+}
+
+}  // namespace misor

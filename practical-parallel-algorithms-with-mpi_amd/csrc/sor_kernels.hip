@@ -1,0 +1,352 @@
+// sor_kernels.hip -- fused red-black SOR sweep for gfx950 (MI355X).
+//
+// One launch = one full red+black iteration of solveRB
+// (assignment-4/src/solver.c:197-229): both colour passes, the residual
+// sum r^2 of both colours, and the Neumann ghost copy of :219-227, reading p
+// from `src` and writing the new p to `dst` (ping-pong buffers).
+//
+// Why fused: two half-sweep kernels on the natural layout touch every cache
+// line of p and rhs twice per iteration (~48 B per lattice update); this kernel
+// reads p and rhs once and writes p once: 24 B/LUP, the algorithmic minimum.
+//
+// Work decomposition
+//   wave      = one strip of 128 columns (lane l owns columns ia=c0+2l, ia+1;
+//               one 16-byte load per lane per row = one 1 KiB wave access)
+//   workgroup = 4 strips side by side x H rows (blockIdx.y)
+// Each wave marches up its H rows keeping a 3-row window in registers:
+//   step r: red update of row r   (needs old rows r-1, r, r+1)
+//           black update of row r-1 (needs the new red values of rows r-2..r)
+//           store row r-1 once.
+// The red values one column left/right of the strip (needed by the strip's
+// edge black cells) and one row below/above the block are recomputed
+// redundantly from the same old values, so they are bit-identical to the
+// values the owning wave computes.  Nothing is exchanged between waves or
+// workgroups inside a launch.
+//
+// Bit-exactness: the update and residual use the reference expression order
+// ((P(i+1)-2P)+P(i-1))*idx2 + ((P(j+1)-2P)+P(j-1))*idy2 with no FMA
+// contraction (-ffp-contract=off), so every cell value equals the CPU's
+// bit for bit.  Only the order in which r^2 is summed differs (deterministic:
+// fixed lane tree, fixed wave order, fixed block order in the finish kernel).
+//
+// Colour: cell (i,j) is red iff (i+j) is even in GLOBAL indices (pass 0 of
+// solveRB starts at i=1 on j=1); `parity` carries the offset of this rank's
+// block so decomposed runs colour identically.
+
+#include "misor_internal.h"
+
+namespace misor {
+
+namespace {
+
+__device__ __forceinline__ double2 ld2(const double* p) {
+    return *reinterpret_cast<const double2*>(p);
+}
+__device__ __forceinline__ void st2(double* p, double2 v) {
+    *reinterpret_cast<double2*>(p) = v;
+}
+// lane l receives lane l-1's value (lane 0: its own, overridden by callers)
+__device__ __forceinline__ double from_left(double v) { return __shfl_up(v, 1, 64); }
+// lane l receives lane l+1's value (lane 63: its own, overridden by callers)
+__device__ __forceinline__ double from_right(double v) { return __shfl_down(v, 1, 64); }
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(kSweepThreads) void rb_sweep_kernel(
+    SweepParams prm, const double* __restrict__ src, double* __restrict__ dst,
+    const double* __restrict__ rhs, double* __restrict__ partials,
+    const DevState* __restrict__ st) {
+    __shared__ double wsum[kWavesX];
+    if (st->done) return;  // converged or capped: the whole grid exits
+
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int strip = blockIdx.x * kWavesX + wave;
+    const int ni = prm.ni, nj = prm.nj;
+    const int c0 = 1 + strip * kStripCells;
+    const int ia = c0 + 2 * lane;  // odd local column
+    const int ib = ia + 1;
+    const long long pitch = prm.pitch;
+    const double idx2 = prm.idx2, idy2 = prm.idy2, coef = prm.coef;
+
+    const bool hl = (lane == 0);   // holds the left halo pair  (c0-2, c0-1)
+    const bool hr = (lane == 63);  // holds the right halo pair (c0+128, c0+129)
+    const bool in_a = ia <= ni;
+    const bool in_b = ib <= ni;
+    const int hcol = hl ? c0 - 1 : c0 + kStripCells;  // halo column that can be red
+    const bool in_h = (hcol >= 1) && (hcol <= ni);
+    const int hoff = hl ? -2 : 2;  // halo pair address relative to ia (lanes 0 / 63)
+
+    double acc = 0.0;
+
+    // physical corners are never touched by solveRB; carry them into dst
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 4) {
+        const int t = threadIdx.x;
+        const int ci = (t & 1) ? ni + 1 : 0, cj = (t & 2) ? nj + 1 : 0;
+        const bool phys = ((t & 1) ? prm.ghost_right : prm.ghost_left) &&
+                          ((t & 2) ? prm.ghost_top : prm.ghost_bottom);
+        if (phys) {
+            const long long k = (long long)(cj + kYOff) * pitch + (ci + kXOff);
+            dst[k] = src[k];
+        }
+    }
+
+    if (c0 <= ni) {  // wave-uniform: strips past the domain only join the reduction
+        const int j0 = 1 + (int)blockIdx.y * prm.rows_per_block;
+        const int j1 = min(j0 + prm.rows_per_block, nj + 1);
+
+        // element (ia, j) of the three arrays: base + j*pitch
+        const double* sp = src + (long long)kYOff * pitch + kXOff + ia;
+        const double* rp = rhs + (long long)kYOff * pitch + kXOff + ia;
+        double* dp = dst + (long long)kYOff * pitch + kXOff + ia;
+
+        auto ldp = [&](int j) { return ld2(sp + (long long)j * pitch); };
+        auto ldr = [&](int j) { return ld2(rp + (long long)j * pitch); };
+        auto ldph = [&](int j) {
+            double2 v = make_double2(0.0, 0.0);
+            if (hl | hr) v = ld2(sp + (long long)j * pitch + hoff);
+            return v;
+        };
+        auto ldrh = [&](int j) {
+            double2 v = make_double2(0.0, 0.0);
+            if (hl | hr) v = ld2(rp + (long long)j * pitch + hoff);
+            return v;
+        };
+
+        // window: Mm2 = M(r-2), Mm1 = M(r-1) (red new, black old), Oc = O(r),
+        // Up = O(r+1), Nx = O(r+2) in flight; H* = halo pairs; R* = rhs.
+        double2 Mm1 = ldp(j0 - 2), Hm1 = ldph(j0 - 2);
+        double2 Oc = ldp(j0 - 1), Hc = ldph(j0 - 1);
+        double2 Up = ldp(j0), Hup = ldph(j0);
+        double2 Rc = ldr(j0 - 1), RHc = ldrh(j0 - 1);
+        double2 Mm2 = make_double2(0.0, 0.0), Rm1 = make_double2(0.0, 0.0);
+        double HRm1 = 0.0;
+
+        for (int r = j0 - 1; r <= j1; ++r) {
+            // prefetch two rows ahead (p) / one row ahead (rhs)
+            const double2 Nx = ldp(r + 2), HNx = ldph(r + 2);
+            const double2 RNx = ldr(r + 1), RHNx = ldrh(r + 1);
+
+            // ---------------- red pass on row r ----------------
+            const int q = (prm.parity + 1 + r) & 1;  // 0: column ia red, 1: column ib red
+            double2 Mr = Oc;
+            double HRc = hl ? Hc.y : Hc.x;  // halo-column value after the red pass
+            if (r >= 1 && r <= nj) {
+                const bool own = (r >= j0) && (r < j1);
+                if (q == 0) {
+                    // (ia, r) red; left neighbour from lane l-1 (lane 0: halo)
+                    double L = from_left(Oc.y);
+                    if (hl) L = Hc.y;
+                    const double c = Oc.x;
+                    const double rr = Rc.x - (((Oc.y - 2.0 * c) + L) * idx2 +
+                                              ((Up.x - 2.0 * c) + Mm1.x) * idy2);
+                    if (in_a) {
+                        Mr.x = c - coef * rr;
+                        if (own) acc += rr * rr;
+                    }
+                    // right halo column c0+128 is red too (same parity as ia)
+                    if (hr && in_h) {
+                        const double ch = Hc.x;
+                        const double rh = RHc.x - (((Hc.y - 2.0 * ch) + Oc.y) * idx2 +
+                                                   ((Hup.x - 2.0 * ch) + Hm1.x) * idy2);
+                        HRc = ch - coef * rh;
+                    }
+                } else {
+                    // (ib, r) red; right neighbour from lane l+1 (lane 63: halo)
+                    double R = from_right(Oc.x);
+                    if (hr) R = Hc.x;
+                    const double c = Oc.y;
+                    const double rr = Rc.y - (((R - 2.0 * c) + Oc.x) * idx2 +
+                                              ((Up.y - 2.0 * c) + Mm1.y) * idy2);
+                    if (in_b) {
+                        Mr.y = c - coef * rr;
+                        if (own) acc += rr * rr;
+                    }
+                    // left halo column c0-1 is red (same parity as ib)
+                    if (hl && in_h) {
+                        const double ch = Hc.y;
+                        const double rh = RHc.y - (((Oc.x - 2.0 * ch) + Hc.x) * idx2 +
+                                                   ((Hup.y - 2.0 * ch) + Hm1.y) * idy2);
+                        HRc = ch - coef * rh;
+                    }
+                }
+            }
+
+            // ---------------- black pass on row r-1, then store ----------------
+            const int jw = r - 1;
+            if (jw >= j0) {  // implies 1 <= jw <= nj
+                double2 F = Mm1;
+                if (q == 0) {
+                    // row r-1 has q' = 1: column ia black, its right neighbour ib red
+                    double Ln = from_left(Mm1.y);
+                    if (hl) Ln = HRm1;
+                    const double c = Mm1.x;
+                    const double rr = Rm1.x - (((Mm1.y - 2.0 * c) + Ln) * idx2 +
+                                               ((Mr.x - 2.0 * c) + Mm2.x) * idy2);
+                    if (in_a) {
+                        F.x = c - coef * rr;
+                        acc += rr * rr;
+                    }
+                } else {
+                    // row r-1 has q' = 0: column ib black
+                    double Rn = from_right(Mm1.x);
+                    if (hr) Rn = HRm1;
+                    const double c = Mm1.y;
+                    const double rr = Rm1.y - (((Rn - 2.0 * c) + Mm1.x) * idx2 +
+                                               ((Mr.y - 2.0 * c) + Mm2.y) * idy2);
+                    if (in_b) {
+                        F.y = c - coef * rr;
+                        acc += rr * rr;
+                    }
+                }
+
+                // Neumann ghost copy (assignment-4/src/solver.c:219-227), fused:
+                // columns 0 / ni+1 of this row, rows 0 / nj+1 from rows 1 / nj.
+                double2 out = F;
+                if (prm.ghost_right) {
+                    const double fb_left = from_left(F.y);  // final value at column ia-1
+                    if (ia == ni + 1) out.x = fb_left;
+                    if (ib == ni + 1) out.y = F.x;
+                }
+                double* drow = dp + (long long)jw * pitch;
+                st2(drow, out);
+                if (prm.ghost_left && strip == 0 && hl)  // (pad, P(0,jw) = P(1,jw))
+                    st2(drow - 2, make_double2(Hm1.x, F.x));
+                if (prm.ghost_right && hr && c0 + kStripCells == ni + 1)
+                    st2(drow + 2, make_double2(F.y, Hm1.y));  // (P(ni+1)=P(ni), pad)
+                if (prm.ghost_bottom && jw == 1) {
+                    // row 0 <- row 1 for 1 <= i <= ni; corners keep their old value
+                    const double2 o0 = Mm2;  // = old row 0 (ghost rows are never updated)
+                    st2(dp, make_double2(in_a ? F.x : o0.x, in_b ? F.y : o0.y));
+                }
+                if (prm.ghost_top && jw == nj) {
+                    const double2 on = Mr;  // = old row nj+1
+                    st2(drow + pitch, make_double2(in_a ? F.x : on.x, in_b ? F.y : on.y));
+                }
+            }
+
+            // rotate the window
+            Mm2 = Mm1;
+            Mm1 = Mr;
+            Oc = Up;
+            Up = Nx;
+            Hm1 = Hc;
+            Hc = Hup;
+            Hup = HNx;
+            Rm1 = Rc;
+            Rc = RNx;
+            RHc = RHNx;
+            HRm1 = HRc;
+        }
+    }
+
+    // deterministic reduction: lane tree, then waves 0..3 in order
+    acc = wave_sum(acc);
+    if (lane == 0) wsum[wave] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double s = 0.0;
+#pragma unroll
+        for (int w = 0; w < kWavesX; ++w) s += wsum[w];
+        partials[(long long)blockIdx.y * gridDim.x + blockIdx.x] = s;
+    }
+}
+
+// Sum of the per-block partials in a fixed order, then the loop test of
+// solveRB (assignment-4/src/solver.c:197,229,233):
+//   res = sum / (imax*jmax); it++; continue while res >= eps^2 && it < itermax
+__global__ __launch_bounds__(1024) void rb_finish_kernel(const double* __restrict__ partials,
+                                                         int n, DevState* st,
+                                                         double cells) {
+    __shared__ double sh[1024];
+    if (st->done) return;
+    const int t = threadIdx.x;
+    double s = 0.0;
+    for (int k = t; k < n; k += 1024) s += partials[k];
+    sh[t] = s;
+    __syncthreads();
+#pragma unroll
+    for (int w = 512; w >= 64; w >>= 1) {
+        if (t < w) sh[t] += sh[t + w];
+        __syncthreads();
+    }
+    if (t < 64) {
+        double v = sh[t];
+        v = wave_sum(v);
+        if (t == 0) {
+            const double res = v / cells;
+            const int it = st->it + 1;
+            st->res = res;
+            st->it = it;
+            st->done = !((res >= st->epssq) && (it < st->itermax));
+        }
+    }
+}
+
+int sweep_partials(int ni, int nj, int rows_per_block, int* nbx, int* nby) {
+    const int strips = (ni + kStripCells - 1) / kStripCells;
+    *nbx = (strips + kWavesX - 1) / kWavesX;
+    *nby = (nj + rows_per_block - 1) / rows_per_block;
+    return (*nbx) * (*nby);
+}
+
+void launch_sweep(hipStream_t s, const SweepParams& prm, const double* src, double* dst,
+                  const double* rhs, double* partials, const DevState* st, int nbx,
+                  int nby) {
+    hipLaunchKernelGGL(rb_sweep_kernel, dim3(nbx, nby), dim3(kSweepThreads), 0, s, prm, src,
+                       dst, rhs, partials, st);
+}
+
+void launch_finish(hipStream_t s, const double* partials, int nparts, DevState* st,
+                   double cells) {
+    hipLaunchKernelGGL(rb_finish_kernel, dim3(1), dim3(1024), 0, s, partials, nparts, st, cells);
+}
+
+// ---------------------------------------------------------------------------
+// Field initialisation
+// ---------------------------------------------------------------------------
+
+__global__ void fill_kernel(double* a, long long n, double v) {
+    long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (; k < n; k += stride) a[k] = v;
+}
+
+void launch_fill(hipStream_t s, double* a, long long n, double v) {
+    long long blocks = (n + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(fill_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, n, v);
+}
+
+// assignment-4/src/solver.c:105-123: P(i,j) = sin(4 pi i dx) + sin(4 pi j dy),
+// RHS(i,j) = sin(2 pi i dx) (problem 2) else 0, for all cells incl. ghosts.
+// The sines come from host tables evaluated with libm exactly as the
+// reference evaluates them; the sum of two doubles is correctly rounded on
+// both sides, so the device field is bit-identical to the CPU's.
+__global__ void poisson_init_kernel(double* p, double* rhs, const double* sx, const double* sy,
+                                    const double* rx, int ni, int nj, long long pitch,
+                                    int problem) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int j = blockIdx.y;
+    if (i > ni + 1 || j > nj + 1) return;
+    const long long k = (long long)(j + kYOff) * pitch + (i + kXOff);
+    p[k] = sx[i] + sy[j];
+    rhs[k] = (problem == 2) ? rx[i] : 0.0;
+}
+
+void launch_poisson_init(hipStream_t s, double* p, double* rhs, const double* sx,
+                         const double* sy, const double* rx, int ni, int nj, long long pitch,
+                         int problem) {
+    dim3 grid((ni + 2 + 255) / 256, nj + 2);
+    hipLaunchKernelGGL(poisson_init_kernel, grid, dim3(256), 0, s, p, rhs, sx, sy, rx, ni, nj,
+                       pitch, problem);
+}
+
+}  // namespace misor

@@ -1,0 +1,118 @@
+/*
+ * solver_poisson.c -- assignment-4's solver entry points (src/solver.c) as
+ * wrappers over libmisor.  Behaviour kept from the reference:
+ *   initSolver  : dx = xlength/imax, dy = ylength/jmax, p/rhs initial fields
+ *                 (problem 2: rhs = sin(2 pi x)), solver.c:83-124
+ *   solveRB     : red-black SOR until res < eps^2 or itermax, prints "%d "
+ *                 (the iteration count), solver.c:179-238
+ *   solveRBA    : the omega-outside variant, solver.c:240-299
+ *   solve       : the reference's lexicographic SOR has no data-parallel form;
+ *                 on the GPU it runs solveRB (red-black ordering)
+ *   writeResult : "%f " for every cell incl. ghosts, '\n' per row, solver.c:301-323
+ */
+#include "solver_poisson.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "util.h"
+
+void initSolver(Solver* solver, Parameter* params, int problem)
+{
+    solver->imax = params->imax;
+    solver->jmax = params->jmax;
+    solver->dx = params->xlength / params->imax;
+    solver->dy = params->ylength / params->jmax;
+    solver->eps = params->eps;
+    solver->omega = params->omg;
+    solver->itermax = params->itermax;
+    solver->rank = 0;
+    solver->size = 1;
+    solver->jmaxLocal = solver->jmax;
+    solver->ys = 0.0;
+    solver->p = NULL;
+    solver->rhs = NULL;
+
+    misor_desc d = { 0 };
+    d.imax = solver->imax;
+    d.jmax = solver->jmax;
+    d.dx = solver->dx;
+    d.dy = solver->dy;
+    d.omega = solver->omega;
+    d.eps = solver->eps;
+    d.itermax = solver->itermax;
+    d.variant = MISOR_SOLVE_RB;
+    d.device = -1;
+    d.nranks = 1;
+    misorCheck(misor_create(&solver->dev, &d), "misor_create");
+    misorCheck(misor_poisson_init(solver->dev, params->xlength, params->ylength, problem),
+               "misor_poisson_init");
+}
+
+static void run(Solver* solver, int variant)
+{
+    int it = 0;
+    double res = 0.0;
+    (void)variant;
+    misorCheck(misor_solve_rb(solver->dev, &it, &res), "misor_solve_rb");
+    printf("%d ", it);
+}
+
+void solveRB(Solver* solver) { run(solver, MISOR_SOLVE_RB); }
+
+void solve(Solver* solver) { run(solver, MISOR_SOLVE_RB); }
+
+void solveRBA(Solver* solver)
+{
+    /* the update form is a property of the device grid: rebuild it as RBA,
+     * carrying the current p and rhs over */
+    size_t n = (size_t)(solver->imax + 2) * (size_t)(solver->jmax + 2);
+    double* p = allocate(64, n * sizeof(double));
+    double* rhs = allocate(64, n * sizeof(double));
+    misorCheck(misor_download(solver->dev, MISOR_P, p), "misor_download");
+    misorCheck(misor_download(solver->dev, MISOR_RHS, rhs), "misor_download");
+    misor_destroy(solver->dev);
+    misor_desc d = { 0 };
+    d.imax = solver->imax;
+    d.jmax = solver->jmax;
+    d.dx = solver->dx;
+    d.dy = solver->dy;
+    d.omega = solver->omega;
+    d.eps = solver->eps;
+    d.itermax = solver->itermax;
+    d.variant = MISOR_SOLVE_RBA;
+    d.device = -1;
+    d.nranks = 1;
+    misorCheck(misor_create(&solver->dev, &d), "misor_create");
+    misorCheck(misor_upload(solver->dev, MISOR_P, p), "misor_upload");
+    misorCheck(misor_upload(solver->dev, MISOR_RHS, rhs), "misor_upload");
+    free(p);
+    free(rhs);
+    run(solver, MISOR_SOLVE_RBA);
+}
+
+void getResult(Solver* solver)
+{
+    size_t n = (size_t)(solver->imax + 2) * (size_t)(solver->jmax + 2);
+    if (!solver->p) solver->p = allocate(64, n * sizeof(double));
+    misorCheck(misor_download(solver->dev, MISOR_P, solver->p), "misor_download");
+}
+
+void writeResult(Solver* solver, char* filename)
+{
+    int imax = solver->imax;
+    int jmax = solver->jmax;
+    getResult(solver);
+    double* p = solver->p;
+
+    FILE* fp = fopen(filename, "w");
+    if (fp == NULL) {
+        printf("Error!\n");
+        exit(EXIT_FAILURE);
+    }
+    for (int j = 0; j < jmax + 2; j++) {
+        for (int i = 0; i < imax + 2; i++) fprintf(fp, "%f ", p[(size_t)j * (imax + 2) + i]);
+        fprintf(fp, "\n");
+    }
+    fclose(fp);
+}

@@ -1,0 +1,152 @@
+"""Parity of the HIP red-black SOR (libmisor, through its C ABI) with the
+reference's solveRB (assignment-4/src/solver.c:179-238).
+
+Bar: bit-exact p (the per-cell arithmetic follows the reference expression
+order with no FMA contraction) and identical iteration counts.  Only the
+residual's summation order differs, so res is compared with rel 1e-12.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import orc
+import pymisor as M
+
+pytestmark = pytest.mark.gpu
+
+OMEGA, EPS = 1.9, 1e-6
+
+
+def make_grid(ni, nj, xl=1.0, yl=1.0, omega=OMEGA, eps=EPS, itermax=1000000,
+              variant=M.SOLVE_RB):
+    return M.Grid(ni, nj, xl / ni, yl / nj, omega, eps, itermax, variant=variant)
+
+
+def test_poisson_init_bitwise():
+    for (ni, nj, xl, yl) in ((100, 100, 1.0, 1.0), (37, 23, 1.0, 2.0), (700, 5, 3.0, 0.5)):
+        with make_grid(ni, nj, xl, yl) as g:
+            g.poisson_init(xl, yl, 2)
+            p, rhs = orc.poisson_init(ni, nj, xl, yl, 2)
+            assert np.array_equal(g.download(M.P), p)
+            assert np.array_equal(g.download(M.RHS), rhs)
+            g.poisson_init(xl, yl, 1)
+            assert not g.download(M.RHS).any()
+
+
+def test_sweep_fixtures(golden):
+    z = np.load(os.path.join(golden, "rb_sweeps.npz"))
+    for key in z.files:
+        if not key.startswith("geom_"):
+            continue
+        ni, nj, xl, yl = z[key]
+        ni, nj = int(ni), int(nj)
+        for k in (1, 2, 7):
+            with make_grid(ni, nj, xl, yl, eps=1e-300) as g:
+                g.poisson_init(xl, yl, 2)
+                it, res = g.solve_rb(itermax=k)
+                assert it == k
+                got = g.download(M.P)
+                want = z["p_%dx%d_k%d" % (ni, nj, k)]
+                assert np.array_equal(got, want), (ni, nj, k, np.abs(got - want).max())
+
+
+def test_poisson_par_converges_like_reference(golden):
+    z = np.load(os.path.join(golden, "rb_poisson100.npz"))
+    with make_grid(100, 100) as g:
+        g.poisson_init(1.0, 1.0, 2)
+        it, res = g.solve_rb()
+        assert it == int(z["iterations"]) == 2388
+        assert np.array_equal(g.download(M.P), z["p"])
+        assert res < EPS * EPS
+
+
+def test_iteration_kats(golden):
+    kat = json.load(open(os.path.join(golden, "rb_kat.json")))["iterations"]
+    for key, want in kat.items():
+        if "x" in key:
+            ni, nj = map(int, key.split("x"))
+        else:
+            ni = nj = int(key)
+        if ni * nj > 130 * 130:
+            continue  # 200^2 takes 8.7k sweeps; covered by the CPU KAT test
+        with make_grid(ni, nj) as g:
+            g.poisson_init(1.0, 1.0, 2)
+            it, _ = g.solve_rb()
+            assert it == want, (key, it, want)
+
+
+def test_rba_variant():
+    ni, nj = 64, 48
+    p, rhs = orc.poisson_init(ni, nj)
+    it_ref, res_ref = orc.solve_rb(p, rhs, 1.0 / ni, 1.0 / nj, OMEGA, EPS, 100000, "rba")
+    with make_grid(ni, nj, variant=M.SOLVE_RBA) as g:
+        g.poisson_init(1.0, 1.0, 2)
+        it, res = g.solve_rb()
+        assert it == it_ref
+        assert np.array_equal(g.download(M.P), p)
+        assert abs(res - res_ref) <= 1e-12 * res_ref
+
+
+@pytest.mark.parametrize("ni,nj,k", [(3, 2, 5), (2, 7, 4), (127, 129, 3), (128, 128, 3),
+                                     (129, 33, 4), (255, 17, 2), (256, 300, 3),
+                                     (511, 40, 3), (512, 65, 2), (513, 513, 3),
+                                     (1000, 777, 2), (2049, 130, 2)])
+def test_random_fields_vs_oracle(ni, nj, k):
+    rng = np.random.default_rng(ni * 7919 + nj)
+    p = rng.standard_normal((nj + 2, ni + 2))
+    rhs = rng.standard_normal((nj + 2, ni + 2))
+    dx, dy = 1.3 / ni, 0.7 / nj
+    want = p.copy()
+    it_ref, res_ref = orc.solve_rb(want, rhs, dx, dy, 1.7, 1e-300, k)
+    with M.Grid(ni, nj, dx, dy, 1.7, 1e-300, k) as g:
+        g.upload(M.P, p)
+        g.upload(M.RHS, rhs)
+        it, res = g.solve_rb()
+        got = g.download(M.P)
+    assert it == it_ref == k
+    assert np.array_equal(got, want), np.argwhere(got != want)[:5]
+    assert abs(res - res_ref) <= 1e-12 * abs(res_ref)
+
+
+def test_consecutive_solves_track_buffers():
+    """odd + even + odd iteration counts: the ping-pong buffer bookkeeping"""
+    ni, nj = 97, 61
+    rng = np.random.default_rng(5)
+    p = rng.standard_normal((nj + 2, ni + 2))
+    rhs = rng.standard_normal((nj + 2, ni + 2))
+    want = p.copy()
+    with M.Grid(ni, nj, 1.0 / ni, 1.0 / nj, 1.5, 1e-300, 10) as g:
+        g.upload(M.P, p)
+        g.upload(M.RHS, rhs)
+        for k in (3, 4, 1, 6):
+            g.solve_rb(itermax=k)
+            orc.solve_rb(want, rhs, 1.0 / ni, 1.0 / nj, 1.5, 1e-300, k)
+            assert np.array_equal(g.download(M.P), want), k
+
+
+def test_zero_iterations():
+    with make_grid(10, 10, itermax=0) as g:
+        g.poisson_init(1.0, 1.0, 2)
+        p0 = g.download(M.P)
+        it, res = g.solve_rb()
+        assert (it, res) == (0, 1.0)
+        assert np.array_equal(g.download(M.P), p0)
+    with make_grid(10, 10, eps=2.0) as g:  # eps^2 > res0 = 1: loop never entered
+        assert g.solve_rb() == (0, 1.0)
+
+
+def test_large_grid_two_sweeps():
+    """8192^2 (67M cells, 0.54 GB per field): bit-exact after 2 sweeps"""
+    n = 8192
+    p, rhs = orc.poisson_init(n, n)
+    want = p.copy()
+    it_ref, res_ref = orc.solve_rb(want, rhs, 1.0 / n, 1.0 / n, OMEGA, 1e-300, 2)
+    with make_grid(n, n, eps=1e-300, itermax=2) as g:
+        g.poisson_init(1.0, 1.0, 2)
+        it, res = g.solve_rb()
+        got = g.download(M.P)
+    assert it == 2
+    assert np.array_equal(got, want)
+    assert abs(res - res_ref) <= 1e-12 * res_ref

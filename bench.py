@@ -1,0 +1,199 @@
+#!/usr/bin/env python3
+"""Headline benchmark: red-black SOR MLUP/s + % of HBM roofline, 32768^2 grid
+(BASELINE.json metric; SURVEY 8d config 4 -- strong scaling 1/2/4/8 GPUs).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--size 32768]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+A "step" is one red+black SOR iteration (one fused sweep launch, the
+reference's solveRB loop body, assignment-4/src/solver.c:197-234) over the
+whole global grid.  The Poisson problem is assignment-4's problem 2 init
+(p = sin(4 pi x) + sin(4 pi y), rhs = sin(2 pi x)), omega 1.9, with eps so
+small that exactly K iterations run (convergence at 32768^2 needs ~2e8
+sweeps).  Fields are initialised on the device before the timed
+region; the timed region is K iterations, barrier + device sync on both
+sides, max over ranks.  Rank 0 prints ONE JSON line.
+
+roofline: algorithmic bytes per launch = 24 B per lattice update (read p,
+read rhs, write p: SURVEY 8d) x local cells, divided by the sweep kernel's
+average duration measured with HIP events recorded around every sweep launch
+on the library's stream (misor_enable_timing).  peak = 8000 GB/s (MI355X HBM3E
+spec, MI355X_MICROARCH.md).  traffic = HBM bytes per launch from the PMC
+profile committed under profiles/ for this configuration (FETCH_SIZE x 2 +
+WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md §HBM), or null.
+
+cpu_baseline: the reference's own solveRB (assignment-4/src/solver.c:179-238,
+compiled in place by oracle/Makefile into oracle/_ref/libref.so) on one host
+core, on a bounded sample (8192^2 grid, 40 sweeps); falls back to the C
+restatement (oracle/liboracle.so, kind "port") when _ref is absent.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "practical-parallel-algorithms-with-mpi_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+PEAK_GBS = 8000.0
+BYTES_PER_LUP = 24.0
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(n=8192, sweeps=40):
+    """Reference solveRB on 1 core, bounded sample; returns the JSON object."""
+    import ctypes as C
+
+    import numpy as np
+    import orc
+
+    kind = "reference" if orc.have_ref() else "port"
+    p = np.zeros((n + 2, n + 2))
+    rhs = np.zeros((n + 2, n + 2))
+    if kind == "reference":
+        R = orc.ref()
+        # refa4_run does init + solve; time init separately by a 0-sweep call
+        t0 = time.perf_counter()
+        R.refa4_run(n, n, 1.0, 1.0, 0, 1e-300, 1.9, 2, 1, None, None, None)
+        t1 = time.perf_counter()
+        it = R.refa4_run(n, n, 1.0, 1.0, sweeps, 1e-300, 1.9, 2, 1, None, None, None)
+        t2 = time.perf_counter()
+        solve_s = (t2 - t1) - (t1 - t0)
+    else:
+        p, rhs = orc.poisson_init(n, n)
+        t1 = time.perf_counter()
+        it, _ = orc.solve_rb(p, rhs, 1.0 / n, 1.0 / n, 1.9, 1e-300, sweeps)
+        solve_s = time.perf_counter() - t1
+    assert it == sweeps
+    mlups = n * n * sweeps / solve_s / 1e6
+    return {"value": round(mlups, 2), "unit": "MLUP/s", "cores": 1, "kind": kind,
+            "sample": "solveRB %dx%d, %d sweeps, %.2f s solve (init excluded), 1 host core"
+                      % (n, n, sweeps, solve_s)}
+
+
+def pmc_traffic(size, nranks):
+    """HBM bytes per sweep launch from the committed PMC summary, or None."""
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+        try:
+            d = json.load(open(path))
+        except Exception:
+            continue
+        if d.get("size") == size and d.get("nranks", 1) == nranks and "bytes_per_launch" in d:
+            best = d["bytes_per_launch"]
+    return best
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--size", type=int, default=32768)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log("warning: WORLD_SIZE=%d but --gpus %d" % (world, args.gpus))
+
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # noqa: F811
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    import pymisor as M
+
+    n = args.size
+    comm_id = None
+    if world > 1:
+        obj = [M.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        comm_id = obj[0]
+    g = M.Grid(n, n, 1.0 / n, 1.0 / n, 1.9, 1e-300, args.steps, device=local_rank,
+               nranks=world, rank=rank, comm_id=comm_id)
+    g.poisson_init(1.0, 1.0, 2)
+    local_cells = g.loc.ni * g.loc.nj
+
+    def barrier():
+        torch.cuda.synchronize()
+        g.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    if args.warmup > 0:
+        g.solve_rb(itermax=args.warmup)
+    g.enable_timing(True)
+    g.reset_stats()
+    barrier()
+    t0 = time.perf_counter()
+    it, res = g.solve_rb(itermax=args.steps)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    st = g.stats()
+    assert it == args.steps, (it, args.steps)
+
+    if dist is not None:
+        tt = torch.tensor([elapsed, st["sweep_ms"] / max(st["timed_sweeps"], 1)],
+                          dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = tt.tolist()
+    else:
+        kern_ms = st["sweep_ms"] / max(st["timed_sweeps"], 1)
+
+    total_lup = float(n) * float(n) * args.steps
+    mlups = total_lup / elapsed / 1e6
+    achieved = BYTES_PER_LUP * local_cells / (kern_ms * 1e-3) / 1e9  # GB/s per GPU
+    dims = "%dx%d" % tuple(g.loc.dims)
+    out = {
+        "metric": "red-black SOR MLUP/s + % HBM roofline at 1/2/4/8 MI355X, 32768^2 grid",
+        "value": round(mlups, 1),
+        "unit": "MLUP/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (assignment-4 problem-2 fields, generated on device)",
+        "config": {"workload": "2D Poisson red-black SOR (solveRB), %dx%d interior cells, "
+                               "fixed %d sweeps per timed region, 1 sweep = 1 step" % (n, n, args.steps),
+                   "imax": n, "jmax": n, "omega": 1.9, "problem": 2,
+                   "decomposition": dims, "baseline_config": 4},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / PEAK_GBS, 4),
+                     "traffic": pmc_traffic(n, world),
+                     "kernel": "rb_sweep_kernel", "kernel_ms": round(kern_ms, 4),
+                     "bytes_per_launch": BYTES_PER_LUP * local_cells},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline()
+        except Exception as e:  # reported, never fatal for the GPU number
+            out["cpu_baseline"] = {"value": None, "error": repr(e)}
+    g.close()
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -390,3 +390,32 @@ int orc_ns_run(orc_ns* s, int solver, int max_steps, int* iters, int cap,
     if (t_out) *t_out = t;
     return nt;
 }
+
+/* Generalised colour pass for the multi-rank CPU model of the GPU algorithm
+ * (tests/test_distributed_cpu.py): arrays with row stride `stride`, local
+ * cell (li,lj) at p[(lj+org)*stride + li+org]; updates the cells of colour
+ * `colour` (GLOBAL parity, global = (ioff+li, joff+lj)) in
+ * [ilo..ihi] x [jlo..jhi] and returns sum r^2 over the updated cells that
+ * also lie in [oilo..oihi] x [ojlo..ojhi] (the cells the rank owns).
+ * Arithmetic as solveRB, assignment-4/src/solver.c:207-212. */
+double orc_rb_pass_range(int stride, int org, int ilo, int ihi, int jlo, int jhi,
+                         int oilo, int oihi, int ojlo, int ojhi, int ioff, int joff,
+                         int colour, double idx2, double idy2, double factor, double* p,
+                         const double* rhs)
+{
+#define RG(a, i, j) (a)[(size_t)((j) + org) * (size_t)stride + (size_t)((i) + org)]
+    double res = 0.0;
+    for (int j = jlo; j <= jhi; j++) {
+        for (int i = ilo; i <= ihi; i++) {
+            if (((ioff + i + joff + j) & 1) != colour) continue;
+            double c = RG(p, i, j);
+            double r = RG(rhs, i, j) -
+                       ((RG(p, i + 1, j) - 2.0 * c + RG(p, i - 1, j)) * idx2 +
+                        (RG(p, i, j + 1) - 2.0 * c + RG(p, i, j - 1)) * idy2);
+            RG(p, i, j) = c - (factor * r);
+            if (i >= oilo && i <= oihi && j >= ojlo && j <= ojhi) res += (r * r);
+        }
+    }
+    return res;
+#undef RG
+}

@@ -54,6 +54,13 @@ double orc_rb_pass_block(int ni, int nj, int ioff, int joff, int colour,
                          double idx2, double idy2, double factor, double* p,
                          const double* rhs);
 
+/* Range form of the pass above for the 2-deep-halo model of the GPU
+ * decomposition; see oracle.c. */
+double orc_rb_pass_range(int stride, int org, int ilo, int ihi, int jlo, int jhi,
+                         int oilo, int oihi, int ojlo, int ojhi, int ioff, int joff,
+                         int colour, double idx2, double idy2, double factor, double* p,
+                         const double* rhs);
+
 /* ---------------- 2D Navier-Stokes (assignment-5/sequential) ---------------- */
 typedef struct {
     int imax, jmax;

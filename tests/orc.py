@@ -58,6 +58,8 @@ def lib():
         L.orc_rb_pass_block.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                         C.c_double, C.c_double, C.c_double, _dp, _dp]
         L.orc_rb_pass_block.restype = C.c_double
+        L.orc_rb_pass_range.argtypes = [C.c_int] * 13 + [C.c_double] * 3 + [_dp, _dp]
+        L.orc_rb_pass_range.restype = C.c_double
         for name in ("orc_ns_setup", "orc_ns_compute_timestep", "orc_ns_set_bc",
                      "orc_ns_set_special_bc", "orc_ns_compute_fg", "orc_ns_compute_rhs",
                      "orc_ns_normalize_pressure", "orc_ns_adapt_uv"):

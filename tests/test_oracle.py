@@ -1,0 +1,154 @@
+"""Pin the CPU oracle (oracle/oracle.c) before trusting it.
+
+1. Against the reference's own committed fixtures (assignment-4/p.dat,
+   init.dat) -- always.
+2. Against vectors generated from the reference compiled in this container
+   (tests/golden/*.npz, rb_kat.json; see tests/golden/make_golden.py) -- always.
+3. Against the reference itself (oracle/_ref/libref.so) on fresh random
+   inputs -- when _ref was built (build container; it also travels to the GPU
+   box as an in-tree .so).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import orc
+
+A6_DCAVITY = "a6_dcavity.par"
+A6_CANAL = "a6_canal.par"
+
+
+def fmt_rows(p):
+    return "\n".join("".join("%f " % x for x in row) for row in p) + "\n"
+
+
+def test_lexicographic_matches_committed_pdat(golden):
+    """assignment-4/p.dat is the reference's own output of poisson.par"""
+    p, rhs = orc.poisson_init(100, 100, 1.0, 1.0, 2)
+    it, _ = orc.solve_lex(p, rhs, 0.01, 0.01, 1.9, 1e-6, 1000000, xorder=0)
+    assert it == 2388
+    assert fmt_rows(p) == open(os.path.join(golden, "a4_p.dat")).read()
+
+
+def test_init_matches_committed_initdat(golden):
+    """init.dat agrees to its 6 printed decimals; it shows -0.000000 where our
+    (glibc) sin gives +1.2e-16 at x = pi multiples, so compare numerically."""
+    p, _ = orc.poisson_init(100, 100, 1.0, 1.0, 2)
+    ref = np.array([[float(x) for x in line.split()]
+                    for line in open(os.path.join(golden, "a4_init.dat"))])
+    assert ref.shape == p.shape
+    assert np.abs(np.round(p, 6) - ref).max() <= 1e-6
+
+
+def test_rb_iteration_kats(golden):
+    kat = json.load(open(os.path.join(golden, "rb_kat.json")))
+    for key, want in kat["iterations"].items():
+        ni, nj = (map(int, key.split("x")) if "x" in key else (int(key), int(key)))
+        p, rhs = orc.poisson_init(ni, nj)
+        it, res = orc.solve_rb(p, rhs, 1.0 / ni, 1.0 / nj, kat["omega"], kat["eps"], 10 ** 7)
+        assert it == want, key
+        assert res < kat["eps"] ** 2
+
+
+def test_rb_poisson100_fixture(golden):
+    z = np.load(os.path.join(golden, "rb_poisson100.npz"))
+    p, rhs = orc.poisson_init(100, 100)
+    it, _ = orc.solve_rb(p, rhs, 0.01, 0.01, 1.9, 1e-6, 1000000)
+    assert it == int(z["iterations"])
+    assert np.array_equal(p, z["p"])
+    p, rhs = orc.poisson_init(100, 100)
+    it, _ = orc.solve_lex(p, rhs, 0.01, 0.01, 1.9, 1e-6, 1000000, xorder=0)
+    assert it == int(z["iterations_lex"])
+    assert np.array_equal(p, z["p_lex"])
+
+
+def test_rb_sweep_fixtures(golden):
+    z = np.load(os.path.join(golden, "rb_sweeps.npz"))
+    for key in z.files:
+        if not key.startswith("geom_"):
+            continue
+        ni, nj, xl, yl = z[key]
+        ni, nj = int(ni), int(nj)
+        for k in (1, 2, 7):
+            p, rhs = orc.poisson_init(ni, nj, xl, yl, 2)
+            it, _ = orc.solve_rb(p, rhs, xl / ni, yl / nj, 1.9, 1e-300, k)
+            assert it == k
+            assert np.array_equal(p, z["p_%dx%d_k%d" % (ni, nj, k)]), key
+
+
+@pytest.mark.parametrize("name,par", [("ns_canal_rb_short.npz", A6_CANAL),
+                                      ("ns_dcavity_rb_short.npz", A6_DCAVITY)])
+def test_rb_ns_fixtures(golden, name, par):
+    z = np.load(os.path.join(golden, name))
+    prm = orc.read_par(os.path.join(golden, par))
+    prm["te"] = float(z["te"])
+    ns = orc.NS(prm)
+    n, iters, t = ns.run(solver=1)
+    assert n == int(z["steps"])
+    assert np.array_equal(iters, z["iters"])
+    for f in ("p", "u", "v"):
+        assert np.array_equal(getattr(ns, f), z[f]), f
+    assert t == float(z["t"])
+
+
+# ------------------------------------------------------------ vs the reference
+
+needs_ref = pytest.mark.skipif(not orc.have_ref(), reason="oracle/_ref not built")
+
+
+@needs_ref
+@pytest.mark.parametrize("which", ["rb", "rba", "lex"])
+def test_solvers_vs_reference_random(which):
+    rng = np.random.default_rng(11)
+    for (ni, nj) in ((5, 4), (31, 17), (64, 90)):
+        init = rng.standard_normal((nj + 2, ni + 2))
+        it_ref, p_ref, rhs = orc.ref_a4(ni, nj, which, itermax=37, eps=1e-300, omg=1.7,
+                                        xlength=1.3, ylength=0.9, init_p=init)
+        p = init.copy()
+        dx, dy = 1.3 / ni, 0.9 / nj
+        if which == "lex":
+            it, _ = orc.solve_lex(p, rhs, dx, dy, 1.7, 1e-300, 37, xorder=0)
+        else:
+            it, _ = orc.solve_rb(p, rhs, dx, dy, 1.7, 1e-300, 37, variant=which)
+        assert it == it_ref == 37
+        assert np.array_equal(p, p_ref)
+
+
+@needs_ref
+@pytest.mark.parametrize("par,steps", [(A6_DCAVITY, 25), (A6_CANAL, 12)])
+def test_ns_vs_reference(golden, par, steps):
+    path = os.path.join(golden, par)
+    for solver in (0, 1):
+        n, iters, p, u, v, t = orc.ref_ns(path, max_steps=steps, solver=solver)
+        ns = orc.NS(orc.read_par(path))
+        n2, iters2, t2 = ns.run(solver=solver, max_steps=steps)
+        assert n == n2 == steps and t == t2
+        if solver == 1:
+            assert np.array_equal(iters, iters2)
+        for f, ref in (("p", p), ("u", u), ("v", v)):
+            assert np.array_equal(getattr(ns, f), ref), (solver, f)
+
+
+@needs_ref
+def test_ns_step_functions_vs_reference_bc_variants(golden, tmp_path):
+    """every boundary flag on every wall, via edited copies of canal.par"""
+    base = open(os.path.join(golden, A6_CANAL)).read()
+    for combo in ((2, 2, 2, 2), (1, 3, 2, 1), (3, 1, 1, 3), (2, 1, 3, 2)):
+        txt = base
+        for key, val in zip(("bcLeft", "bcRight", "bcBottom", "bcTop"), combo):
+            lines = [("%s    %d\t\t#" % (key, val)) if ln.startswith(key) else ln
+                     for ln in txt.split("\n")]
+            txt = "\n".join(lines)
+        txt = txt.replace("imax          200", "imax          40").replace(
+            "jmax          50", "jmax          20")
+        f = tmp_path / ("c%d%d%d%d.par" % combo)
+        f.write_text(txt)
+        n, iters, p, u, v, t = orc.ref_ns(str(f), max_steps=6, solver=1)
+        prm = orc.read_par(str(f))
+        assert (prm["bcLeft"], prm["bcRight"], prm["bcBottom"], prm["bcTop"]) == combo
+        ns = orc.NS(prm)
+        ns.run(solver=1, max_steps=6)
+        for fld, ref in (("p", p), ("u", u), ("v", v)):
+            assert np.array_equal(getattr(ns, fld), ref), (combo, fld)

@@ -69,7 +69,13 @@ typedef struct {
      * nranks = 1 for a single GPU; then the rest is ignored. */
     int nranks, rank;
     int dims[2];        /* process grid {x, y}; {0,0} = MPI_Dims_create rule */
-    const void* comm_id; /* MISOR_COMM_ID_BYTES from misor_comm_unique_id() on rank 0 */
+    const void* comm_id; /* MISOR_COMM_ID_BYTES from misor_comm_unique_id() on rank 0:
+                          * one process per GPU, halos and reductions over RCCL.
+                          * Bytes starting with "LOCAL:<name>" select the in-process
+                          * transport instead: the nranks grids of group <name> are
+                          * created and driven by nranks host threads of ONE process
+                          * (any devices, also all on one GPU); every member must make
+                          * the same sequence of calls, as with RCCL. */
 } misor_desc;
 
 #define MISOR_COMM_ID_BYTES 128
@@ -152,6 +158,16 @@ int misor_normalize_pressure(misor_grid* g);                /* :204-217 */
 int misor_adapt_uv(misor_grid* g);                          /* :438-455 */
 /* max |u| and max |v| over all cells incl. ghosts (maxElement, :193-202) */
 int misor_max_uv(misor_grid* g, double* umax, double* vmax);
+
+/* launch-geometry knobs of the sweep kernel (defaults chosen by measurement,
+ * DESIGN.md); results are bit-identical for every setting */
+enum {
+    MISOR_TUNE_SWEEP_VARIANT = 1,  /* 0..7: strips per workgroup x rows in flight x nt stores */
+    MISOR_TUNE_ROWS_PER_BLOCK = 2, /* rows one workgroup marches; <= 0: automatic */
+    MISOR_TUNE_XCD_REMAP = 3       /* 1: adjacent blocks on one XCD (shared L2 halos) */
+};
+int misor_set_tuning(misor_grid* g, int key, int value);
+int misor_get_tuning(const misor_grid* g, int key, int* value);
 
 int misor_enable_timing(misor_grid* g, int on);
 int misor_get_stats(const misor_grid* g, misor_stats* out);

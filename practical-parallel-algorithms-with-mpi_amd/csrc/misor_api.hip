@@ -6,7 +6,11 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <condition_variable>
 #include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <vector>
 
 #include "misor_internal.h"
@@ -58,6 +62,37 @@ void dims_create(int n, int dims[2]) {
 // sizeOfRank (assignment-5/skeleton/src/solver.c:30-32)
 int size_of_rank(int rank, int size, int n) { return n / size + ((n % size > rank) ? 1 : 0); }
 
+// In-process transport: every rank of the group is a misor_grid owned by its
+// own host thread of ONE process (any devices, including all on one GPU).
+// Collectives are a host barrier plus device-to-device copies; the sum is
+// combined in rank order.  It exists so the decomposed kernels can be run and
+// checked on a single-GPU machine; across GPUs the RCCL path is used.
+struct LocalGroup {
+    int n = 0;
+    std::vector<misor_grid*> members;
+    std::vector<double> vals;  // n * 4 scratch for all-reduce
+    std::mutex m;
+    std::condition_variable cv;
+    int arrived = 0;
+    long long generation = 0;
+    int joined = 0, left = 0;
+
+    void barrier() {
+        std::unique_lock<std::mutex> lk(m);
+        const long long gen = generation;
+        if (++arrived == n) {
+            arrived = 0;
+            ++generation;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return generation != gen; });
+        }
+    }
+};
+std::mutex g_groups_mu;
+std::map<std::string, std::shared_ptr<LocalGroup>> g_groups;
+constexpr char kLocalPrefix[] = "LOCAL:";
+
 }  // namespace
 
 struct misor_grid {
@@ -72,7 +107,7 @@ struct misor_grid {
 
     // sweep
     SweepParams sp{};
-    int nbx = 0, nby = 0, nparts = 0;
+    int nbx = 0, nby = 0, nparts = 0, partials_cap = 0;
     double* partials = nullptr;
     DevState* st = nullptr;
     DevState* st_host = nullptr;  // pinned
@@ -90,6 +125,11 @@ struct misor_grid {
     // multi-GPU
     bool dist = false;
     ncclComm_t comm = nullptr;
+    int nbr[kDirs] = {-1, -1, -1, -1, -1, -1, -1, -1};  // L R B T BL BR TL TR
+    HaloPlan plan[3] = {};                               // by halo depth 1, 2
+    std::shared_ptr<LocalGroup> local;                   // in-process transport
+    double* sendbuf = nullptr;
+    double* recvbuf = nullptr;
 
     // stats
     bool timing = false;
@@ -161,23 +201,151 @@ void misor_destroy(misor_grid* g) {
     (void)hipFree(g->red_partials);
     (void)hipFree(g->red_out);
     (void)hipHostFree(g->red_host);
+    (void)hipFree(g->sendbuf);
+    (void)hipFree(g->recvbuf);
     for (auto e : g->ev) (void)hipEventDestroy(e);
     if (g->comm) ncclCommDestroy(g->comm);
     if (g->own_stream && g->stream) (void)hipStreamDestroy(g->stream);
     delete g;
 }
 
-static int pick_rows_per_block(int ni, int nj) {
+// Regions of the 8-neighbour exchange at halo depth d.  A rank sends the
+// cells it owns (interior, plus ghost cells on its physical sides) next to each
+// neighbour; ranks in one process row share nj and their physical top/bottom,
+// ranks in one process column share ni, so send and receive extents match.
+static void build_plan(misor_grid* g, int d) {
+    const int ni = g->loc.ni, nj = g->loc.nj;
+    const int* nb = g->nbr;
+    const int cl = nb[0] >= 0 ? 1 : 0, ch = nb[1] >= 0 ? ni : ni + 1;
+    const int rl = nb[2] >= 0 ? 1 : 0, rh = nb[3] >= 0 ? nj : nj + 1;
+    HaloRegion S[kDirs] = {
+        {1, rl, d, rh - rl + 1, 0},      {ni - d + 1, rl, d, rh - rl + 1, 0},
+        {cl, 1, ch - cl + 1, d, 0},      {cl, nj - d + 1, ch - cl + 1, d, 0},
+        {1, 1, d, d, 0},                 {ni - d + 1, 1, d, d, 0},
+        {1, nj - d + 1, d, d, 0},        {ni - d + 1, nj - d + 1, d, d, 0}};
+    HaloRegion R[kDirs] = {
+        {1 - d, rl, d, rh - rl + 1, 0},  {ni + 1, rl, d, rh - rl + 1, 0},
+        {cl, 1 - d, ch - cl + 1, d, 0},  {cl, nj + 1, ch - cl + 1, d, 0},
+        {1 - d, 1 - d, d, d, 0},         {ni + 1, 1 - d, d, d, 0},
+        {1 - d, nj + 1, d, d, 0},        {ni + 1, nj + 1, d, d, 0}};
+    HaloPlan& P = g->plan[d];
+    long long so = 0, ro = 0;
+    for (int k = 0; k < kDirs; ++k) {
+        if (nb[k] < 0) S[k].w = S[k].h = R[k].w = R[k].h = 0;
+        S[k].off = so;
+        R[k].off = ro;
+        so += (long long)S[k].w * S[k].h;
+        ro += (long long)R[k].w * R[k].h;
+        P.send[k] = S[k];
+        P.recv[k] = R[k];
+    }
+    P.total = so > ro ? so : ro;
+}
+
+// one 8-neighbour exchange of `field` at depth d over RCCL on the grid stream
+static int exchange(misor_grid* g, double* field, int d) {
+    if (!g->dist) return MISOR_OK;
+    const HaloPlan& P = g->plan[d];
+    launch_pack(g->stream, field, g->pitch, P, g->sendbuf);
+    if (g->local) {
+        static const int opposite[kDirs] = {1, 0, 3, 2, 7, 6, 5, 4};
+        HIPCHK(hipStreamSynchronize(g->stream));
+        g->local->barrier();  // every rank packed
+        for (int k = 0; k < kDirs; ++k) {
+            if (g->nbr[k] < 0) continue;
+            const misor_grid* q = g->local->members[g->nbr[k]];
+            const HaloRegion& sr = q->plan[d].send[opposite[k]];
+            const HaloRegion& rr = P.recv[k];
+            HIPCHK(hipMemcpyAsync(g->recvbuf + rr.off, q->sendbuf + sr.off,
+                                  sizeof(double) * (size_t)rr.w * rr.h,
+                                  hipMemcpyDeviceToDevice, g->stream));
+        }
+        launch_unpack(g->stream, field, g->pitch, P, g->recvbuf);
+        HIPCHK(hipStreamSynchronize(g->stream));
+        g->local->barrier();  // nobody repacks before every copy is done
+        HIPCHK(hipGetLastError());
+        return MISOR_OK;
+    }
+    NCCLCHK(ncclGroupStart());
+    for (int k = 0; k < kDirs; ++k) {
+        if (g->nbr[k] < 0) continue;
+        const size_t ns = (size_t)P.send[k].w * P.send[k].h;
+        const size_t nr = (size_t)P.recv[k].w * P.recv[k].h;
+        NCCLCHK(ncclSend(g->sendbuf + P.send[k].off, ns, ncclDouble, g->nbr[k], g->comm,
+                         g->stream));
+        NCCLCHK(ncclRecv(g->recvbuf + P.recv[k].off, nr, ncclDouble, g->nbr[k], g->comm,
+                         g->stream));
+    }
+    NCCLCHK(ncclGroupEnd());
+    launch_unpack(g->stream, field, g->pitch, P, g->recvbuf);
+    HIPCHK(hipGetLastError());
+    return MISOR_OK;
+}
+
+// all-reduce of n <= 4 device doubles (sum or max) across the ranks
+static int allreduce(misor_grid* g, double* dev, int n, int is_max) {
+    if (!g->dist) return MISOR_OK;
+    if (g->local) {
+        LocalGroup& G = *g->local;
+        double v[4];
+        HIPCHK(hipMemcpyAsync(v, dev, sizeof(double) * n, hipMemcpyDeviceToHost, g->stream));
+        HIPCHK(hipStreamSynchronize(g->stream));
+        const int r = g->desc.rank;
+        for (int k = 0; k < n; ++k) G.vals[4 * r + k] = v[k];
+        G.barrier();
+        for (int k = 0; k < n; ++k) {
+            double a = G.vals[k];
+            for (int q = 1; q < G.n; ++q) {
+                const double b = G.vals[4 * q + k];
+                a = is_max ? ((a > b) ? a : b) : a + b;
+            }
+            v[k] = a;
+        }
+        G.barrier();
+        HIPCHK(hipMemcpyAsync(dev, v, sizeof(double) * n, hipMemcpyHostToDevice, g->stream));
+        HIPCHK(hipStreamSynchronize(g->stream));
+        return MISOR_OK;
+    }
+    NCCLCHK(ncclAllReduce(dev, dev, n, ncclDouble, is_max ? ncclMax : ncclSum, g->comm,
+                          g->stream));
+    return MISOR_OK;
+}
+
+static int pick_rows_per_block(int ni, int nj, int waves) {
     // enough workgroups to fill 256 CUs several times, but long enough row
     // marches that the two redundant halo rows per block stay cheap
     const int strips = (ni + kStripCells - 1) / kStripCells;
-    const int nbx = (strips + kWavesX - 1) / kWavesX;
+    const int nbx = (strips + waves - 1) / waves;
     const int target_blocks = 2048;
     int want_nby = (target_blocks + nbx - 1) / nbx;
     int h = (nj + want_nby - 1) / want_nby;
     if (h < 4) h = 4;
-    if (h > 128) h = 128;
+    if (h > 16) h = 16;  // measured optimum at 32768^2 (profiles/r01_tune_rows.txt)
     return h;
+}
+
+// (re)derive the sweep launch geometry; partials are sized for the largest
+static int configure_sweep(misor_grid* g, int variant, int rows, int remap) {
+    if (variant < 0 || variant >= kNumSweepVariants) return fail(MISOR_EINVAL, "bad variant");
+    SweepParams& sp = g->sp;
+    const int waves = sweep_waves(variant);
+    sp.variant = variant;
+    sp.rows_per_block = rows > 0 ? rows : pick_rows_per_block(g->loc.ni, g->loc.nj, waves);
+    if (sp.rows_per_block < 1) sp.rows_per_block = 1;
+    sp.xcd_remap = remap;
+    int nby = 0;
+    g->nparts = sweep_partials(g->loc.ni, g->loc.nj, sp.rows_per_block, waves, &g->nbx, &nby);
+    g->nby = nby;
+    sp.nbx = g->nbx;
+    sp.nblocks = g->nparts;
+    if (g->nparts > g->partials_cap) {
+        if (g->partials) (void)hipFree(g->partials);
+        g->partials = nullptr;
+        if (hipMalloc(&g->partials, sizeof(double) * g->nparts) != hipSuccess)
+            return fail(MISOR_ENOMEM, "partials allocation failed");
+        g->partials_cap = g->nparts;
+    }
+    return MISOR_OK;
 }
 
 int misor_create(misor_grid** out, const misor_desc* d) {
@@ -230,12 +398,15 @@ int misor_create(misor_grid** out, const misor_desc* d) {
     sp.pitch = g->pitch;
     sp.ni = L.ni;
     sp.nj = L.nj;
-    sp.rows_per_block = pick_rows_per_block(L.ni, L.nj);
     sp.parity = (L.ioff + L.joff) & 1;
     sp.ghost_left = L.neighbours[0] < 0;
     sp.ghost_right = L.neighbours[1] < 0;
     sp.ghost_bottom = L.neighbours[2] < 0;
     sp.ghost_top = L.neighbours[3] < 0;
+    sp.red_lo_i = sp.ghost_left ? 1 : 0;
+    sp.red_hi_i = sp.ghost_right ? L.ni : L.ni + 1;
+    sp.red_lo_j = sp.ghost_bottom ? 1 : 0;
+    sp.red_hi_j = sp.ghost_top ? L.nj : L.nj + 1;
     const double dx2 = d->dx * d->dx, dy2 = d->dy * d->dy;
     sp.idx2 = 1.0 / dx2;
     sp.idy2 = 1.0 / dy2;
@@ -245,9 +416,11 @@ int misor_create(misor_grid** out, const misor_desc* d) {
     } else {
         sp.coef = d->omega * 0.5 * (dx2 * dy2) / (dx2 + dy2);  // solver.c:189
     }
-    g->nparts = sweep_partials(L.ni, L.nj, sp.rows_per_block, &g->nbx, &g->nby);
-    if (hipMalloc(&g->partials, sizeof(double) * g->nparts) != hipSuccess ||
-        hipMalloc(&g->st, sizeof(DevState)) != hipSuccess ||
+    if (configure_sweep(g, kDefaultSweepVariant, 0, 1) != MISOR_OK) {
+        misor_destroy(g);
+        return MISOR_ENOMEM;
+    }
+    if (hipMalloc(&g->st, sizeof(DevState)) != hipSuccess ||
         hipHostMalloc(&g->st_host, sizeof(DevState), hipHostMallocDefault) != hipSuccess)
         CREATE_FAIL(MISOR_ENOMEM, "state allocation failed");
     const int rb = reduce_blocks(L.ni, L.nj);
@@ -258,10 +431,45 @@ int misor_create(misor_grid** out, const misor_desc* d) {
 
     if (g->dist) {
         if (!d->comm_id) CREATE_FAIL(MISOR_EINVAL, "nranks > 1 needs comm_id");
-        ncclUniqueId id;
-        memcpy(&id, d->comm_id, sizeof id);
-        if (ncclCommInitRank(&g->comm, nranks, id, d->rank) != ncclSuccess)
-            CREATE_FAIL(MISOR_ECOMM, "ncclCommInitRank failed");
+        const int cx = L.coords[0], cy = L.coords[1], dx_ = L.dims[0], dy_ = L.dims[1];
+        auto at = [&](int x, int y) {
+            return (x >= 0 && x < dx_ && y >= 0 && y < dy_) ? x * dy_ + y : -1;
+        };
+        const int nbrs[kDirs] = {at(cx - 1, cy),     at(cx + 1, cy),     at(cx, cy - 1),
+                                 at(cx, cy + 1),     at(cx - 1, cy - 1), at(cx + 1, cy - 1),
+                                 at(cx - 1, cy + 1), at(cx + 1, cy + 1)};
+        for (int k = 0; k < kDirs; ++k) g->nbr[k] = nbrs[k];
+        build_plan(g, 1);
+        build_plan(g, 2);
+        const size_t hb = (size_t)(g->plan[2].total > 0 ? g->plan[2].total : 1) * sizeof(double);
+        if (hipMalloc(&g->sendbuf, hb) != hipSuccess || hipMalloc(&g->recvbuf, hb) != hipSuccess)
+            CREATE_FAIL(MISOR_ENOMEM, "halo buffer allocation failed");
+        if (memcmp(d->comm_id, kLocalPrefix, sizeof kLocalPrefix - 1) == 0) {
+            char name[MISOR_COMM_ID_BYTES + 1];
+            memcpy(name, d->comm_id, MISOR_COMM_ID_BYTES);
+            name[MISOR_COMM_ID_BYTES] = '\0';
+            {
+                std::lock_guard<std::mutex> lk(g_groups_mu);
+                auto& G = g_groups[name];
+                if (!G) {
+                    G = std::make_shared<LocalGroup>();
+                    G->n = nranks;
+                    G->members.assign(nranks, nullptr);
+                    G->vals.assign(4 * (size_t)nranks, 0.0);
+                }
+                if (G->n != nranks || G->members[d->rank])
+                    CREATE_FAIL(MISOR_EINVAL, "local group %s: bad rank/size", name);
+                G->members[d->rank] = g;
+                g->local = G;
+                if (++G->joined == nranks) g_groups.erase(name);  // name reusable
+            }
+            g->local->barrier();  // every member registered before any exchange
+        } else {
+            ncclUniqueId id;
+            memcpy(&id, d->comm_id, sizeof id);
+            if (ncclCommInitRank(&g->comm, nranks, id, d->rank) != ncclSuccess)
+                CREATE_FAIL(MISOR_ECOMM, "ncclCommInitRank failed");
+        }
     }
     if (hipStreamSynchronize(g->stream) != hipSuccess)
         CREATE_FAIL(MISOR_EHIP, "hipStreamSynchronize failed");
@@ -406,7 +614,6 @@ static int ensure_events(misor_grid* g, size_t n) {
 
 int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
     if (!g) return fail(MISOR_EINVAL, "null grid");
-    if (g->dist) return fail(MISOR_ESTATE, "decomposed solve not built yet");
     HIPCHK(hipSetDevice(g->device));
     const double epssq = g->desc.eps * g->desc.eps;
     DevState s0{};
@@ -438,11 +645,21 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
             const long long k = launched + b;
             const double* src = g->fld[kP0 + ((cur0 + k) & 1)];
             double* dst = g->fld[kP0 + ((cur0 + k + 1) & 1)];
+            if (g->dist) {  // 2-deep halo of src: one exchange per iteration
+                int rc = exchange(g, const_cast<double*>(src), 2);
+                if (rc) return rc;
+            }
             if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b], g->stream));
-            launch_sweep(g->stream, g->sp, src, dst, g->fld[kRhs], g->partials, g->st, g->nbx,
-                         g->nby);
+            launch_sweep(g->stream, g->sp, src, dst, g->fld[kRhs], g->partials, g->st);
             if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b + 1], g->stream));
-            launch_finish(g->stream, g->partials, g->nparts, g->st, cells);
+            if (g->dist) {
+                launch_finish(g->stream, g->partials, g->nparts, g->st, cells, 0);
+                int rc = allreduce(g, &g->st->sum, 1, 0);
+                if (rc) return rc;
+                launch_decide(g->stream, g->st, cells);
+            } else {
+                launch_finish(g->stream, g->partials, g->nparts, g->st, cells, 1);
+            }
         }
         HIPCHK(hipGetLastError());
         launched += batch;
@@ -468,6 +685,11 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
     }
     const int it = g->st_host->it;
     g->cur = (cur0 + it) & 1;
+    if (g->dist) {  // leave the halo of the final field consistent (adaptUV reads it)
+        int rc = exchange(g, g->fld[g->cur], 2);
+        if (rc) return rc;
+        HIPCHK(hipStreamSynchronize(g->stream));
+    }
     g->last_iters = it;
     g->stats.sweeps += it;
     if (iters) *iters = it;
@@ -531,8 +753,10 @@ int misor_max_uv(misor_grid* g, double* umax, double* vmax) {
                          kReduceMax, 2, g->red_out);
     HIPCHK(hipGetLastError());
     if (g->dist)
-        NCCLCHK(ncclAllReduce(g->red_out, g->red_out, 2, ncclDouble, ncclMax, g->comm,
-                              g->stream));
+    {
+        int rc = allreduce(g, g->red_out, 2, 1);
+        if (rc) return rc;
+    }
     HIPCHK(hipMemcpyAsync(g->red_host, g->red_out, 2 * sizeof(double), hipMemcpyDeviceToHost,
                           g->stream));
     HIPCHK(hipStreamSynchronize(g->stream));
@@ -577,6 +801,9 @@ int misor_set_special_boundary_condition(misor_grid* g) {
 
 int misor_compute_fg(misor_grid* g) {
     NEED_NS(g);
+    int rc = exchange(g, g->fld[kU], 1);  // 9-point stencil incl. diagonals: corners too
+    if (!rc) rc = exchange(g, g->fld[kV], 1);
+    if (rc) return rc;
     launch_compute_fg(g->nl, g->fld[kU], g->fld[kV], g->fld[kF], g->fld[kG]);
     HIPCHK(hipGetLastError());
     return MISOR_OK;
@@ -584,6 +811,9 @@ int misor_compute_fg(misor_grid* g) {
 
 int misor_compute_rhs(misor_grid* g) {
     NEED_NS(g);
+    int rc = exchange(g, g->fld[kF], 1);  // F(i-1,j), G(i,j-1): the skeleton's shift()
+    if (!rc) rc = exchange(g, g->fld[kG], 1);
+    if (rc) return rc;
     launch_compute_rhs(g->nl, g->fld[kF], g->fld[kG], g->fld[kRhs]);
     HIPCHK(hipGetLastError());
     return MISOR_OK;
@@ -596,8 +826,10 @@ int misor_normalize_pressure(misor_grid* g) {
     launch_finish_reduce(g->stream, g->red_partials, reduce_blocks(g->loc.ni, g->loc.nj),
                          kReduceSum, 1, g->red_out);
     if (g->dist)
-        NCCLCHK(ncclAllReduce(g->red_out, g->red_out, 1, ncclDouble, ncclSum, g->comm,
-                              g->stream));
+    {
+        int rc = allreduce(g, g->red_out, 1, 0);
+        if (rc) return rc;
+    }
     const double cells = (double)(g->desc.imax + 2) * (double)(g->desc.jmax + 2);
     launch_sub_mean(g->nl, p, g->red_out, cells);
     HIPCHK(hipGetLastError());
@@ -621,6 +853,29 @@ int misor_get_stats(const misor_grid* g, misor_stats* out) {
     if (!g || !out) return fail(MISOR_EINVAL, "null argument");
     *out = g->stats;
     return MISOR_OK;
+}
+
+int misor_set_tuning(misor_grid* g, int key, int value) {
+    if (!g) return fail(MISOR_EINVAL, "null grid");
+    switch (key) {
+    case MISOR_TUNE_SWEEP_VARIANT:
+        return configure_sweep(g, value, g->sp.rows_per_block, g->sp.xcd_remap);
+    case MISOR_TUNE_ROWS_PER_BLOCK:
+        return configure_sweep(g, g->sp.variant, value, g->sp.xcd_remap);
+    case MISOR_TUNE_XCD_REMAP:
+        return configure_sweep(g, g->sp.variant, g->sp.rows_per_block, value != 0);
+    default: return fail(MISOR_EINVAL, "unknown tuning key %d", key);
+    }
+}
+
+int misor_get_tuning(const misor_grid* g, int key, int* value) {
+    if (!g || !value) return fail(MISOR_EINVAL, "null argument");
+    switch (key) {
+    case MISOR_TUNE_SWEEP_VARIANT: *value = g->sp.variant; return MISOR_OK;
+    case MISOR_TUNE_ROWS_PER_BLOCK: *value = g->sp.rows_per_block; return MISOR_OK;
+    case MISOR_TUNE_XCD_REMAP: *value = g->sp.xcd_remap; return MISOR_OK;
+    default: return fail(MISOR_EINVAL, "unknown tuning key %d", key);
+    }
 }
 
 int misor_reset_stats(misor_grid* g) {

@@ -22,7 +22,7 @@ namespace misor {
 //    line; the ghost column i = 0 is the last double of the preceding line.
 //  - kYOff = 2 and two spare rows at the top give every sweep block its two
 //    halo rows (j0-2 .. j1+1) without clamping.
-//  - pitch = 32 + round_up(ni, kStripCells * kWavesX): left pad line, the
+//  - pitch = 32 + round_up(ni, kStripCells * kMaxWavesX): left pad line, the
 //    strips, the right halo pair and pad; a multiple of 16 doubles (128 B).
 // Padding cells are zero and never feed an interior result.
 // ---------------------------------------------------------------------------
@@ -30,14 +30,27 @@ constexpr int kXOff = 15;
 constexpr int kYOff = 2;
 constexpr int kLanes = 64;                 // wavefront
 constexpr int kStripCells = 2 * kLanes;    // 128 columns per wave (2 per lane)
-constexpr int kWavesX = 4;                 // waves per workgroup, side by side
-constexpr int kSweepThreads = kLanes * kWavesX;
+constexpr int kMaxWavesX = 16;             // strips per sweep workgroup (max)
+constexpr int kMaxAhead = 3;               // rows a sweep keeps in flight (max)
 
 inline long long layout_pitch(int ni) {
-    const int w = kStripCells * kWavesX;
+    const int w = kStripCells * kMaxWavesX;
     return 32 + (long long)((ni + w - 1) / w) * w;
 }
-inline long long layout_rows(int nj) { return (long long)nj + 6; }
+// rows j = -2 .. nj+1+kMaxAhead+1 (sweep prefetch runs past the top halo)
+inline long long layout_rows(int nj) { return (long long)nj + 4 + kMaxAhead + 2; }
+
+// sweep kernel variants: strips per workgroup, rows in flight, nt stores
+struct SweepVariant {
+    int waves, ahead, nt_store, nt_load;
+};
+constexpr SweepVariant kSweepVariants[] = {
+    {4, 1, 0, 0}, {4, 2, 0, 0}, {4, 3, 0, 0}, {4, 1, 1, 0}, {4, 2, 1, 0},
+    {8, 1, 0, 0}, {8, 2, 0, 0}, {8, 2, 1, 0}, {8, 1, 1, 0}, {8, 3, 1, 0},
+    {16, 1, 1, 0}, {16, 2, 1, 0}, {4, 3, 1, 0}, {8, 2, 1, 1}, {16, 2, 1, 1}};
+constexpr int kNumSweepVariants = 15;
+constexpr int kDefaultSweepVariant = 7;  // 8 strips, 2 rows ahead, nt stores (tools/tune_sweep.py)
+int sweep_waves(int variant);
 
 // Solver state that lives on the device between launches.  Written only by
 // the finish kernel (one workgroup) and read by the next sweep launch.
@@ -48,6 +61,7 @@ struct DevState {
     int pad;
     double res;    // residual of the last iteration
     double epssq;
+    double sum;    // sum r^2 of the last sweep (this rank, then all-reduced)
 };
 
 struct SweepParams {
@@ -56,6 +70,10 @@ struct SweepParams {
     int rows_per_block;  // H
     int parity;          // (ioff + joff) & 1 : global colour of local cell (0,0)
     int ghost_left, ghost_right, ghost_bottom, ghost_top;  // physical boundary -> Neumann copy
+    int red_lo_i, red_hi_i, red_lo_j, red_hi_j;  // cells whose red value is computed
+    int variant;         // index into kSweepVariants
+    int nbx, nblocks;    // launch geometry (logical blocks nbx x nby)
+    int xcd_remap;       // deal consecutive logical blocks to one XCD
     double idx2, idy2, coef;  // 1/dx^2, 1/dy^2, factor (RB) or omega*factor (RBA)
 };
 
@@ -68,11 +86,27 @@ struct NsParams {
 
 // kernel launchers (sor_kernels.hip, ns_kernels.hip)
 void launch_sweep(hipStream_t s, const SweepParams& prm, const double* src, double* dst,
-                  const double* rhs, double* partials, const DevState* st, int nblocks_x,
-                  int nblocks_y);
+                  const double* rhs, double* partials, const DevState* st);
 void launch_finish(hipStream_t s, const double* partials, int nparts, DevState* st,
-                   double inv_cells);
-int sweep_partials(int ni, int nj, int rows_per_block, int* nbx, int* nby);
+                   double cells, int decide);
+void launch_decide(hipStream_t s, DevState* st, double cells);
+
+// 8-neighbour halo exchange of one field (halo.hip): regions in local cell
+// coordinates; direction order L, R, B, T, BL, BR, TL, TR
+constexpr int kDirs = 8;
+struct HaloRegion {
+    int x0, y0, w, h;  // first cell and extent (local reference indices)
+    long long off;     // offset in the packed buffer (doubles)
+};
+struct HaloPlan {
+    HaloRegion send[kDirs], recv[kDirs];
+    long long total;  // doubles in each of the send / recv buffers
+};
+void launch_pack(hipStream_t s, const double* field, long long pitch, const HaloPlan& plan,
+                 double* sendbuf);
+void launch_unpack(hipStream_t s, double* field, long long pitch, const HaloPlan& plan,
+                   const double* recvbuf);
+int sweep_partials(int ni, int nj, int rows_per_block, int waves, int* nbx, int* nby);
 
 void launch_fill(hipStream_t s, double* a, long long count, double v);
 void launch_poisson_init(hipStream_t s, double* p, double* rhs, const double* sx,

@@ -39,12 +39,6 @@ namespace misor {
 
 namespace {
 
-__device__ __forceinline__ double2 ld2(const double* p) {
-    return *reinterpret_cast<const double2*>(p);
-}
-__device__ __forceinline__ void st2(double* p, double2 v) {
-    *reinterpret_cast<double2*>(p) = v;
-}
 // lane l receives lane l-1's value (lane 0: its own, overridden by callers)
 __device__ __forceinline__ double from_left(double v) { return __shfl_up(v, 1, 64); }
 // lane l receives lane l+1's value (lane 63: its own, overridden by callers)
@@ -58,16 +52,45 @@ __device__ __forceinline__ double wave_sum(double v) {
 
 }  // namespace
 
-__global__ __launch_bounds__(kSweepThreads) void rb_sweep_kernel(
+typedef double d2 __attribute__((ext_vector_type(2)));
+
+template <bool NT = false>
+__device__ __forceinline__ d2 ldv(const double* p) {
+    if (NT) return __builtin_nontemporal_load(reinterpret_cast<const d2*>(p));
+    return *reinterpret_cast<const d2*>(p);
+}
+
+template <bool NT>
+__device__ __forceinline__ void stv(double* p, d2 v) {
+    if (NT)
+        __builtin_nontemporal_store(v, reinterpret_cast<d2*>(p));
+    else
+        *reinterpret_cast<d2*>(p) = v;
+}
+
+// WAVES: strips per workgroup; D: rows of p / rhs kept in flight ahead of the
+// row being updated; NT: non-temporal stores of the new p (write-once stream)
+template <int WAVES, int D, bool NT, bool LNT>
+__global__ __launch_bounds__(kLanes* WAVES) void rb_sweep_kernel(
     SweepParams prm, const double* __restrict__ src, double* __restrict__ dst,
     const double* __restrict__ rhs, double* __restrict__ partials,
     const DevState* __restrict__ st) {
-    __shared__ double wsum[kWavesX];
+    __shared__ double wsum[WAVES];
     if (st->done) return;  // converged or capped: the whole grid exits
+
+    // logical block: with xcd_remap, blocks that the dispatcher deals to one XCD
+    // (b, b+8, b+16, ...) get consecutive logical ids, so horizontally and
+    // vertically adjacent blocks share that XCD's L2 for their halo lines
+    int L = blockIdx.x;
+    if (prm.xcd_remap) {
+        const int nwg = prm.nblocks, q = nwg / 8, rr = nwg % 8, x = L % 8;
+        L = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + L / 8;
+    }
+    const int bx = L % prm.nbx, by = L / prm.nbx;
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int strip = blockIdx.x * kWavesX + wave;
+    const int strip = bx * WAVES + wave;
     const int ni = prm.ni, nj = prm.nj;
     const int c0 = 1 + strip * kStripCells;
     const int ia = c0 + 2 * lane;  // odd local column
@@ -77,16 +100,20 @@ __global__ __launch_bounds__(kSweepThreads) void rb_sweep_kernel(
 
     const bool hl = (lane == 0);   // holds the left halo pair  (c0-2, c0-1)
     const bool hr = (lane == 63);  // holds the right halo pair (c0+128, c0+129)
-    const bool in_a = ia <= ni;
+    const bool in_a = ia <= ni;    // owned: black update + residual
     const bool in_b = ib <= ni;
+    // red is also recomputed on the 1-deep halo ring where a neighbour rank
+    // owns it (red_lo/hi = 0 / n+1 there), from the 2-deep halo of p
+    const bool red_a = ia <= prm.red_hi_i;
+    const bool red_b = ib <= prm.red_hi_i;
     const int hcol = hl ? c0 - 1 : c0 + kStripCells;  // halo column that can be red
-    const bool in_h = (hcol >= 1) && (hcol <= ni);
+    const bool in_h = (hcol >= prm.red_lo_i) && (hcol <= prm.red_hi_i);
     const int hoff = hl ? -2 : 2;  // halo pair address relative to ia (lanes 0 / 63)
 
     double acc = 0.0;
 
     // physical corners are never touched by solveRB; carry them into dst
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 4) {
+    if (L == 0 && threadIdx.x < 4) {
         const int t = threadIdx.x;
         const int ci = (t & 1) ? ni + 1 : 0, cj = (t & 2) ? nj + 1 : 0;
         const bool phys = ((t & 1) ? prm.ghost_right : prm.ghost_left) &&
@@ -98,7 +125,7 @@ __global__ __launch_bounds__(kSweepThreads) void rb_sweep_kernel(
     }
 
     if (c0 <= ni) {  // wave-uniform: strips past the domain only join the reduction
-        const int j0 = 1 + (int)blockIdx.y * prm.rows_per_block;
+        const int j0 = 1 + by * prm.rows_per_block;
         const int j1 = min(j0 + prm.rows_per_block, nj + 1);
 
         // element (ia, j) of the three arrays: base + j*pitch
@@ -106,50 +133,55 @@ __global__ __launch_bounds__(kSweepThreads) void rb_sweep_kernel(
         const double* rp = rhs + (long long)kYOff * pitch + kXOff + ia;
         double* dp = dst + (long long)kYOff * pitch + kXOff + ia;
 
-        auto ldp = [&](int j) { return ld2(sp + (long long)j * pitch); };
-        auto ldr = [&](int j) { return ld2(rp + (long long)j * pitch); };
+        auto ldp = [&](int j) { return ldv<LNT>(sp + (long long)j * pitch); };
+        auto ldr = [&](int j) { return ldv<LNT>(rp + (long long)j * pitch); };
         auto ldph = [&](int j) {
-            double2 v = make_double2(0.0, 0.0);
-            if (hl | hr) v = ld2(sp + (long long)j * pitch + hoff);
+            d2 v = {0.0, 0.0};
+            if (hl | hr) v = ldv(sp + (long long)j * pitch + hoff);
             return v;
         };
         auto ldrh = [&](int j) {
-            double2 v = make_double2(0.0, 0.0);
-            if (hl | hr) v = ld2(rp + (long long)j * pitch + hoff);
+            d2 v = {0.0, 0.0};
+            if (hl | hr) v = ldv(rp + (long long)j * pitch + hoff);
             return v;
         };
 
-        // window: Mm2 = M(r-2), Mm1 = M(r-1) (red new, black old), Oc = O(r),
-        // Up = O(r+1), Nx = O(r+2) in flight; H* = halo pairs; R* = rhs.
-        double2 Mm1 = ldp(j0 - 2), Hm1 = ldph(j0 - 2);
-        double2 Oc = ldp(j0 - 1), Hc = ldph(j0 - 1);
-        double2 Up = ldp(j0), Hup = ldph(j0);
-        double2 Rc = ldr(j0 - 1), RHc = ldrh(j0 - 1);
-        double2 Mm2 = make_double2(0.0, 0.0), Rm1 = make_double2(0.0, 0.0);
+        // window: Mm2 = M(r-2), Mm1 = M(r-1) (red new, black old), Oc = O(r);
+        // rings Pq = O(r+1 .. r+D), Rq = rhs(r .. r+D-1) (+ halo pairs) in flight
+        d2 Mm1 = ldp(j0 - 2), Hm1 = ldph(j0 - 2);
+        d2 Oc = ldp(j0 - 1), Hc = ldph(j0 - 1);
+        d2 Pq[D], Hq[D], Rq[D], RHq[D];
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            Pq[k] = ldp(j0 + k);
+            Hq[k] = ldph(j0 + k);
+            Rq[k] = ldr(j0 - 1 + k);
+            RHq[k] = ldrh(j0 - 1 + k);
+        }
+        d2 Mm2 = {0.0, 0.0}, Rm1 = {0.0, 0.0};
         double HRm1 = 0.0;
 
         for (int r = j0 - 1; r <= j1; ++r) {
-            // prefetch two rows ahead (p) / one row ahead (rhs)
-            const double2 Nx = ldp(r + 2), HNx = ldph(r + 2);
-            const double2 RNx = ldr(r + 1), RHNx = ldrh(r + 1);
+            // issue the loads D rows ahead
+            const d2 nP = ldp(r + 1 + D), nH = ldph(r + 1 + D);
+            const d2 nR = ldr(r + D), nRH = ldrh(r + D);
+            const d2 Up = Pq[0], Hup = Hq[0], Rc = Rq[0], RHc = RHq[0];
 
             // ---------------- red pass on row r ----------------
             const int q = (prm.parity + 1 + r) & 1;  // 0: column ia red, 1: column ib red
-            double2 Mr = Oc;
+            d2 Mr = Oc;
             double HRc = hl ? Hc.y : Hc.x;  // halo-column value after the red pass
-            if (r >= 1 && r <= nj) {
+            if (r >= prm.red_lo_j && r <= prm.red_hi_j) {
                 const bool own = (r >= j0) && (r < j1);
                 if (q == 0) {
                     // (ia, r) red; left neighbour from lane l-1 (lane 0: halo)
-                    double L = from_left(Oc.y);
-                    if (hl) L = Hc.y;
+                    double Lf = from_left(Oc.y);
+                    if (hl) Lf = Hc.y;
                     const double c = Oc.x;
-                    const double rr = Rc.x - (((Oc.y - 2.0 * c) + L) * idx2 +
+                    const double rr = Rc.x - (((Oc.y - 2.0 * c) + Lf) * idx2 +
                                               ((Up.x - 2.0 * c) + Mm1.x) * idy2);
-                    if (in_a) {
-                        Mr.x = c - coef * rr;
-                        if (own) acc += rr * rr;
-                    }
+                    if (red_a) Mr.x = c - coef * rr;
+                    if (in_a && own) acc += rr * rr;
                     // right halo column c0+128 is red too (same parity as ia)
                     if (hr && in_h) {
                         const double ch = Hc.x;
@@ -159,15 +191,13 @@ __global__ __launch_bounds__(kSweepThreads) void rb_sweep_kernel(
                     }
                 } else {
                     // (ib, r) red; right neighbour from lane l+1 (lane 63: halo)
-                    double R = from_right(Oc.x);
-                    if (hr) R = Hc.x;
+                    double Rf = from_right(Oc.x);
+                    if (hr) Rf = Hc.x;
                     const double c = Oc.y;
-                    const double rr = Rc.y - (((R - 2.0 * c) + Oc.x) * idx2 +
+                    const double rr = Rc.y - (((Rf - 2.0 * c) + Oc.x) * idx2 +
                                               ((Up.y - 2.0 * c) + Mm1.y) * idy2);
-                    if (in_b) {
-                        Mr.y = c - coef * rr;
-                        if (own) acc += rr * rr;
-                    }
+                    if (red_b) Mr.y = c - coef * rr;
+                    if (in_b && own) acc += rr * rr;
                     // left halo column c0-1 is red (same parity as ib)
                     if (hl && in_h) {
                         const double ch = Hc.y;
@@ -181,7 +211,7 @@ __global__ __launch_bounds__(kSweepThreads) void rb_sweep_kernel(
             // ---------------- black pass on row r-1, then store ----------------
             const int jw = r - 1;
             if (jw >= j0) {  // implies 1 <= jw <= nj
-                double2 F = Mm1;
+                d2 F = Mm1;
                 if (q == 0) {
                     // row r-1 has q' = 1: column ia black, its right neighbour ib red
                     double Ln = from_left(Mm1.y);
@@ -208,53 +238,60 @@ __global__ __launch_bounds__(kSweepThreads) void rb_sweep_kernel(
 
                 // Neumann ghost copy (assignment-4/src/solver.c:219-227), fused:
                 // columns 0 / ni+1 of this row, rows 0 / nj+1 from rows 1 / nj.
-                double2 out = F;
+                d2 out = F;
                 if (prm.ghost_right) {
                     const double fb_left = from_left(F.y);  // final value at column ia-1
                     if (ia == ni + 1) out.x = fb_left;
                     if (ib == ni + 1) out.y = F.x;
                 }
                 double* drow = dp + (long long)jw * pitch;
-                st2(drow, out);
+                stv<NT>(drow, out);
                 if (prm.ghost_left && strip == 0 && hl)  // (pad, P(0,jw) = P(1,jw))
-                    st2(drow - 2, make_double2(Hm1.x, F.x));
+                    stv<false>(drow - 2, d2{Hm1.x, F.x});
                 if (prm.ghost_right && hr && c0 + kStripCells == ni + 1)
-                    st2(drow + 2, make_double2(F.y, Hm1.y));  // (P(ni+1)=P(ni), pad)
+                    stv<false>(drow + 2, d2{F.y, Hm1.y});  // (P(ni+1)=P(ni), pad)
                 if (prm.ghost_bottom && jw == 1) {
                     // row 0 <- row 1 for 1 <= i <= ni; corners keep their old value
-                    const double2 o0 = Mm2;  // = old row 0 (ghost rows are never updated)
-                    st2(dp, make_double2(in_a ? F.x : o0.x, in_b ? F.y : o0.y));
+                    const d2 o0 = Mm2;  // = old row 0 (ghost rows are never updated)
+                    stv<false>(dp, d2{in_a ? F.x : o0.x, in_b ? F.y : o0.y});
                 }
                 if (prm.ghost_top && jw == nj) {
-                    const double2 on = Mr;  // = old row nj+1
-                    st2(drow + pitch, make_double2(in_a ? F.x : on.x, in_b ? F.y : on.y));
+                    const d2 on = Mr;  // = old row nj+1
+                    stv<false>(drow + pitch, d2{in_a ? F.x : on.x, in_b ? F.y : on.y});
                 }
             }
 
-            // rotate the window
+            // rotate the window and the rings
             Mm2 = Mm1;
             Mm1 = Mr;
             Oc = Up;
-            Up = Nx;
             Hm1 = Hc;
             Hc = Hup;
-            Hup = HNx;
             Rm1 = Rc;
-            Rc = RNx;
-            RHc = RHNx;
             HRm1 = HRc;
+#pragma unroll
+            for (int k = 0; k + 1 < D; ++k) {
+                Pq[k] = Pq[k + 1];
+                Hq[k] = Hq[k + 1];
+                Rq[k] = Rq[k + 1];
+                RHq[k] = RHq[k + 1];
+            }
+            Pq[D - 1] = nP;
+            Hq[D - 1] = nH;
+            Rq[D - 1] = nR;
+            RHq[D - 1] = nRH;
         }
     }
 
-    // deterministic reduction: lane tree, then waves 0..3 in order
+    // deterministic reduction: lane tree, then waves in order
     acc = wave_sum(acc);
     if (lane == 0) wsum[wave] = acc;
     __syncthreads();
     if (threadIdx.x == 0) {
         double s = 0.0;
 #pragma unroll
-        for (int w = 0; w < kWavesX; ++w) s += wsum[w];
-        partials[(long long)blockIdx.y * gridDim.x + blockIdx.x] = s;
+        for (int w = 0; w < WAVES; ++w) s += wsum[w];
+        partials[L] = s;  // logical id: the sum order does not depend on the remap
     }
 }
 
@@ -262,8 +299,8 @@ __global__ __launch_bounds__(kSweepThreads) void rb_sweep_kernel(
 // solveRB (assignment-4/src/solver.c:197,229,233):
 //   res = sum / (imax*jmax); it++; continue while res >= eps^2 && it < itermax
 __global__ __launch_bounds__(1024) void rb_finish_kernel(const double* __restrict__ partials,
-                                                         int n, DevState* st,
-                                                         double cells) {
+                                                         int n, DevState* st, double cells,
+                                                         int decide) {
     __shared__ double sh[1024];
     if (st->done) return;
     const int t = threadIdx.x;
@@ -279,7 +316,8 @@ __global__ __launch_bounds__(1024) void rb_finish_kernel(const double* __restric
     if (t < 64) {
         double v = sh[t];
         v = wave_sum(v);
-        if (t == 0) {
+        if (t == 0 && !decide) st->sum = v;  // decomposed: all-reduce, then decide
+        if (t == 0 && decide) {
             const double res = v / cells;
             const int it = st->it + 1;
             st->res = res;
@@ -289,23 +327,60 @@ __global__ __launch_bounds__(1024) void rb_finish_kernel(const double* __restric
     }
 }
 
-int sweep_partials(int ni, int nj, int rows_per_block, int* nbx, int* nby) {
+int sweep_waves(int variant) { return kSweepVariants[variant].waves; }
+
+int sweep_partials(int ni, int nj, int rows_per_block, int waves, int* nbx, int* nby) {
     const int strips = (ni + kStripCells - 1) / kStripCells;
-    *nbx = (strips + kWavesX - 1) / kWavesX;
+    *nbx = (strips + waves - 1) / waves;
     *nby = (nj + rows_per_block - 1) / rows_per_block;
     return (*nbx) * (*nby);
 }
 
 void launch_sweep(hipStream_t s, const SweepParams& prm, const double* src, double* dst,
-                  const double* rhs, double* partials, const DevState* st, int nbx,
-                  int nby) {
-    hipLaunchKernelGGL(rb_sweep_kernel, dim3(nbx, nby), dim3(kSweepThreads), 0, s, prm, src,
-                       dst, rhs, partials, st);
+                  const double* rhs, double* partials, const DevState* st) {
+#define SWEEP(W, D, NT, LNT)                                                                \
+    hipLaunchKernelGGL((rb_sweep_kernel<W, D, NT, LNT>), dim3(prm.nblocks), dim3(kLanes * W), \
+                       0, s, prm, src, dst, rhs, partials, st)
+    // must match kSweepVariants (misor_internal.h)
+    switch (prm.variant) {
+    case 0: SWEEP(4, 1, false, false); break;
+    case 1: SWEEP(4, 2, false, false); break;
+    case 2: SWEEP(4, 3, false, false); break;
+    case 3: SWEEP(4, 1, true, false); break;
+    case 4: SWEEP(4, 2, true, false); break;
+    case 5: SWEEP(8, 1, false, false); break;
+    case 6: SWEEP(8, 2, false, false); break;
+    case 7: SWEEP(8, 2, true, false); break;
+    case 8: SWEEP(8, 1, true, false); break;
+    case 9: SWEEP(8, 3, true, false); break;
+    case 10: SWEEP(16, 1, true, false); break;
+    case 11: SWEEP(16, 2, true, false); break;
+    case 12: SWEEP(4, 3, true, false); break;
+    case 13: SWEEP(8, 2, true, true); break;
+    case 14: SWEEP(16, 2, true, true); break;
+    default: SWEEP(8, 2, true, false); break;
+    }
+#undef SWEEP
 }
 
 void launch_finish(hipStream_t s, const double* partials, int nparts, DevState* st,
-                   double cells) {
-    hipLaunchKernelGGL(rb_finish_kernel, dim3(1), dim3(1024), 0, s, partials, nparts, st, cells);
+                   double cells, int decide) {
+    hipLaunchKernelGGL(rb_finish_kernel, dim3(1), dim3(1024), 0, s, partials, nparts, st, cells,
+                       decide);
+}
+
+// decomposed runs: st->sum holds the all-reduced sum r^2 of every rank
+__global__ void rb_decide_kernel(DevState* st, double cells) {
+    if (st->done) return;
+    const double res = st->sum / cells;
+    const int it = st->it + 1;
+    st->res = res;
+    st->it = it;
+    st->done = !((res >= st->epssq) && (it < st->itermax));
+}
+
+void launch_decide(hipStream_t s, DevState* st, double cells) {
+    hipLaunchKernelGGL(rb_decide_kernel, dim3(1), dim3(1), 0, s, st, cells);
 }
 
 // ---------------------------------------------------------------------------

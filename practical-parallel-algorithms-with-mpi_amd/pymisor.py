@@ -22,6 +22,7 @@ P, RHS, U, V, F, G = range(6)
 NOSLIP, SLIP, OUTFLOW, PERIODIC = 1, 2, 3, 4
 PROBLEM_NONE, PROBLEM_DCAVITY, PROBLEM_CANAL = 0, 1, 2
 SOLVE_RB, SOLVE_RBA = 0, 1
+TUNE_SWEEP_VARIANT, TUNE_ROWS_PER_BLOCK, TUNE_XCD_REMAP = 1, 2, 3
 COMM_ID_BYTES = 128
 
 _dp = C.POINTER(C.c_double)
@@ -80,6 +81,8 @@ SIGNATURES = {
     "misor_normalize_pressure": (C.c_int, [C.c_void_p]),
     "misor_adapt_uv": (C.c_int, [C.c_void_p]),
     "misor_max_uv": (C.c_int, [C.c_void_p, _dp, _dp]),
+    "misor_set_tuning": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
+    "misor_get_tuning": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_int)]),
     "misor_enable_timing": (C.c_int, [C.c_void_p, C.c_int]),
     "misor_get_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
     "misor_reset_stats": (C.c_int, [C.c_void_p]),
@@ -224,6 +227,15 @@ class Grid:
 
     def call(self, name):
         _check(getattr(lib(), "misor_" + name)(self.h))
+
+    # ---- tuning (launch geometry only; results are bit-identical)
+    def set_tuning(self, key, value):
+        _check(lib().misor_set_tuning(self.h, key, value))
+
+    def get_tuning(self, key):
+        v = C.c_int(0)
+        _check(lib().misor_get_tuning(self.h, key, C.byref(v)))
+        return v.value
 
     # ---- stats
     def enable_timing(self, on=True):

@@ -633,6 +633,10 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
     const double cells = (double)g->desc.imax * (double)g->desc.jmax;
     const int cur0 = g->cur;
     long long launched = 0;
+    if (g->dist) {  // the halo-ring red updates read rhs one cell outside the block
+        int rc = exchange(g, g->fld[kRhs], 1);
+        if (rc) return rc;
+    }
     int batch = g->last_iters > 8 ? g->last_iters : 8;
     for (;;) {
         if (batch > itermax - launched) batch = (int)(itermax - launched);

@@ -1,0 +1,186 @@
+"""Parity of the HIP Navier-Stokes step kernels with
+assignment-5/sequential/src/solver.c, and of whole NS runs with the composed
+red-black NS oracle (the sequential solver with assignment-4's
+solveRB as the pressure solve).
+
+Per-cell kernels (BCs, computeFG, computeRHS, adaptUV, the dt reduction) are
+bit-exact.  normalizePressure's mean depends on the summation order; it is
+checked to 1e-15 relative, and whole runs to the north-star bar: the same
+pressure-iteration count in every time step and p/u/v within 1e-12 relative
+(max-norm, relative to max |field|).
+"""
+import itertools
+import os
+import threading
+
+import numpy as np
+import pytest
+
+import ns_gpu_driver as D
+import orc
+import pymisor as M
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = (("p", M.P), ("rhs", M.RHS), ("u", M.U), ("v", M.V), ("f", M.F), ("g", M.G))
+
+
+def par(golden, name, **over):
+    prm = orc.read_par(os.path.join(golden, name))
+    prm.update(over)
+    return prm
+
+
+def random_state(prm, seed):
+    rng = np.random.default_rng(seed)
+    shape = (prm["jmax"] + 2, prm["imax"] + 2)
+    return {k: rng.standard_normal(shape) for k, _ in FIELDS}
+
+
+def load_both(prm, state, dt):
+    ns = orc.NS(prm)
+    for k, _ in FIELDS:
+        getattr(ns, k)[...] = state[k]
+    ns.s.dt = dt
+    g = D.ns_grid(prm)
+    for k, fid in FIELDS:
+        g.upload(fid, state[k])
+    g.set_dt(dt)
+    return ns, g
+
+
+def assert_fields(ns, g, names, rtol=0.0):
+    for k, fid in FIELDS:
+        if k not in names:
+            continue
+        got, want = g.download(fid), getattr(ns, k)
+        if rtol == 0.0:
+            assert np.array_equal(got, want), (k, np.argwhere(got != want)[:4])
+        else:
+            assert np.abs(got - want).max() <= rtol * np.abs(want).max(), k
+
+
+BCS = list(itertools.product((1, 2, 3), repeat=2))
+
+
+@pytest.mark.parametrize("lr,bt", [(BCS[k], BCS[(3 * k + 1) % 9]) for k in range(9)])
+@pytest.mark.parametrize("name", ["a6_dcavity.par", "a6_canal.par"])
+def test_boundary_conditions_bitwise(golden, name, lr, bt):
+    prm = par(golden, name, imax=37, jmax=23, bcLeft=lr[0], bcRight=lr[1], bcBottom=bt[0],
+              bcTop=bt[1])
+    ns, g = load_both(prm, random_state(prm, 7), 0.01)
+    ns.call("set_bc")
+    g.call("set_boundary_conditions")
+    assert_fields(ns, g, ("u", "v"))
+    ns.call("set_special_bc")
+    g.call("set_special_boundary_condition")
+    assert_fields(ns, g, ("u", "v"))
+    g.close()
+
+
+@pytest.mark.parametrize("ni,nj", [(37, 23), (128, 128), (200, 50), (513, 70)])
+def test_fg_rhs_adapt_bitwise(golden, ni, nj):
+    prm = par(golden, "a6_canal.par", imax=ni, jmax=nj)
+    ns, g = load_both(prm, random_state(prm, ni + nj), 0.0137)
+    ns.call("compute_fg")
+    g.call("compute_fg")
+    assert_fields(ns, g, ("f", "g", "u", "v"))
+    ns.call("compute_rhs")
+    g.call("compute_rhs")
+    assert_fields(ns, g, ("rhs",))
+    ns.call("adapt_uv")
+    g.call("adapt_uv")
+    assert_fields(ns, g, ("u", "v"))
+    g.close()
+
+
+def test_timestep_and_normalize(golden):
+    prm = par(golden, "a6_dcavity.par", imax=300, jmax=211)
+    st = random_state(prm, 3)
+    st["u"] *= 3.0
+    ns, g = load_both(prm, st, 0.02)
+    ns.call("compute_timestep")
+    dt = g.compute_timestep(ns.s.dtBound, prm["tau"])
+    assert dt == ns.s.dt  # max is order-independent: exact
+    umax, vmax = g.max_uv()
+    assert umax == orc.lib().orc_ns_max_element(ns.s, orc._ptr(ns.u))
+    assert vmax == orc.lib().orc_ns_max_element(ns.s, orc._ptr(ns.v))
+    ns.call("normalize_pressure")
+    g.call("normalize_pressure")
+    assert np.abs(g.download(M.P) - ns.p).max() <= 1e-15 * np.abs(ns.p).max() * 10
+    g.close()
+
+
+def check_run(golden, fixture, parname, nranks=1):
+    z = np.load(os.path.join(golden, fixture))
+    prm = par(golden, parname, te=float(z["te"]))
+    if nranks == 1:
+        g = D.ns_grid(prm)
+        steps, iters, t = D.run(g, prm)
+        fields = {k: g.download(fid) for k, fid in (("p", M.P), ("u", M.U), ("v", M.V))}
+        g.close()
+    else:
+        out = [None] * nranks
+        errs = []
+        cid = ("LOCAL:ns%s%d" % (fixture, nranks)).encode()
+
+        def body(r):
+            try:
+                g = D.ns_grid(prm, nranks=nranks, rank=r, comm_id=cid)
+                res = D.run(g, prm)
+                out[r] = (g.loc, res, {k: g.download(fid)
+                                       for k, fid in (("p", M.P), ("u", M.U), ("v", M.V))})
+                g.close()
+            except BaseException as e:
+                errs.append(repr(e))
+
+        th = [threading.Thread(target=body, args=(r,)) for r in range(nranks)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join(600)
+        assert not errs, errs
+        steps, iters, t = out[0][1]
+        for o in out[1:]:
+            assert o[1][0] == steps and np.array_equal(o[1][1], iters)
+        fields = {}
+        for k in ("p", "u", "v"):
+            glob = np.zeros_like(z[k])
+            for loc, _, f in out:
+                nb = list(loc.neighbours)
+                i0, j0 = (0 if nb[0] < 0 else 1), (0 if nb[2] < 0 else 1)
+                i1 = loc.ni + 1 if nb[1] < 0 else loc.ni
+                j1 = loc.nj + 1 if nb[3] < 0 else loc.nj
+                glob[loc.joff + j0:loc.joff + j1 + 1, loc.ioff + i0:loc.ioff + i1 + 1] = \
+                    f[k][j0:j1 + 1, i0:i1 + 1]
+            fields[k] = glob
+    assert steps == int(z["steps"])
+    assert np.array_equal(iters, z["iters"]), np.argwhere(iters != z["iters"])[:5]
+    assert abs(t - float(z["t"])) <= 1e-12 * abs(float(z["t"]))
+    for k in ("p", "u", "v"):
+        err = np.abs(fields[k] - z[k]).max() / np.abs(z[k]).max()
+        assert err <= 1e-12, (k, err)
+
+
+def test_dcavity_short_run(golden):
+    check_run(golden, "ns_dcavity_rb_short.npz", "a6_dcavity.par")
+
+
+def test_canal_short_run(golden):
+    check_run(golden, "ns_canal_rb_short.npz", "a6_canal.par")
+
+
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_canal_decomposed(golden, nranks):
+    """BASELINE config 3: canal over 2 and 4 ranks (2x1 / 2x2)"""
+    check_run(golden, "ns_canal_rb_short.npz", "a6_canal.par", nranks)
+
+
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_dcavity_decomposed(golden, nranks):
+    check_run(golden, "ns_dcavity_rb_short.npz", "a6_dcavity.par", nranks)
+
+
+def test_dcavity_full_run(golden):
+    """BASELINE config 2: a6 dcavity.par (2D) to te=10: 4628 steps, 810,389 sweeps"""
+    check_run(golden, "ns_dcavity_rb_full.npz", "a6_dcavity.par")

@@ -164,7 +164,9 @@ int misor_max_uv(misor_grid* g, double* umax, double* vmax);
 enum {
     MISOR_TUNE_SWEEP_VARIANT = 1,  /* 0..7: strips per workgroup x rows in flight x nt stores */
     MISOR_TUNE_ROWS_PER_BLOCK = 2, /* rows one workgroup marches; <= 0: automatic */
-    MISOR_TUNE_XCD_REMAP = 3       /* 1: adjacent blocks on one XCD (shared L2 halos) */
+    MISOR_TUNE_XCD_REMAP = 3,      /* 1: adjacent blocks on one XCD (shared L2 halos) */
+    MISOR_TUNE_SMALL_SOLVE = 4     /* 1 (default): whole solve in one workgroup, p in LDS,
+                                    * when the grid fits (single rank, <= ~140^2) */
 };
 int misor_set_tuning(misor_grid* g, int key, int value);
 int misor_get_tuning(const misor_grid* g, int key, int* value);

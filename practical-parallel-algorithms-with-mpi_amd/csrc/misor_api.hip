@@ -112,6 +112,7 @@ struct misor_grid {
     DevState* st = nullptr;
     DevState* st_host = nullptr;  // pinned
     int last_iters = 0;
+    bool small_solve = true;  // whole-solve LDS kernel when p fits (single rank)
 
     // reductions
     double* red_partials = nullptr;
@@ -631,6 +632,34 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
     HIPCHK(hipMemcpyAsync(g->st, g->st_host, sizeof(DevState), hipMemcpyHostToDevice,
                           g->stream));
     const double cells = (double)g->desc.imax * (double)g->desc.jmax;
+    if (!g->dist && g->small_solve && small_solve_fits(g->loc.ni, g->loc.nj)) {
+        double* p = g->fld[g->cur];
+        if (g->timing) {
+            int rc = ensure_events(g, 2);
+            if (rc) return rc;
+            HIPCHK(hipEventRecord(g->ev[0], g->stream));
+        }
+        launch_solve_small(g->stream, p, g->fld[kRhs], g->loc.ni, g->loc.nj, g->pitch,
+                           g->sp.idx2, g->sp.idy2, g->sp.coef, cells, g->st);
+        HIPCHK(hipGetLastError());
+        if (g->timing) HIPCHK(hipEventRecord(g->ev[1], g->stream));
+        HIPCHK(hipMemcpyAsync(g->st_host, g->st, sizeof(DevState), hipMemcpyDeviceToHost,
+                              g->stream));
+        HIPCHK(hipStreamSynchronize(g->stream));
+        const int it = g->st_host->it;
+        if (g->timing) {
+            float ms = 0.f;
+            HIPCHK(hipEventElapsedTime(&ms, g->ev[0], g->ev[1]));
+            g->stats.sweep_ms += ms;
+            g->stats.timed_sweeps += it;
+        }
+        g->stats.launches += 1;
+        g->stats.sweeps += it;
+        g->last_iters = it;
+        if (iters) *iters = it;
+        if (res) *res = g->st_host->res;
+        return MISOR_OK;
+    }
     const int cur0 = g->cur;
     long long launched = 0;
     if (g->dist) {  // the halo-ring red updates read rhs one cell outside the block
@@ -868,6 +897,7 @@ int misor_set_tuning(misor_grid* g, int key, int value) {
         return configure_sweep(g, g->sp.variant, value, g->sp.xcd_remap);
     case MISOR_TUNE_XCD_REMAP:
         return configure_sweep(g, g->sp.variant, g->sp.rows_per_block, value != 0);
+    case MISOR_TUNE_SMALL_SOLVE: g->small_solve = value != 0; return MISOR_OK;
     default: return fail(MISOR_EINVAL, "unknown tuning key %d", key);
     }
 }
@@ -878,6 +908,7 @@ int misor_get_tuning(const misor_grid* g, int key, int* value) {
     case MISOR_TUNE_SWEEP_VARIANT: *value = g->sp.variant; return MISOR_OK;
     case MISOR_TUNE_ROWS_PER_BLOCK: *value = g->sp.rows_per_block; return MISOR_OK;
     case MISOR_TUNE_XCD_REMAP: *value = g->sp.xcd_remap; return MISOR_OK;
+    case MISOR_TUNE_SMALL_SOLVE: *value = g->small_solve; return MISOR_OK;
     default: return fail(MISOR_EINVAL, "unknown tuning key %d", key);
     }
 }

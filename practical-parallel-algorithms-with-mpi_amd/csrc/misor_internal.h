@@ -90,6 +90,11 @@ void launch_sweep(hipStream_t s, const SweepParams& prm, const double* src, doub
 void launch_finish(hipStream_t s, const double* partials, int nparts, DevState* st,
                    double cells, int decide);
 void launch_decide(hipStream_t s, DevState* st, double cells);
+// whole-solve single-workgroup kernel for grids whose p fits in LDS
+int small_solve_fits(int ni, int nj);
+void launch_solve_small(hipStream_t s, double* p, const double* rhs, int ni, int nj,
+                        long long pitch, double idx2, double idy2, double coef, double cells,
+                        DevState* st);
 
 // 8-neighbour halo exchange of one field (halo.hip): regions in local cell
 // coordinates; direction order L, R, B, T, BL, BR, TL, TR

@@ -384,6 +384,133 @@ void launch_decide(hipStream_t s, DevState* st, double cells) {
 }
 
 // ---------------------------------------------------------------------------
+// Small grids (the NS cases: 128^2 dcavity, 200x50 canal, 100^2 poisson.par):
+// the whole solveRB loop in ONE workgroup, p resident in LDS.
+//
+// At these sizes a sweep moves ~0.4 MB and is pure launch/latency cost on
+// the multi-block path (two launches per iteration); here an iteration is
+// two LDS passes and a block reduction, with no launch and no host round
+// trip until convergence.  In-place red then black pass, exactly solveRB's
+// order of dependencies (assignment-4/src/solver.c:201-217), ghost copy rows
+// then columns (:219-227), res = sum / (imax*jmax) and the same loop test.
+// Each thread owns fixed (red, black) cell pairs, so its rhs values stay in
+// registers for the whole solve.
+// ---------------------------------------------------------------------------
+constexpr int kSmallThreads = 1024;
+constexpr int kSmallMaxPairs = 8;  // pairs per thread (128^2: exactly 8)
+
+int small_solve_fits(int ni, int nj) {
+    const long long cells = (long long)(ni + 2) * (nj + 2);
+    const long long pairs = (long long)nj * ((ni + 1) / 2);
+    return cells * 8 + 256 <= 160 * 1024 && pairs <= (long long)kSmallThreads * kSmallMaxPairs;
+}
+
+__global__ __launch_bounds__(kSmallThreads) void rb_solve_small_kernel(
+    double* __restrict__ p_glob, const double* __restrict__ rhs_glob, int ni, int nj,
+    long long pitch, double idx2, double idy2, double coef, double cells, DevState* st) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    double* red = lds;          // 16 wave partials + broadcast slot
+    double* P = lds + 32;       // (ni+2) x (nj+2), row stride ni+2
+    const int W = ni + 2;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const long long ncell = (long long)W * (nj + 2);
+
+    for (long long k = t; k < ncell; k += kSmallThreads) {
+        const int i = (int)(k % W), j = (int)(k / W);
+        P[k] = p_glob[(long long)(j + kYOff) * pitch + (i + kXOff)];
+    }
+    // this thread's pairs: pair e covers columns 1+2m, 2+2m of row 1 + e / half
+    const int half = (ni + 1) / 2;
+    const int npairs = nj * half;
+    int ci[kSmallMaxPairs][2];  // LDS index of (colour-0 cell, colour-1 cell), -1: none
+    double rh[kSmallMaxPairs][2];
+#pragma unroll
+    for (int m = 0; m < kSmallMaxPairs; ++m) {
+        const int e = t + m * kSmallThreads;
+        ci[m][0] = ci[m][1] = -1;
+        rh[m][0] = rh[m][1] = 0.0;
+        if (e < npairs) {
+            const int j = 1 + e / half, i0 = 1 + 2 * (e % half);
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                // colour c cell of this pair: (i + j) & 1 == c
+                const int i = ((i0 + j) & 1) == c ? i0 : i0 + 1;
+                if (i <= ni) {
+                    ci[m][c] = j * W + i;
+                    rh[m][c] = rhs_glob[(long long)(j + kYOff) * pitch + (i + kXOff)];
+                }
+            }
+        }
+    }
+    __syncthreads();
+
+    const double epssq = st->epssq;
+    const int itermax = st->itermax;
+    double res = 1.0;
+    int it = 0;
+    while ((res >= epssq) && (it < itermax)) {
+        double acc = 0.0;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+#pragma unroll
+            for (int m = 0; m < kSmallMaxPairs; ++m) {
+                const int k = ci[m][c];
+                if (k >= 0) {
+                    const double cc = P[k];
+                    const double r = rh[m][c] - (((P[k + 1] - 2.0 * cc) + P[k - 1]) * idx2 +
+                                                 ((P[k + W] - 2.0 * cc) + P[k - W]) * idy2);
+                    P[k] = cc - coef * r;
+                    acc += r * r;
+                }
+            }
+            __syncthreads();
+        }
+        // Neumann ghost copy: rows, then columns (corners untouched)
+        for (int i = 1 + t; i <= ni; i += kSmallThreads) {
+            P[i] = P[W + i];
+            P[(nj + 1) * W + i] = P[nj * W + i];
+        }
+        __syncthreads();
+        for (int j = 1 + t; j <= nj; j += kSmallThreads) {
+            P[j * W] = P[j * W + 1];
+            P[j * W + ni + 1] = P[j * W + ni];
+        }
+        // fixed-order block sum of r^2
+        acc = wave_sum(acc);
+        if (lane == 0) red[wave] = acc;
+        __syncthreads();
+        if (t == 0) {
+            double s = 0.0;
+            for (int w = 0; w < kSmallThreads / 64; ++w) s += red[w];
+            red[16] = s;
+        }
+        __syncthreads();
+        res = red[16] / cells;
+        ++it;
+    }
+
+    for (long long k = t; k < ncell; k += kSmallThreads) {
+        const int i = (int)(k % W), j = (int)(k / W);
+        p_glob[(long long)(j + kYOff) * pitch + (i + kXOff)] = P[k];
+    }
+    if (t == 0) {
+        st->it = it;
+        st->res = res;
+        st->done = 1;
+    }
+}
+
+void launch_solve_small(hipStream_t s, double* p, const double* rhs, int ni, int nj,
+                        long long pitch, double idx2, double idy2, double coef, double cells,
+                        DevState* st) {
+    const size_t lds = sizeof(double) * (32 + (size_t)(ni + 2) * (nj + 2));
+    (void)hipFuncSetAttribute((const void*)rb_solve_small_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL(rb_solve_small_kernel, dim3(1), dim3(kSmallThreads), lds, s, p, rhs, ni,
+                       nj, pitch, idx2, idy2, coef, cells, st);
+}
+
+// ---------------------------------------------------------------------------
 // Field initialisation
 // ---------------------------------------------------------------------------
 

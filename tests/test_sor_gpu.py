@@ -20,8 +20,15 @@ OMEGA, EPS = 1.9, 1e-6
 
 
 def make_grid(ni, nj, xl=1.0, yl=1.0, omega=OMEGA, eps=EPS, itermax=1000000,
-              variant=M.SOLVE_RB):
-    return M.Grid(ni, nj, xl / ni, yl / nj, omega, eps, itermax, variant=variant)
+              variant=M.SOLVE_RB, small=1):
+    g = M.Grid(ni, nj, xl / ni, yl / nj, omega, eps, itermax, variant=variant)
+    # small=1: whole-solve LDS kernel where the grid fits; 0: always the
+    # multi-block sweep path (both must match the reference)
+    g.set_tuning(M.TUNE_SMALL_SOLVE, small)
+    return g
+
+
+PATHS = pytest.mark.parametrize("small", [1, 0], ids=["lds", "blocks"])
 
 
 def test_poisson_init_bitwise():
@@ -35,7 +42,8 @@ def test_poisson_init_bitwise():
             assert not g.download(M.RHS).any()
 
 
-def test_sweep_fixtures(golden):
+@PATHS
+def test_sweep_fixtures(golden, small):
     z = np.load(os.path.join(golden, "rb_sweeps.npz"))
     for key in z.files:
         if not key.startswith("geom_"):
@@ -43,7 +51,7 @@ def test_sweep_fixtures(golden):
         ni, nj, xl, yl = z[key]
         ni, nj = int(ni), int(nj)
         for k in (1, 2, 7):
-            with make_grid(ni, nj, xl, yl, eps=1e-300) as g:
+            with make_grid(ni, nj, xl, yl, eps=1e-300, small=small) as g:
                 g.poisson_init(xl, yl, 2)
                 it, res = g.solve_rb(itermax=k)
                 assert it == k
@@ -52,9 +60,10 @@ def test_sweep_fixtures(golden):
                 assert np.array_equal(got, want), (ni, nj, k, np.abs(got - want).max())
 
 
-def test_poisson_par_converges_like_reference(golden):
+@PATHS
+def test_poisson_par_converges_like_reference(golden, small):
     z = np.load(os.path.join(golden, "rb_poisson100.npz"))
-    with make_grid(100, 100) as g:
+    with make_grid(100, 100, small=small) as g:
         g.poisson_init(1.0, 1.0, 2)
         it, res = g.solve_rb()
         assert it == int(z["iterations"]) == 2388
@@ -62,7 +71,8 @@ def test_poisson_par_converges_like_reference(golden):
         assert res < EPS * EPS
 
 
-def test_iteration_kats(golden):
+@PATHS
+def test_iteration_kats(golden, small):
     kat = json.load(open(os.path.join(golden, "rb_kat.json")))["iterations"]
     for key, want in kat.items():
         if "x" in key:
@@ -71,17 +81,18 @@ def test_iteration_kats(golden):
             ni = nj = int(key)
         if ni * nj > 130 * 130:
             continue  # 200^2 takes 8.7k sweeps; covered by the CPU KAT test
-        with make_grid(ni, nj) as g:
+        with make_grid(ni, nj, small=small) as g:
             g.poisson_init(1.0, 1.0, 2)
             it, _ = g.solve_rb()
             assert it == want, (key, it, want)
 
 
-def test_rba_variant():
+@PATHS
+def test_rba_variant(small):
     ni, nj = 64, 48
     p, rhs = orc.poisson_init(ni, nj)
     it_ref, res_ref = orc.solve_rb(p, rhs, 1.0 / ni, 1.0 / nj, OMEGA, EPS, 100000, "rba")
-    with make_grid(ni, nj, variant=M.SOLVE_RBA) as g:
+    with make_grid(ni, nj, variant=M.SOLVE_RBA, small=small) as g:
         g.poisson_init(1.0, 1.0, 2)
         it, res = g.solve_rb()
         assert it == it_ref
@@ -93,7 +104,8 @@ def test_rba_variant():
                                      (129, 33, 4), (255, 17, 2), (256, 300, 3),
                                      (511, 40, 3), (512, 65, 2), (513, 513, 3),
                                      (1000, 777, 2), (2049, 130, 2)])
-def test_random_fields_vs_oracle(ni, nj, k):
+@PATHS
+def test_random_fields_vs_oracle(ni, nj, k, small):
     rng = np.random.default_rng(ni * 7919 + nj)
     p = rng.standard_normal((nj + 2, ni + 2))
     rhs = rng.standard_normal((nj + 2, ni + 2))
@@ -101,6 +113,7 @@ def test_random_fields_vs_oracle(ni, nj, k):
     want = p.copy()
     it_ref, res_ref = orc.solve_rb(want, rhs, dx, dy, 1.7, 1e-300, k)
     with M.Grid(ni, nj, dx, dy, 1.7, 1e-300, k) as g:
+        g.set_tuning(M.TUNE_SMALL_SOLVE, small)
         g.upload(M.P, p)
         g.upload(M.RHS, rhs)
         it, res = g.solve_rb()
@@ -110,7 +123,8 @@ def test_random_fields_vs_oracle(ni, nj, k):
     assert abs(res - res_ref) <= 1e-12 * abs(res_ref)
 
 
-def test_consecutive_solves_track_buffers():
+@PATHS
+def test_consecutive_solves_track_buffers(small):
     """odd + even + odd iteration counts: the ping-pong buffer bookkeeping"""
     ni, nj = 97, 61
     rng = np.random.default_rng(5)
@@ -118,6 +132,7 @@ def test_consecutive_solves_track_buffers():
     rhs = rng.standard_normal((nj + 2, ni + 2))
     want = p.copy()
     with M.Grid(ni, nj, 1.0 / ni, 1.0 / nj, 1.5, 1e-300, 10) as g:
+        g.set_tuning(M.TUNE_SMALL_SOLVE, small)
         g.upload(M.P, p)
         g.upload(M.RHS, rhs)
         for k in (3, 4, 1, 6):

@@ -165,8 +165,11 @@ enum {
     MISOR_TUNE_SWEEP_VARIANT = 1,  /* 0..7: strips per workgroup x rows in flight x nt stores */
     MISOR_TUNE_ROWS_PER_BLOCK = 2, /* rows one workgroup marches; <= 0: automatic */
     MISOR_TUNE_XCD_REMAP = 3,      /* 1: adjacent blocks on one XCD (shared L2 halos) */
-    MISOR_TUNE_SMALL_SOLVE = 4     /* 1 (default): whole solve in one workgroup, p in LDS,
-                                    * when the grid fits (single rank, <= ~140^2) */
+    MISOR_TUNE_SMALL_SOLVE = 4,    /* 1 (default): whole solve in one workgroup, p in LDS,
+                                    * when the grid fits (single rank, <= 128^2 cells) */
+    MISOR_TUNE_OVERLAP = 5         /* decomposed: 1 (default) = halo exchange and residual
+                                    * all-reduce on a second stream, overlapped with the
+                                    * interior blocks of the sweep; 0 = serial */
 };
 int misor_set_tuning(misor_grid* g, int key, int value);
 int misor_get_tuning(const misor_grid* g, int key, int* value);

@@ -129,6 +129,9 @@ struct misor_grid {
     int nbr[kDirs] = {-1, -1, -1, -1, -1, -1, -1, -1};  // L R B T BL BR TL TR
     HaloPlan plan[3] = {};                               // by halo depth 1, 2
     std::shared_ptr<LocalGroup> local;                   // in-process transport
+    bool overlap = true;            // exchange on cstream while the interior sweeps
+    hipStream_t cstream = nullptr;  // communication stream
+    hipEvent_t ev_s = nullptr, ev_x = nullptr;
     double* sendbuf = nullptr;
     double* recvbuf = nullptr;
 
@@ -204,6 +207,10 @@ void misor_destroy(misor_grid* g) {
     (void)hipHostFree(g->red_host);
     (void)hipFree(g->sendbuf);
     (void)hipFree(g->recvbuf);
+    if (g->cstream) (void)hipStreamSynchronize(g->cstream);
+    if (g->cstream) (void)hipStreamDestroy(g->cstream);
+    if (g->ev_s) (void)hipEventDestroy(g->ev_s);
+    if (g->ev_x) (void)hipEventDestroy(g->ev_x);
     for (auto e : g->ev) (void)hipEventDestroy(e);
     if (g->comm) ncclCommDestroy(g->comm);
     if (g->own_stream && g->stream) (void)hipStreamDestroy(g->stream);
@@ -244,13 +251,14 @@ static void build_plan(misor_grid* g, int d) {
 }
 
 // one 8-neighbour exchange of `field` at depth d over RCCL on the grid stream
-static int exchange(misor_grid* g, double* field, int d) {
+static int exchange(misor_grid* g, double* field, int d, hipStream_t s = nullptr) {
     if (!g->dist) return MISOR_OK;
+    if (!s) s = g->stream;
     const HaloPlan& P = g->plan[d];
-    launch_pack(g->stream, field, g->pitch, P, g->sendbuf);
+    launch_pack(s, field, g->pitch, P, g->sendbuf);
     if (g->local) {
         static const int opposite[kDirs] = {1, 0, 3, 2, 7, 6, 5, 4};
-        HIPCHK(hipStreamSynchronize(g->stream));
+        HIPCHK(hipStreamSynchronize(s));
         g->local->barrier();  // every rank packed
         for (int k = 0; k < kDirs; ++k) {
             if (g->nbr[k] < 0) continue;
@@ -259,10 +267,10 @@ static int exchange(misor_grid* g, double* field, int d) {
             const HaloRegion& rr = P.recv[k];
             HIPCHK(hipMemcpyAsync(g->recvbuf + rr.off, q->sendbuf + sr.off,
                                   sizeof(double) * (size_t)rr.w * rr.h,
-                                  hipMemcpyDeviceToDevice, g->stream));
+                                  hipMemcpyDeviceToDevice, s));
         }
-        launch_unpack(g->stream, field, g->pitch, P, g->recvbuf);
-        HIPCHK(hipStreamSynchronize(g->stream));
+        launch_unpack(s, field, g->pitch, P, g->recvbuf);
+        HIPCHK(hipStreamSynchronize(s));
         g->local->barrier();  // nobody repacks before every copy is done
         HIPCHK(hipGetLastError());
         return MISOR_OK;
@@ -272,25 +280,24 @@ static int exchange(misor_grid* g, double* field, int d) {
         if (g->nbr[k] < 0) continue;
         const size_t ns = (size_t)P.send[k].w * P.send[k].h;
         const size_t nr = (size_t)P.recv[k].w * P.recv[k].h;
-        NCCLCHK(ncclSend(g->sendbuf + P.send[k].off, ns, ncclDouble, g->nbr[k], g->comm,
-                         g->stream));
-        NCCLCHK(ncclRecv(g->recvbuf + P.recv[k].off, nr, ncclDouble, g->nbr[k], g->comm,
-                         g->stream));
+        NCCLCHK(ncclSend(g->sendbuf + P.send[k].off, ns, ncclDouble, g->nbr[k], g->comm, s));
+        NCCLCHK(ncclRecv(g->recvbuf + P.recv[k].off, nr, ncclDouble, g->nbr[k], g->comm, s));
     }
     NCCLCHK(ncclGroupEnd());
-    launch_unpack(g->stream, field, g->pitch, P, g->recvbuf);
+    launch_unpack(s, field, g->pitch, P, g->recvbuf);
     HIPCHK(hipGetLastError());
     return MISOR_OK;
 }
 
 // all-reduce of n <= 4 device doubles (sum or max) across the ranks
-static int allreduce(misor_grid* g, double* dev, int n, int is_max) {
+static int allreduce(misor_grid* g, double* dev, int n, int is_max, hipStream_t s = nullptr) {
     if (!g->dist) return MISOR_OK;
+    if (!s) s = g->stream;
     if (g->local) {
         LocalGroup& G = *g->local;
         double v[4];
-        HIPCHK(hipMemcpyAsync(v, dev, sizeof(double) * n, hipMemcpyDeviceToHost, g->stream));
-        HIPCHK(hipStreamSynchronize(g->stream));
+        HIPCHK(hipMemcpyAsync(v, dev, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
         const int r = g->desc.rank;
         for (int k = 0; k < n; ++k) G.vals[4 * r + k] = v[k];
         G.barrier();
@@ -303,12 +310,11 @@ static int allreduce(misor_grid* g, double* dev, int n, int is_max) {
             v[k] = a;
         }
         G.barrier();
-        HIPCHK(hipMemcpyAsync(dev, v, sizeof(double) * n, hipMemcpyHostToDevice, g->stream));
-        HIPCHK(hipStreamSynchronize(g->stream));
+        HIPCHK(hipMemcpyAsync(dev, v, sizeof(double) * n, hipMemcpyHostToDevice, s));
+        HIPCHK(hipStreamSynchronize(s));
         return MISOR_OK;
     }
-    NCCLCHK(ncclAllReduce(dev, dev, n, ncclDouble, is_max ? ncclMax : ncclSum, g->comm,
-                          g->stream));
+    NCCLCHK(ncclAllReduce(dev, dev, n, ncclDouble, is_max ? ncclMax : ncclSum, g->comm, s));
     return MISOR_OK;
 }
 
@@ -363,7 +369,9 @@ int misor_create(misor_grid** out, const misor_desc* d) {
     g->desc = *d;
     g->desc.nranks = nranks;
     g->loc = L;
-    g->dist = nranks > 1;
+    // a comm id with nranks == 1 still runs the decomposed code path (one rank, no
+    // neighbours): lets the RCCL / overlap machinery be exercised on one GPU
+    g->dist = nranks > 1 || d->comm_id != nullptr;
     if (d->device >= 0) {
         g->device = d->device;
         if (hipSetDevice(g->device) != hipSuccess) {
@@ -442,6 +450,17 @@ int misor_create(misor_grid** out, const misor_desc* d) {
         for (int k = 0; k < kDirs; ++k) g->nbr[k] = nbrs[k];
         build_plan(g, 1);
         build_plan(g, 2);
+        if (hipStreamCreateWithFlags(&g->cstream, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&g->ev_s, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&g->ev_x, hipEventDisableTiming) != hipSuccess)
+            CREATE_FAIL(MISOR_EHIP, "comm stream/event creation failed");
+        // blocks whose footprint (rows j0-2..j1+1, columns c0-2..c_end+1) stays clear
+        // of the halo on neighbour sides AND of the 2-deep send region can sweep
+        // while the exchange is in flight
+        sp.int_lo_i = L.neighbours[0] >= 0 ? 3 : -1000000000;
+        sp.int_hi_i = L.neighbours[1] >= 0 ? L.ni - 2 : 2000000000;
+        sp.int_lo_j = L.neighbours[2] >= 0 ? 3 : -1000000000;
+        sp.int_hi_j = L.neighbours[3] >= 0 ? L.nj - 2 : 2000000000;
         const size_t hb = (size_t)(g->plan[2].total > 0 ? g->plan[2].total : 1) * sizeof(double);
         if (hipMalloc(&g->sendbuf, hb) != hipSuccess || hipMalloc(&g->recvbuf, hb) != hipSuccess)
             CREATE_FAIL(MISOR_ENOMEM, "halo buffer allocation failed");
@@ -674,7 +693,46 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
             int rc = ensure_events(g, 2 * (size_t)batch);
             if (rc) return rc;
         }
-        for (int b = 0; b < batch; ++b) {
+        for (int b = 0; b < batch && g->dist && g->overlap; ++b) {
+            // Overlapped iteration k.  comm stream: [wait sweep k-1] all-reduce and
+            // decide of k-1, 2-deep exchange of src_k.  compute stream: interior
+            // blocks of sweep k (no halo reads) meanwhile, then [wait exchange]
+            // boundary blocks, partial sum.  An interior pass launched after
+            // convergence (decide k-1 still in flight) only writes the buffer that
+            // is not the result; every other kernel sees `done` in stream order.
+            const long long k = launched + b;
+            const double* src = g->fld[kP0 + ((cur0 + k) & 1)];
+            double* dst = g->fld[kP0 + ((cur0 + k + 1) & 1)];
+            HIPCHK(hipEventRecord(g->ev_s, g->stream));
+            HIPCHK(hipStreamWaitEvent(g->cstream, g->ev_s, 0));
+            if (b > 0) {  // iteration k-1 of this batch (the previous batch closed its own)
+                int rc = allreduce(g, &g->st->sum, 1, 0, g->cstream);
+                if (rc) return rc;
+                launch_decide(g->cstream, g->st, cells);
+            }
+            int rc = exchange(g, const_cast<double*>(src), 2, g->cstream);
+            if (rc) return rc;
+            HIPCHK(hipEventRecord(g->ev_x, g->cstream));
+            if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b], g->stream));
+            SweepParams sp = g->sp;
+            sp.part = 1;
+            launch_sweep(g->stream, sp, src, dst, g->fld[kRhs], g->partials, g->st);
+            HIPCHK(hipStreamWaitEvent(g->stream, g->ev_x, 0));
+            sp.part = 2;
+            launch_sweep(g->stream, sp, src, dst, g->fld[kRhs], g->partials, g->st);
+            if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b + 1], g->stream));
+            launch_finish(g->stream, g->partials, g->nparts, g->st, cells, 0);
+            if (b == batch - 1) {  // close the batch: all-reduce + decide of the last one
+                HIPCHK(hipEventRecord(g->ev_s, g->stream));
+                HIPCHK(hipStreamWaitEvent(g->cstream, g->ev_s, 0));
+                rc = allreduce(g, &g->st->sum, 1, 0, g->cstream);
+                if (rc) return rc;
+                launch_decide(g->cstream, g->st, cells);
+                HIPCHK(hipEventRecord(g->ev_x, g->cstream));
+                HIPCHK(hipStreamWaitEvent(g->stream, g->ev_x, 0));
+            }
+        }
+        for (int b = 0; b < batch && !(g->dist && g->overlap); ++b) {
             const long long k = launched + b;
             const double* src = g->fld[kP0 + ((cur0 + k) & 1)];
             double* dst = g->fld[kP0 + ((cur0 + k + 1) & 1)];
@@ -898,6 +956,7 @@ int misor_set_tuning(misor_grid* g, int key, int value) {
     case MISOR_TUNE_XCD_REMAP:
         return configure_sweep(g, g->sp.variant, g->sp.rows_per_block, value != 0);
     case MISOR_TUNE_SMALL_SOLVE: g->small_solve = value != 0; return MISOR_OK;
+    case MISOR_TUNE_OVERLAP: g->overlap = value != 0; return MISOR_OK;
     default: return fail(MISOR_EINVAL, "unknown tuning key %d", key);
     }
 }
@@ -909,6 +968,7 @@ int misor_get_tuning(const misor_grid* g, int key, int* value) {
     case MISOR_TUNE_ROWS_PER_BLOCK: *value = g->sp.rows_per_block; return MISOR_OK;
     case MISOR_TUNE_XCD_REMAP: *value = g->sp.xcd_remap; return MISOR_OK;
     case MISOR_TUNE_SMALL_SOLVE: *value = g->small_solve; return MISOR_OK;
+    case MISOR_TUNE_OVERLAP: *value = g->overlap; return MISOR_OK;
     default: return fail(MISOR_EINVAL, "unknown tuning key %d", key);
     }
 }

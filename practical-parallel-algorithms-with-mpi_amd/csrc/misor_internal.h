@@ -74,6 +74,8 @@ struct SweepParams {
     int variant;         // index into kSweepVariants
     int nbx, nblocks;    // launch geometry (logical blocks nbx x nby)
     int xcd_remap;       // deal consecutive logical blocks to one XCD
+    int part;            // 0: all blocks, 1: interior blocks only, 2: boundary blocks only
+    int int_lo_i, int_hi_i, int_lo_j, int_hi_j;  // footprint bounds of an interior block
     double idx2, idy2, coef;  // 1/dx^2, 1/dy^2, factor (RB) or omega*factor (RBA)
 };
 

@@ -87,6 +87,15 @@ __global__ __launch_bounds__(kLanes* WAVES) void rb_sweep_kernel(
         L = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + L / 8;
     }
     const int bx = L % prm.nbx, by = L / prm.nbx;
+    if (prm.part != 0) {  // overlapped decomposed sweep: interior / boundary split
+        const int c0b = 1 + bx * WAVES * kStripCells;
+        const int j0b = 1 + by * prm.rows_per_block;
+        const int j1b = min(j0b + prm.rows_per_block, prm.nj + 1);
+        const bool interior = (c0b - 2 >= prm.int_lo_i) &&
+                              (c0b + WAVES * kStripCells + 1 <= prm.int_hi_i) &&
+                              (j0b - 2 >= prm.int_lo_j) && (j1b + 1 <= prm.int_hi_j);
+        if (interior != (prm.part == 1)) return;  // the other launch owns this block
+    }
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;

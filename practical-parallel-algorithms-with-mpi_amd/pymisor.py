@@ -22,7 +22,8 @@ P, RHS, U, V, F, G = range(6)
 NOSLIP, SLIP, OUTFLOW, PERIODIC = 1, 2, 3, 4
 PROBLEM_NONE, PROBLEM_DCAVITY, PROBLEM_CANAL = 0, 1, 2
 SOLVE_RB, SOLVE_RBA = 0, 1
-TUNE_SWEEP_VARIANT, TUNE_ROWS_PER_BLOCK, TUNE_XCD_REMAP, TUNE_SMALL_SOLVE = 1, 2, 3, 4
+TUNE_SWEEP_VARIANT, TUNE_ROWS_PER_BLOCK, TUNE_XCD_REMAP, TUNE_SMALL_SOLVE, TUNE_OVERLAP = \
+    1, 2, 3, 4, 5
 COMM_ID_BYTES = 128
 
 _dp = C.POINTER(C.c_double)

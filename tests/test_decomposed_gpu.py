@@ -67,8 +67,9 @@ def assemble(parts, shape):
 
 @pytest.mark.parametrize("world,dims", [(2, (0, 0)), (2, (1, 2)), (3, (0, 0)), (4, (0, 0)),
                                         (4, (1, 4)), (6, (0, 0)), (8, (0, 0))])
-@pytest.mark.parametrize("ni,nj,k", [(61, 43, 5), (300, 257, 3)])
-def test_fixed_sweeps_partition_independent(world, dims, ni, nj, k):
+@pytest.mark.parametrize("ni,nj,k", [(61, 43, 5), (300, 257, 3), (2100, 90, 2)])
+@pytest.mark.parametrize("overlap", [1, 0], ids=["overlap", "serial"])
+def test_fixed_sweeps_partition_independent(world, dims, ni, nj, k, overlap):
     rng = np.random.default_rng(ni + 31 * nj + world)
     p = rng.standard_normal((nj + 2, ni + 2))
     rhs = rng.standard_normal((nj + 2, ni + 2)) * 20
@@ -79,6 +80,7 @@ def test_fixed_sweeps_partition_independent(world, dims, ni, nj, k):
     def rank_fn(r, cid, dims):
         with M.Grid(ni, nj, dx, dy, 1.85, 1e-300, k, device=0, nranks=world, rank=r,
                     dims=dims, comm_id=cid) as g:
+            g.set_tuning(M.TUNE_OVERLAP, overlap)
             g.upload(M.P, local_window(p, g.loc))
             g.upload(M.RHS, local_window(rhs, g.loc))
             it, res = g.solve_rb()
@@ -107,3 +109,26 @@ def test_poisson_par_converges_decomposed(golden, world):
     assert all(o[2] == 2388 for o in outs)
     got = assemble([(o[0], o[1]) for o in outs], z["p"].shape)
     assert np.array_equal(got, z["p"])  # corners included: the corner ranks own them
+
+
+def test_rccl_single_rank_path(golden):
+    """nranks=1 with a real RCCL id: the decomposed code path (RCCL init and
+    all-reduce on the comm stream, interior/boundary split launches) on the
+    one GPU of the box -- RCCL cannot put two ranks on one device."""
+    z = np.load(golden + "/rb_poisson100.npz")
+    cid = M.comm_unique_id()
+    with M.Grid(100, 100, 0.01, 0.01, 1.9, 1e-6, 1000000, device=0, nranks=1, rank=0,
+                comm_id=cid) as g:
+        g.poisson_init(1.0, 1.0, 2)
+        it, res = g.solve_rb()
+        assert it == 2388
+        assert np.array_equal(g.download(M.P), z["p"])
+    n = 3000
+    p, rhs = orc.poisson_init(n, n)
+    it_ref, res_ref = orc.solve_rb(p, rhs, 1.0 / n, 1.0 / n, 1.9, 1e-300, 3)
+    with M.Grid(n, n, 1.0 / n, 1.0 / n, 1.9, 1e-300, 3, device=0, nranks=1, rank=0,
+                comm_id=M.comm_unique_id()) as g:
+        g.poisson_init(1.0, 1.0, 2)
+        it, res = g.solve_rb()
+        assert it == 3 and np.array_equal(g.download(M.P), p)
+        assert abs(res - res_ref) <= 1e-12 * res_ref

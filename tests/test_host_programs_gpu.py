@@ -1,0 +1,54 @@
+"""The reference-compatible host programs (C, on libmisor) end to end:
+bin/exe-poisson <par> like assignment-4/src/main.c, bin/exe-ns <par> like
+assignment-5/sequential/src/main.c -- stdout lines, output files, results."""
+import os
+import re
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "practical-parallel-algorithms-with-mpi_amd", "bin")
+
+
+def fmt_pdat(p):  # writeResult, assignment-4/src/solver.c:315-320
+    return "\n".join("".join("%f " % x for x in row) for row in p) + "\n"
+
+
+def test_exe_poisson(golden, tmp_path):
+    shutil.copy(os.path.join(golden, "a4_poisson.par"), tmp_path / "poisson.par")
+    out = subprocess.run([os.path.join(BIN, "exe-poisson"), "poisson.par"], cwd=tmp_path,
+                         capture_output=True, text=True, timeout=120, check=True).stdout
+    assert "Parameters:" in out and "Cells (x, y): 100, 100" in out
+    assert re.search(r"(^|\s)2388 ", out), out
+    assert re.search(r"Walltime \d+\.\d\ds", out)
+    z = np.load(os.path.join(golden, "rb_poisson100.npz"))
+    assert (tmp_path / "p.dat").read_text() == fmt_pdat(z["p"])
+
+
+def test_exe_ns_dcavity(golden, tmp_path):
+    z = np.load(os.path.join(golden, "ns_dcavity_rb_short.npz"))
+    txt = open(os.path.join(golden, "a6_dcavity.par")).read()
+    txt = re.sub(r"(?m)^te .*$", "te       %r" % float(z["te"]), txt)
+    (tmp_path / "dcavity.par").write_text(txt)
+    env = dict(os.environ, MISOR_ITERLOG=str(tmp_path / "iters.log"))
+    out = subprocess.run([os.path.join(BIN, "exe-ns"), "dcavity.par"], cwd=tmp_path, env=env,
+                         capture_output=True, text=True, timeout=300, check=True).stdout
+    assert "Parameters for dcavity" in out and "Solution took" in out
+    log = np.loadtxt(tmp_path / "iters.log")
+    assert len(log) == int(z["steps"])
+    assert np.array_equal(log[:, 3].astype(int), z["iters"])
+    # pressure.dat: "%.2f %.2f %f" per interior cell, blank line after each row
+    pr = np.loadtxt(tmp_path / "pressure.dat")
+    assert pr.shape == (128 * 128, 3)
+    assert np.abs(pr[:, 2] - z["p"][1:-1, 1:-1].ravel()).max() <= 1e-6
+    ve = np.loadtxt(tmp_path / "velocity.dat")
+    u, v = z["u"], z["v"]
+    uc = ((u[1:-1, 1:-1] + u[1:-1, :-2]) / 2.0).ravel()
+    vc = ((v[1:-1, 1:-1] + v[:-2, 1:-1]) / 2.0).ravel()
+    assert np.abs(ve[:, 2] - uc).max() <= 1e-6
+    assert np.abs(ve[:, 3] - vc).max() <= 1e-6

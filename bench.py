@@ -14,13 +14,21 @@ sweeps).  Fields are initialised on the device before the timed
 region; the timed region is K iterations, barrier + device sync on both
 sides, max over ranks.  Rank 0 prints ONE JSON line.
 
+A launch (a "pass") of the default temporally blocked kernel performs T
+complete iterations (sor_tb.hip; T = iters_per_pass, default 3): it reads p
+and rhs once and writes p once per T iterations.
+
 roofline: algorithmic bytes per launch = 24 B per lattice update (read p,
-read rhs, write p: SURVEY 8d) x local cells, divided by the sweep kernel's
-average duration measured with HIP events recorded around every sweep launch
+read rhs, write p: SURVEY 8d) x local cells x T, divided by the kernel's
+average launch duration measured with HIP events recorded around every pass
 on the library's stream (misor_enable_timing).  peak = 8000 GB/s (MI355X HBM3E
-spec, MI355X_MICROARCH.md).  traffic = HBM bytes per launch from the PMC
-profile committed under profiles/ for this configuration (FETCH_SIZE x 2 +
-WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md §HBM), or null.
+spec, MI355X_MICROARCH.md).  Because one launch does T iterations for one
+read/write of the fields, frac can exceed 1: it is the iteration-equivalent
+(algorithmic) rate.  hbm_achieved = the bytes one launch must move (24 B x
+cells, its own minimum) / launch time, i.e. the kernel's real HBM rate.
+traffic = HBM bytes per launch from the PMC profile committed under profiles/
+for this configuration and T (FETCH_SIZE x 2 + WRITE_SIZE, the gfx950
+correction of MI355X_MICROARCH.md §HBM), or null.
 
 cpu_baseline: the reference's own solveRB (assignment-4/src/solver.c:179-238,
 compiled in place by oracle/Makefile into oracle/_ref/libref.so) on one host
@@ -79,15 +87,16 @@ def cpu_baseline(n=8192, sweeps=40):
                       % (n, n, sweeps, solve_s)}
 
 
-def pmc_traffic(size, nranks):
-    """HBM bytes per sweep launch from the committed PMC summary, or None."""
+def pmc_traffic(size, nranks, T):
+    """HBM bytes per launch from the committed PMC summary, or None."""
     best = None
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
         try:
             d = json.load(open(path))
         except Exception:
             continue
-        if d.get("size") == size and d.get("nranks", 1) == nranks and "bytes_per_launch" in d:
+        if (d.get("size") == size and d.get("nranks", 1) == nranks
+                and d.get("iters_per_pass", 1) == T and "bytes_per_launch" in d):
             best = d["bytes_per_launch"]
     return best
 
@@ -95,10 +104,12 @@ def pmc_traffic(size, nranks):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=24)
+    ap.add_argument("--warmup", type=int, default=6)
     ap.add_argument("--size", type=int, default=32768)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--tsteps", type=int, default=0,
+                    help="iterations per kernel launch (0: library default)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -126,6 +137,8 @@ def main():
         comm_id = obj[0]
     g = M.Grid(n, n, 1.0 / n, 1.0 / n, 1.9, 1e-300, args.steps, device=local_rank,
                nranks=world, rank=rank, comm_id=comm_id)
+    if args.tsteps > 0:
+        g.set_tuning(M.TUNE_TSTEPS, args.tsteps)
     g.poisson_init(1.0, 1.0, 2)
     local_cells = g.loc.ni * g.loc.nj
 
@@ -147,17 +160,20 @@ def main():
     st = g.stats()
     assert it == args.steps, (it, args.steps)
 
+    T = st["iters_per_pass"]
     if dist is not None:
-        tt = torch.tensor([elapsed, st["sweep_ms"] / max(st["timed_sweeps"], 1)],
+        tt = torch.tensor([elapsed, st["sweep_ms"] / max(st["timed_passes"], 1)],
                           dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = tt.tolist()
     else:
-        kern_ms = st["sweep_ms"] / max(st["timed_sweeps"], 1)
+        kern_ms = st["sweep_ms"] / max(st["timed_passes"], 1)  # per launch (pass)
 
     total_lup = float(n) * float(n) * args.steps
     mlups = total_lup / elapsed / 1e6
-    achieved = BYTES_PER_LUP * local_cells / (kern_ms * 1e-3) / 1e9  # GB/s per GPU
+    bytes_launch = BYTES_PER_LUP * local_cells * T
+    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9  # GB/s per GPU, algorithmic
+    hbm_achieved = BYTES_PER_LUP * local_cells / (kern_ms * 1e-3) / 1e9
     dims = "%dx%d" % tuple(g.loc.dims)
     out = {
         "metric": "red-black SOR MLUP/s + % HBM roofline at 1/2/4/8 MI355X, 32768^2 grid",
@@ -173,14 +189,18 @@ def main():
         "dtype": "f64",
         "data": "synthetic (assignment-4 problem-2 fields, generated on device)",
         "config": {"workload": "2D Poisson red-black SOR (solveRB), %dx%d interior cells, "
-                               "fixed %d sweeps per timed region, 1 sweep = 1 step" % (n, n, args.steps),
+                               "fixed %d iterations per timed region, 1 iteration = 1 step, "
+                               "%d iterations per kernel launch" % (n, n, args.steps, T),
                    "imax": n, "jmax": n, "omega": 1.9, "problem": 2,
                    "decomposition": dims, "baseline_config": 4},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / PEAK_GBS, 4),
-                     "traffic": pmc_traffic(n, world),
-                     "kernel": "rb_sweep_kernel", "kernel_ms": round(kern_ms, 4),
-                     "bytes_per_launch": BYTES_PER_LUP * local_cells},
+                     "traffic": pmc_traffic(n, world, T),
+                     "kernel": "rb_tb_kernel" if T > 1 else "rb_sweep_kernel",
+                     "iters_per_launch": T, "kernel_ms": round(kern_ms, 4),
+                     "bytes_per_launch": bytes_launch,
+                     "hbm_achieved": round(hbm_achieved, 1),
+                     "hbm_frac": round(hbm_achieved / PEAK_GBS, 4)},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:

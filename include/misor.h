@@ -98,12 +98,18 @@ typedef struct {
 } misor_local;
 
 /* per-grid counters; sweep_ms is summed from HIP events recorded around
- * every sweep kernel when timing is enabled (misor_enable_timing) */
+ * every sweep pass when timing is enabled (misor_enable_timing).  A pass is
+ * one sweep kernel launch (two for an overlapped decomposed pass: interior
+ * blocks, then boundary blocks) doing iters_per_pass red+black iterations
+ * (MISOR_TUNE_TSTEPS). */
 typedef struct {
     long long sweeps;       /* red+black iterations executed on the device */
-    long long launches;     /* sweep kernels launched (incl. early-exited) */
-    double sweep_ms;        /* total device time of sweep kernels (timing on) */
-    long long timed_sweeps; /* launches covered by sweep_ms */
+    long long launches;     /* passes launched (incl. early-exited) */
+    double sweep_ms;        /* total device time of timed passes (timing on) */
+    long long timed_sweeps; /* iterations computed by the timed passes */
+    long long timed_passes; /* passes covered by sweep_ms */
+    int iters_per_pass;     /* T of the last multi-block solve (1: single sweep) */
+    int pad_;
 } misor_stats;
 
 const char* misor_last_error(void);
@@ -167,9 +173,15 @@ enum {
     MISOR_TUNE_XCD_REMAP = 3,      /* 1: adjacent blocks on one XCD (shared L2 halos) */
     MISOR_TUNE_SMALL_SOLVE = 4,    /* 1 (default): whole solve in one workgroup, p in LDS,
                                     * when the grid fits (single rank, <= 128^2 cells) */
-    MISOR_TUNE_OVERLAP = 5         /* decomposed: 1 (default) = halo exchange and residual
+    MISOR_TUNE_OVERLAP = 5,        /* decomposed: 1 (default) = halo exchange and residual
                                     * all-reduce on a second stream, overlapped with the
                                     * interior blocks of the sweep; 0 = serial */
+    MISOR_TUNE_TSTEPS = 6,         /* iterations per pass over HBM, 1..4: 1 = single-
+                                    * iteration sweep kernel, T >= 2 = temporally blocked
+                                    * kernel (T iterations per read of p and rhs); the
+                                    * iteration count and every bit of p are unchanged */
+    MISOR_TUNE_TB_VARIANT = 7,     /* temporally blocked kernel: 0..3 strips x rows in flight */
+    MISOR_TUNE_TB_ROWS = 8         /* temporally blocked kernel: rows per block; <= 0: auto */
 };
 int misor_set_tuning(misor_grid* g, int key, int value);
 int misor_get_tuning(const misor_grid* g, int key, int* value);

@@ -2,6 +2,7 @@
 // the solve loop (batched launches with a device-resident convergence flag),
 // the NS step entry points and the 2D decomposition over RCCL.
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -114,6 +115,12 @@ struct misor_grid {
     int last_iters = 0;
     bool small_solve = true;  // whole-solve LDS kernel when p fits (single rank)
 
+    // temporally blocked sweep (sor_tb.hip): T iterations per pass over HBM
+    int tsteps = kDefaultTsteps;  // requested T (1: single-iteration kernel)
+    SweepParams tp{};             // its launch geometry (for T = tsteps)
+    int tb_nparts = 0;
+    int tb_rows_req = 0;          // MISOR_TUNE_TB_ROWS (0: automatic)
+
     // reductions
     double* red_partials = nullptr;
     double* red_out = nullptr;   // 4 doubles on device
@@ -127,11 +134,12 @@ struct misor_grid {
     bool dist = false;
     ncclComm_t comm = nullptr;
     int nbr[kDirs] = {-1, -1, -1, -1, -1, -1, -1, -1};  // L R B T BL BR TL TR
-    HaloPlan plan[3] = {};                               // by halo depth 1, 2
+    HaloPlan plan[2 * kMaxT + 1] = {};                   // by halo depth 1 .. 2*kMaxT
+    int max_depth = 2;                                   // deepest plan built
     std::shared_ptr<LocalGroup> local;                   // in-process transport
     bool overlap = true;            // exchange on cstream while the interior sweeps
     hipStream_t cstream = nullptr;  // communication stream
-    hipEvent_t ev_s = nullptr, ev_x = nullptr;
+    hipEvent_t ev_s = nullptr, ev_x = nullptr, ev_d = nullptr;
     double* sendbuf = nullptr;
     double* recvbuf = nullptr;
 
@@ -211,6 +219,7 @@ void misor_destroy(misor_grid* g) {
     if (g->cstream) (void)hipStreamDestroy(g->cstream);
     if (g->ev_s) (void)hipEventDestroy(g->ev_s);
     if (g->ev_x) (void)hipEventDestroy(g->ev_x);
+    if (g->ev_d) (void)hipEventDestroy(g->ev_d);
     for (auto e : g->ev) (void)hipEventDestroy(e);
     if (g->comm) ncclCommDestroy(g->comm);
     if (g->own_stream && g->stream) (void)hipStreamDestroy(g->stream);
@@ -331,6 +340,17 @@ static int pick_rows_per_block(int ni, int nj, int waves) {
     return h;
 }
 
+static int ensure_partials(misor_grid* g, int n) {
+    if (n <= g->partials_cap) return MISOR_OK;
+    if (g->partials) (void)hipFree(g->partials);
+    g->partials = nullptr;
+    g->partials_cap = 0;
+    if (hipMalloc(&g->partials, sizeof(double) * n) != hipSuccess)
+        return fail(MISOR_ENOMEM, "partials allocation failed");
+    g->partials_cap = n;
+    return MISOR_OK;
+}
+
 // (re)derive the sweep launch geometry; partials are sized for the largest
 static int configure_sweep(misor_grid* g, int variant, int rows, int remap) {
     if (variant < 0 || variant >= kNumSweepVariants) return fail(MISOR_EINVAL, "bad variant");
@@ -345,14 +365,56 @@ static int configure_sweep(misor_grid* g, int variant, int rows, int remap) {
     g->nby = nby;
     sp.nbx = g->nbx;
     sp.nblocks = g->nparts;
-    if (g->nparts > g->partials_cap) {
-        if (g->partials) (void)hipFree(g->partials);
-        g->partials = nullptr;
-        if (hipMalloc(&g->partials, sizeof(double) * g->nparts) != hipSuccess)
-            return fail(MISOR_ENOMEM, "partials allocation failed");
-        g->partials_cap = g->nparts;
+    g->tp.xcd_remap = remap;
+    return ensure_partials(g, g->nparts);
+}
+
+// T that a multi-block solve uses: the requested one, limited so that the
+// 2T-deep halo of a decomposed run fits inside the smallest neighbour block
+static int effective_tsteps(const misor_grid* g) {
+    int T = g->tsteps;
+    if (T < 1) T = 1;
+    if (T > kMaxT) T = kMaxT;
+    if (g->dist) {
+        const int mi = g->desc.imax / g->loc.dims[0], mj = g->desc.jmax / g->loc.dims[1];
+        while (T > 1 && (2 * T > mi || 2 * T > mj || 2 * T > g->max_depth)) --T;
     }
-    return MISOR_OK;
+    return T;
+}
+
+static int pick_tb_rows(int ni, int nj, int T, int waves) {
+    // long marches amortise the 4T rows each block streams beyond its own
+    // (H + 4T loads for H rows), but keep >= ~2 workgroups per CU
+    const int strips = (ni + tb_out_width(T) - 1) / tb_out_width(T);
+    const int nbx = (strips + waves - 1) / waves;
+    const int target_blocks = 1024;
+    const int want_nby = (target_blocks + nbx - 1) / nbx;
+    int h = (nj + want_nby - 1) / want_nby;
+    if (h < 32 * T) h = 32 * T;
+    if (h > kDefaultTbRows) h = kDefaultTbRows;
+    return h;
+}
+
+// geometry of the temporally blocked pass with T iterations into `tp`
+static void tb_geometry(const misor_grid* g, int T, SweepParams& tp) {
+    const int waves = tb_waves(tp.variant);
+    int nby = 0, nbx = 0;
+    tp.nblocks = tb_partials(g->loc.ni, g->loc.nj, T, tp.rows_per_block, waves, &nbx, &nby);
+    tp.nbx = nbx;
+}
+
+static int configure_tb(misor_grid* g, int T, int variant, int rows) {
+    if (T < 1 || T > kMaxT) return fail(MISOR_EINVAL, "iterations per pass must be 1..%d", kMaxT);
+    if (variant < 0 || variant >= kNumTbVariants) return fail(MISOR_EINVAL, "bad tb variant");
+    g->tsteps = T;
+    SweepParams& tp = g->tp;
+    tp.variant = variant;
+    tp.rows_per_block = rows > 0 ? rows : pick_tb_rows(g->loc.ni, g->loc.nj, T, tb_waves(variant));
+    tp.xcd_remap = g->sp.xcd_remap;
+    const int Te = effective_tsteps(g);
+    tb_geometry(g, Te, tp);
+    g->tb_nparts = tp.nblocks;
+    return ensure_partials(g, Te * tp.nblocks);
 }
 
 int misor_create(misor_grid** out, const misor_desc* d) {
@@ -429,6 +491,23 @@ int misor_create(misor_grid** out, const misor_desc* d) {
         misor_destroy(g);
         return MISOR_ENOMEM;
     }
+    {
+        // temporally blocked pass: same physics, its own geometry; every cell of
+        // a neighbour's 2T-deep halo is updated (identical arithmetic), only the
+        // physical sides are bounded
+        constexpr int kBig = 1 << 29;
+        SweepParams& tp = g->tp;
+        tp = sp;
+        tp.upd_lo_i = sp.ghost_left ? 1 : -kBig;
+        tp.upd_hi_i = sp.ghost_right ? L.ni : kBig;
+        tp.upd_lo_j = sp.ghost_bottom ? 1 : -kBig;
+        tp.upd_hi_j = sp.ghost_top ? L.nj : kBig;
+        // an interior block (overlapped pass) streams no halo cell of src
+        tp.int_lo_i = sp.ghost_left ? -kBig : 1;
+        tp.int_hi_i = sp.ghost_right ? kBig : L.ni;
+        tp.int_lo_j = sp.ghost_bottom ? -kBig : 1;
+        tp.int_hi_j = sp.ghost_top ? kBig : L.nj;
+    }
     if (hipMalloc(&g->st, sizeof(DevState)) != hipSuccess ||
         hipHostMalloc(&g->st_host, sizeof(DevState), hipHostMallocDefault) != hipSuccess)
         CREATE_FAIL(MISOR_ENOMEM, "state allocation failed");
@@ -448,11 +527,14 @@ int misor_create(misor_grid** out, const misor_desc* d) {
                                  at(cx, cy + 1),     at(cx - 1, cy - 1), at(cx + 1, cy - 1),
                                  at(cx - 1, cy + 1), at(cx + 1, cy + 1)};
         for (int k = 0; k < kDirs; ++k) g->nbr[k] = nbrs[k];
-        build_plan(g, 1);
-        build_plan(g, 2);
+        // halo plans up to depth 2*kMaxT, as deep as the smallest block allows
+        const int minb = std::min(d->imax / L.dims[0], d->jmax / L.dims[1]);
+        g->max_depth = std::max(2, std::min(2 * kMaxT, minb));
+        for (int dd = 1; dd <= g->max_depth; ++dd) build_plan(g, dd);
         if (hipStreamCreateWithFlags(&g->cstream, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&g->ev_s, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&g->ev_x, hipEventDisableTiming) != hipSuccess)
+            hipEventCreateWithFlags(&g->ev_x, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&g->ev_d, hipEventDisableTiming) != hipSuccess)
             CREATE_FAIL(MISOR_EHIP, "comm stream/event creation failed");
         // blocks whose footprint (rows j0-2..j1+1, columns c0-2..c_end+1) stays clear
         // of the halo on neighbour sides AND of the 2-deep send region can sweep
@@ -461,7 +543,9 @@ int misor_create(misor_grid** out, const misor_desc* d) {
         sp.int_hi_i = L.neighbours[1] >= 0 ? L.ni - 2 : 2000000000;
         sp.int_lo_j = L.neighbours[2] >= 0 ? 3 : -1000000000;
         sp.int_hi_j = L.neighbours[3] >= 0 ? L.nj - 2 : 2000000000;
-        const size_t hb = (size_t)(g->plan[2].total > 0 ? g->plan[2].total : 1) * sizeof(double);
+        long long maxtot = 1;
+        for (int dd = 1; dd <= g->max_depth; ++dd) maxtot = std::max(maxtot, g->plan[dd].total);
+        const size_t hb = (size_t)maxtot * sizeof(double);
         if (hipMalloc(&g->sendbuf, hb) != hipSuccess || hipMalloc(&g->recvbuf, hb) != hipSuccess)
             CREATE_FAIL(MISOR_ENOMEM, "halo buffer allocation failed");
         if (memcmp(d->comm_id, kLocalPrefix, sizeof kLocalPrefix - 1) == 0) {
@@ -491,6 +575,8 @@ int misor_create(misor_grid** out, const misor_desc* d) {
                 CREATE_FAIL(MISOR_ECOMM, "ncclCommInitRank failed");
         }
     }
+    if (configure_tb(g, kDefaultTsteps, kDefaultTbVariant, 0) != MISOR_OK)
+        CREATE_FAIL(MISOR_ENOMEM, "%s", g_err.c_str());
     if (hipStreamSynchronize(g->stream) != hipSuccess)
         CREATE_FAIL(MISOR_EHIP, "hipStreamSynchronize failed");
 #undef CREATE_FAIL
@@ -679,55 +765,78 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
         if (res) *res = g->st_host->res;
         return MISOR_OK;
     }
+    // multi-block path: passes of T iterations (T = 1: single-iteration sweep
+    // kernel; T >= 2: temporally blocked kernel, sor_tb.hip)
+    const int T = effective_tsteps(g);
+    const int depth = 2 * T;  // halo of src each pass needs
+    const int nparts = T == 1 ? g->nparts : g->tb_nparts;
+    double* const rhs = g->fld[kRhs];
+    auto pass = [&](hipStream_t s, int part, const double* src, double* dst, int Tp, int force) {
+        if (T == 1) {
+            SweepParams sp = g->sp;
+            sp.part = part;
+            launch_sweep(s, sp, src, dst, rhs, g->partials, g->st);
+        } else {
+            SweepParams tp = g->tp;
+            tp.part = part;
+            if (Tp != T) tb_geometry(g, Tp, tp);  // narrower cone: wider strips
+            launch_tb(s, Tp, tp, src, dst, rhs, g->partials, g->st, force);
+        }
+    };
     const int cur0 = g->cur;
-    long long launched = 0;
-    if (g->dist) {  // the halo-ring red updates read rhs one cell outside the block
-        int rc = exchange(g, g->fld[kRhs], 1);
+    long long launched = 0;  // passes enqueued
+    if (g->dist) {  // the halo-ring updates read rhs outside the block
+        int rc = exchange(g, rhs, T == 1 ? 1 : depth);
         if (rc) return rc;
     }
-    int batch = g->last_iters > 8 ? g->last_iters : 8;
+    const long long max_passes = (itermax + T - 1) / T;
+    int batch = g->last_iters / T > 8 ? g->last_iters / T : 8;
     for (;;) {
-        if (batch > itermax - launched) batch = (int)(itermax - launched);
+        if (batch > max_passes - launched) batch = (int)(max_passes - launched);
         if (batch < 1) batch = 1;
         if (g->timing) {
             int rc = ensure_events(g, 2 * (size_t)batch);
             if (rc) return rc;
         }
         for (int b = 0; b < batch && g->dist && g->overlap; ++b) {
-            // Overlapped iteration k.  comm stream: [wait sweep k-1] all-reduce and
-            // decide of k-1, 2-deep exchange of src_k.  compute stream: interior
-            // blocks of sweep k (no halo reads) meanwhile, then [wait exchange]
-            // boundary blocks, partial sum.  An interior pass launched after
-            // convergence (decide k-1 still in flight) only writes the buffer that
-            // is not the result; every other kernel sees `done` in stream order.
+            // Overlapped pass k.  comm stream: [wait pass k-1] all-reduce and
+            // decide of k-1, exchange of src_k.  compute stream: interior blocks
+            // of pass k (no halo reads) meanwhile, then [wait exchange] boundary
+            // blocks, partial sums.  With T = 1 an interior pass launched after
+            // convergence (decide k-1 still in flight) only writes the buffer
+            // that is not the result.  With T >= 2 the source of pass k-1 must
+            // survive (a pass that overshoots convergence is recomputed from
+            // it), so the interior blocks wait for decide k-1; the exchange still
+            // overlaps them.
             const long long k = launched + b;
             const double* src = g->fld[kP0 + ((cur0 + k) & 1)];
             double* dst = g->fld[kP0 + ((cur0 + k + 1) & 1)];
             HIPCHK(hipEventRecord(g->ev_s, g->stream));
             HIPCHK(hipStreamWaitEvent(g->cstream, g->ev_s, 0));
-            if (b > 0) {  // iteration k-1 of this batch (the previous batch closed its own)
-                int rc = allreduce(g, &g->st->sum, 1, 0, g->cstream);
+            if (b > 0) {  // pass k-1 of this batch (the previous batch closed its own)
+                int rc = allreduce(g, g->st->sum, T, 0, g->cstream);
                 if (rc) return rc;
-                launch_decide(g->cstream, g->st, cells);
+                launch_decide(g->cstream, g->st, T, cells);
+                if (T > 1) {
+                    HIPCHK(hipEventRecord(g->ev_d, g->cstream));
+                    HIPCHK(hipStreamWaitEvent(g->stream, g->ev_d, 0));
+                }
             }
-            int rc = exchange(g, const_cast<double*>(src), 2, g->cstream);
+            int rc = exchange(g, const_cast<double*>(src), depth, g->cstream);
             if (rc) return rc;
             HIPCHK(hipEventRecord(g->ev_x, g->cstream));
             if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b], g->stream));
-            SweepParams sp = g->sp;
-            sp.part = 1;
-            launch_sweep(g->stream, sp, src, dst, g->fld[kRhs], g->partials, g->st);
+            pass(g->stream, 1, src, dst, T, 0);
             HIPCHK(hipStreamWaitEvent(g->stream, g->ev_x, 0));
-            sp.part = 2;
-            launch_sweep(g->stream, sp, src, dst, g->fld[kRhs], g->partials, g->st);
+            pass(g->stream, 2, src, dst, T, 0);
             if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b + 1], g->stream));
-            launch_finish(g->stream, g->partials, g->nparts, g->st, cells, 0);
+            launch_finish(g->stream, g->partials, nparts, T, g->st, cells, 0);
             if (b == batch - 1) {  // close the batch: all-reduce + decide of the last one
                 HIPCHK(hipEventRecord(g->ev_s, g->stream));
                 HIPCHK(hipStreamWaitEvent(g->cstream, g->ev_s, 0));
-                rc = allreduce(g, &g->st->sum, 1, 0, g->cstream);
+                rc = allreduce(g, g->st->sum, T, 0, g->cstream);
                 if (rc) return rc;
-                launch_decide(g->cstream, g->st, cells);
+                launch_decide(g->cstream, g->st, T, cells);
                 HIPCHK(hipEventRecord(g->ev_x, g->cstream));
                 HIPCHK(hipStreamWaitEvent(g->stream, g->ev_x, 0));
             }
@@ -736,20 +845,20 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
             const long long k = launched + b;
             const double* src = g->fld[kP0 + ((cur0 + k) & 1)];
             double* dst = g->fld[kP0 + ((cur0 + k + 1) & 1)];
-            if (g->dist) {  // 2-deep halo of src: one exchange per iteration
-                int rc = exchange(g, const_cast<double*>(src), 2);
+            if (g->dist) {  // 2T-deep halo of src: one exchange per pass
+                int rc = exchange(g, const_cast<double*>(src), depth);
                 if (rc) return rc;
             }
             if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b], g->stream));
-            launch_sweep(g->stream, g->sp, src, dst, g->fld[kRhs], g->partials, g->st);
+            pass(g->stream, 0, src, dst, T, 0);
             if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b + 1], g->stream));
             if (g->dist) {
-                launch_finish(g->stream, g->partials, g->nparts, g->st, cells, 0);
-                int rc = allreduce(g, &g->st->sum, 1, 0);
+                launch_finish(g->stream, g->partials, nparts, T, g->st, cells, 0);
+                int rc = allreduce(g, g->st->sum, T, 0);
                 if (rc) return rc;
-                launch_decide(g->stream, g->st, cells);
+                launch_decide(g->stream, g->st, T, cells);
             } else {
-                launch_finish(g->stream, g->partials, g->nparts, g->st, cells, 1);
+                launch_finish(g->stream, g->partials, nparts, T, g->st, cells, 1);
             }
         }
         HIPCHK(hipGetLastError());
@@ -759,30 +868,41 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
                               g->stream));
         HIPCHK(hipStreamSynchronize(g->stream));
         if (g->timing) {
-            // launches after convergence exit at once; count only real sweeps
+            // passes after convergence exit at once; count only the real ones
             const long long real_before = launched - batch;
-            const long long real_end = g->st_host->it;
+            const long long real_end = (g->st_host->it + T - 1) / T;
             for (int b = 0; b < batch; ++b) {
                 if (real_before + b >= real_end) break;
                 float ms = 0.f;
                 HIPCHK(hipEventElapsedTime(&ms, g->ev[2 * b], g->ev[2 * b + 1]));
                 g->stats.sweep_ms += ms;
-                g->stats.timed_sweeps++;
+                g->stats.timed_sweeps += T;
+                g->stats.timed_passes++;
             }
         }
         if (g->st_host->done) break;
-        if (launched >= itermax) break;  // cannot happen: done covers it
+        if (launched >= max_passes) break;  // cannot happen: done covers it
         batch = batch < 512 ? 2 * batch : 1024;
     }
     const int it = g->st_host->it;
-    g->cur = (cur0 + it) & 1;
+    const long long passes = (it + T - 1) / T;
+    const int over = (int)(passes * T - it);
+    g->cur = (int)((cur0 + passes) & 1);
+    if (over > 0) {
+        // the last pass ran past the iteration that ended the loop: redo it
+        // with T - over iterations from its source (untouched since)
+        const double* src = g->fld[kP0 + ((cur0 + passes - 1) & 1)];
+        pass(g->stream, 0, src, g->fld[g->cur], T - over, 1);
+        HIPCHK(hipGetLastError());
+    }
     if (g->dist) {  // leave the halo of the final field consistent (adaptUV reads it)
         int rc = exchange(g, g->fld[g->cur], 2);
         if (rc) return rc;
-        HIPCHK(hipStreamSynchronize(g->stream));
     }
+    HIPCHK(hipStreamSynchronize(g->stream));
     g->last_iters = it;
     g->stats.sweeps += it;
+    g->stats.iters_per_pass = T;
     if (iters) *iters = it;
     if (res) *res = g->st_host->res;
     return MISOR_OK;
@@ -957,6 +1077,11 @@ int misor_set_tuning(misor_grid* g, int key, int value) {
         return configure_sweep(g, g->sp.variant, g->sp.rows_per_block, value != 0);
     case MISOR_TUNE_SMALL_SOLVE: g->small_solve = value != 0; return MISOR_OK;
     case MISOR_TUNE_OVERLAP: g->overlap = value != 0; return MISOR_OK;
+    case MISOR_TUNE_TSTEPS: return configure_tb(g, value, g->tp.variant, g->tb_rows_req);
+    case MISOR_TUNE_TB_VARIANT: return configure_tb(g, g->tsteps, value, g->tb_rows_req);
+    case MISOR_TUNE_TB_ROWS:
+        g->tb_rows_req = value;
+        return configure_tb(g, g->tsteps, g->tp.variant, value);
     default: return fail(MISOR_EINVAL, "unknown tuning key %d", key);
     }
 }
@@ -969,6 +1094,9 @@ int misor_get_tuning(const misor_grid* g, int key, int* value) {
     case MISOR_TUNE_XCD_REMAP: *value = g->sp.xcd_remap; return MISOR_OK;
     case MISOR_TUNE_SMALL_SOLVE: *value = g->small_solve; return MISOR_OK;
     case MISOR_TUNE_OVERLAP: *value = g->overlap; return MISOR_OK;
+    case MISOR_TUNE_TSTEPS: *value = g->tsteps; return MISOR_OK;
+    case MISOR_TUNE_TB_VARIANT: *value = g->tp.variant; return MISOR_OK;
+    case MISOR_TUNE_TB_ROWS: *value = g->tp.rows_per_block; return MISOR_OK;
     default: return fail(MISOR_EINVAL, "unknown tuning key %d", key);
     }
 }

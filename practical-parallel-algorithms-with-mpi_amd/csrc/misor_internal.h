@@ -20,14 +20,17 @@ namespace misor {
 //  - kXOff = 15 puts the first interior column i = 1 on a 128-byte boundary,
 //    so every wave's 16-byte-per-lane row segment of 128 cells starts a cache
 //    line; the ghost column i = 0 is the last double of the preceding line.
-//  - kYOff = 2 and two spare rows at the top give every sweep block its two
-//    halo rows (j0-2 .. j1+1) without clamping.
-//  - pitch = 32 + round_up(ni, kStripCells * kMaxWavesX): left pad line, the
-//    strips, the right halo pair and pad; a multiple of 16 doubles (128 B).
+//  - kYOff = 2 * kMaxT rows below row 0 and as many (+ prefetch run-out)
+//    above row nj+1: a block of the temporally blocked sweep streams rows
+//    j0-2T .. j1-1+2T (+ rows in flight) without clamping.
+//  - pitch = 160 + round_up(ni, kStripCells * kMaxWavesX): left pad line, the
+//    strips, the run-out of the last (overlapping) strip and pad; a multiple
+//    of 16 doubles (128 B) that is not a power of two.
 // Padding cells are zero and never feed an interior result.
 // ---------------------------------------------------------------------------
 constexpr int kXOff = 15;
-constexpr int kYOff = 2;
+constexpr int kMaxT = 4;                 // iterations per temporally blocked pass (max)
+constexpr int kYOff = 2 * kMaxT;
 constexpr int kLanes = 64;                 // wavefront
 constexpr int kStripCells = 2 * kLanes;    // 128 columns per wave (2 per lane)
 constexpr int kMaxWavesX = 16;             // strips per sweep workgroup (max)
@@ -35,10 +38,11 @@ constexpr int kMaxAhead = 3;               // rows a sweep keeps in flight (max)
 
 inline long long layout_pitch(int ni) {
     const int w = kStripCells * kMaxWavesX;
-    return 32 + (long long)((ni + w - 1) / w) * w;
+    return 160 + (long long)((ni + w - 1) / w) * w;
 }
-// rows j = -2 .. nj+1+kMaxAhead+1 (sweep prefetch runs past the top halo)
-inline long long layout_rows(int nj) { return (long long)nj + 4 + kMaxAhead + 2; }
+// rows j = -kYOff .. nj + 2*kMaxT + kMaxAhead + 1 (a temporally blocked block
+// streams 2T rows past its last row, plus the rows it keeps in flight)
+inline long long layout_rows(int nj) { return (long long)nj + 2 * kYOff + kMaxAhead + 3; }
 
 // sweep kernel variants: strips per workgroup, rows in flight, nt stores
 struct SweepVariant {
@@ -52,6 +56,19 @@ constexpr int kNumSweepVariants = 15;
 constexpr int kDefaultSweepVariant = 7;  // 8 strips, 2 rows ahead, nt stores (tools/tune_sweep.py)
 int sweep_waves(int variant);
 
+// temporally blocked sweep (sor_tb.hip): strips per workgroup, rows in flight
+struct TbVariant {
+    int waves, ahead;
+};
+constexpr TbVariant kTbVariants[] = {{4, 2}, {8, 2}, {4, 3}, {8, 3}};
+constexpr int kNumTbVariants = 4;
+constexpr int kDefaultTsteps = 3;      // iterations per pass (tools/tune_sweep.py --tb)
+constexpr int kDefaultTbVariant = 0;   // 4 strips, 2 rows in flight
+constexpr int kDefaultTbRows = 256;    // cap of the automatic rows per block
+int tb_waves(int variant);
+int tb_out_width(int T);
+int tb_partials(int ni, int nj, int T, int rows_per_block, int waves, int* nbx, int* nby);
+
 // Solver state that lives on the device between launches.  Written only by
 // the finish kernel (one workgroup) and read by the next sweep launch.
 struct DevState {
@@ -61,7 +78,8 @@ struct DevState {
     int pad;
     double res;    // residual of the last iteration
     double epssq;
-    double sum;    // sum r^2 of the last sweep (this rank, then all-reduced)
+    double sum[kMaxT];  // sum r^2 of each iteration of the last pass (this rank,
+                        // then all-reduced)
 };
 
 struct SweepParams {
@@ -76,6 +94,9 @@ struct SweepParams {
     int xcd_remap;       // deal consecutive logical blocks to one XCD
     int part;            // 0: all blocks, 1: interior blocks only, 2: boundary blocks only
     int int_lo_i, int_hi_i, int_lo_j, int_hi_j;  // footprint bounds of an interior block
+    int upd_lo_i, upd_hi_i, upd_lo_j, upd_hi_j;  // temporally blocked: cells updated
+                                                 // (1..n on physical sides, all on
+                                                 // neighbour sides)
     double idx2, idy2, coef;  // 1/dx^2, 1/dy^2, factor (RB) or omega*factor (RBA)
 };
 
@@ -89,9 +110,12 @@ struct NsParams {
 // kernel launchers (sor_kernels.hip, ns_kernels.hip)
 void launch_sweep(hipStream_t s, const SweepParams& prm, const double* src, double* dst,
                   const double* rhs, double* partials, const DevState* st);
-void launch_finish(hipStream_t s, const double* partials, int nparts, DevState* st,
+// T iterations per pass: partials[t * nparts + block]
+void launch_finish(hipStream_t s, const double* partials, int nparts, int T, DevState* st,
                    double cells, int decide);
-void launch_decide(hipStream_t s, DevState* st, double cells);
+void launch_decide(hipStream_t s, DevState* st, int T, double cells);
+void launch_tb(hipStream_t s, int T, const SweepParams& prm, const double* src, double* dst,
+               const double* rhs, double* partials, const DevState* st, int force);
 // whole-solve single-workgroup kernel for grids whose p fits in LDS
 int small_solve_fits(int ni, int nj);
 void launch_solve_small(hipStream_t s, double* p, const double* rhs, int ni, int nj,

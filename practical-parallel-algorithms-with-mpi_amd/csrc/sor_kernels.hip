@@ -307,32 +307,42 @@ __global__ __launch_bounds__(kLanes* WAVES) void rb_sweep_kernel(
 // Sum of the per-block partials in a fixed order, then the loop test of
 // solveRB (assignment-4/src/solver.c:197,229,233):
 //   res = sum / (imax*jmax); it++; continue while res >= eps^2 && it < itermax
+// A temporally blocked pass leaves T groups of partials (one per iteration);
+// they are decided in iteration order and the first failing test stops the
+// count, exactly as the reference loop would have stopped.
 __global__ __launch_bounds__(1024) void rb_finish_kernel(const double* __restrict__ partials,
-                                                         int n, DevState* st, double cells,
-                                                         int decide) {
+                                                         int n, int T, DevState* st,
+                                                         double cells, int decide) {
     __shared__ double sh[1024];
     if (st->done) return;
     const int t = threadIdx.x;
-    double s = 0.0;
-    for (int k = t; k < n; k += 1024) s += partials[k];
-    sh[t] = s;
-    __syncthreads();
-#pragma unroll
-    for (int w = 512; w >= 64; w >>= 1) {
-        if (t < w) sh[t] += sh[t + w];
+    for (int s_ = 0; s_ < T; ++s_) {
+        const double* pp = partials + (long long)s_ * n;
+        double s = 0.0;
+        for (int k = t; k < n; k += 1024) s += pp[k];
+        sh[t] = s;
         __syncthreads();
-    }
-    if (t < 64) {
-        double v = sh[t];
-        v = wave_sum(v);
-        if (t == 0 && !decide) st->sum = v;  // decomposed: all-reduce, then decide
-        if (t == 0 && decide) {
-            const double res = v / cells;
-            const int it = st->it + 1;
-            st->res = res;
-            st->it = it;
-            st->done = !((res >= st->epssq) && (it < st->itermax));
+#pragma unroll
+        for (int w = 512; w >= 64; w >>= 1) {
+            if (t < w) sh[t] += sh[t + w];
+            __syncthreads();
         }
+        if (t < 64) {
+            double v = sh[t];
+            v = wave_sum(v);
+            if (t == 0) {
+                if (!decide) {
+                    st->sum[s_] = v;  // decomposed: all-reduce, then decide
+                } else if (!st->done) {
+                    const double res = v / cells;
+                    const int it = st->it + 1;
+                    st->res = res;
+                    st->it = it;
+                    st->done = !((res >= st->epssq) && (it < st->itermax));
+                }
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -372,24 +382,26 @@ void launch_sweep(hipStream_t s, const SweepParams& prm, const double* src, doub
 #undef SWEEP
 }
 
-void launch_finish(hipStream_t s, const double* partials, int nparts, DevState* st,
+void launch_finish(hipStream_t s, const double* partials, int nparts, int T, DevState* st,
                    double cells, int decide) {
-    hipLaunchKernelGGL(rb_finish_kernel, dim3(1), dim3(1024), 0, s, partials, nparts, st, cells,
-                       decide);
+    hipLaunchKernelGGL(rb_finish_kernel, dim3(1), dim3(1024), 0, s, partials, nparts, T, st,
+                       cells, decide);
 }
 
-// decomposed runs: st->sum holds the all-reduced sum r^2 of every rank
-__global__ void rb_decide_kernel(DevState* st, double cells) {
-    if (st->done) return;
-    const double res = st->sum / cells;
-    const int it = st->it + 1;
-    st->res = res;
-    st->it = it;
-    st->done = !((res >= st->epssq) && (it < st->itermax));
+// decomposed runs: st->sum[0..T-1] hold the all-reduced sums r^2 of every rank
+__global__ void rb_decide_kernel(DevState* st, int T, double cells) {
+    for (int s_ = 0; s_ < T; ++s_) {
+        if (st->done) return;
+        const double res = st->sum[s_] / cells;
+        const int it = st->it + 1;
+        st->res = res;
+        st->it = it;
+        st->done = !((res >= st->epssq) && (it < st->itermax));
+    }
 }
 
-void launch_decide(hipStream_t s, DevState* st, double cells) {
-    hipLaunchKernelGGL(rb_decide_kernel, dim3(1), dim3(1), 0, s, st, cells);
+void launch_decide(hipStream_t s, DevState* st, int T, double cells) {
+    hipLaunchKernelGGL(rb_decide_kernel, dim3(1), dim3(1), 0, s, st, T, cells);
 }
 
 // ---------------------------------------------------------------------------

@@ -22,8 +22,8 @@ P, RHS, U, V, F, G = range(6)
 NOSLIP, SLIP, OUTFLOW, PERIODIC = 1, 2, 3, 4
 PROBLEM_NONE, PROBLEM_DCAVITY, PROBLEM_CANAL = 0, 1, 2
 SOLVE_RB, SOLVE_RBA = 0, 1
-TUNE_SWEEP_VARIANT, TUNE_ROWS_PER_BLOCK, TUNE_XCD_REMAP, TUNE_SMALL_SOLVE, TUNE_OVERLAP = \
-    1, 2, 3, 4, 5
+(TUNE_SWEEP_VARIANT, TUNE_ROWS_PER_BLOCK, TUNE_XCD_REMAP, TUNE_SMALL_SOLVE, TUNE_OVERLAP,
+ TUNE_TSTEPS, TUNE_TB_VARIANT, TUNE_TB_ROWS) = 1, 2, 3, 4, 5, 6, 7, 8
 COMM_ID_BYTES = 128
 
 _dp = C.POINTER(C.c_double)
@@ -51,7 +51,8 @@ class Local(C.Structure):
 
 class Stats(C.Structure):
     _fields_ = [("sweeps", C.c_longlong), ("launches", C.c_longlong), ("sweep_ms", C.c_double),
-                ("timed_sweeps", C.c_longlong)]
+                ("timed_sweeps", C.c_longlong), ("timed_passes", C.c_longlong),
+                ("iters_per_pass", C.c_int), ("pad_", C.c_int)]
 
 
 # every exported symbol of include/misor.h, with its ctypes signature
@@ -246,7 +247,8 @@ class Grid:
         s = Stats()
         _check(lib().misor_get_stats(self.h, C.byref(s)))
         return {"sweeps": s.sweeps, "launches": s.launches, "sweep_ms": s.sweep_ms,
-                "timed_sweeps": s.timed_sweeps}
+                "timed_sweeps": s.timed_sweeps, "timed_passes": s.timed_passes,
+                "iters_per_pass": s.iters_per_pass}
 
     def reset_stats(self):
         _check(lib().misor_reset_stats(self.h))

@@ -69,7 +69,8 @@ def assemble(parts, shape):
                                         (4, (1, 4)), (6, (0, 0)), (8, (0, 0))])
 @pytest.mark.parametrize("ni,nj,k", [(61, 43, 5), (300, 257, 3), (2100, 90, 2)])
 @pytest.mark.parametrize("overlap", [1, 0], ids=["overlap", "serial"])
-def test_fixed_sweeps_partition_independent(world, dims, ni, nj, k, overlap):
+@pytest.mark.parametrize("T", [1, 2, 4], ids=["t1", "t2", "t4"])
+def test_fixed_sweeps_partition_independent(world, dims, ni, nj, k, overlap, T):
     rng = np.random.default_rng(ni + 31 * nj + world)
     p = rng.standard_normal((nj + 2, ni + 2))
     rhs = rng.standard_normal((nj + 2, ni + 2)) * 20
@@ -81,6 +82,7 @@ def test_fixed_sweeps_partition_independent(world, dims, ni, nj, k, overlap):
         with M.Grid(ni, nj, dx, dy, 1.85, 1e-300, k, device=0, nranks=world, rank=r,
                     dims=dims, comm_id=cid) as g:
             g.set_tuning(M.TUNE_OVERLAP, overlap)
+            g.set_tuning(M.TUNE_TSTEPS, T)  # 2T-deep halo per pass of T iterations
             g.upload(M.P, local_window(p, g.loc))
             g.upload(M.RHS, local_window(rhs, g.loc))
             it, res = g.solve_rb()
@@ -95,12 +97,15 @@ def test_fixed_sweeps_partition_independent(world, dims, ni, nj, k, overlap):
 
 
 @pytest.mark.parametrize("world", [2, 4])
-def test_poisson_par_converges_decomposed(golden, world):
+@pytest.mark.parametrize("T", [1, 3])
+def test_poisson_par_converges_decomposed(golden, world, T):
+    """poisson.par to convergence (2388 iterations) on 2 / 4 ranks"""
     z = np.load(golden + "/rb_poisson100.npz")
 
     def rank_fn(r, cid, dims):
         with M.Grid(100, 100, 0.01, 0.01, 1.9, 1e-6, 1000000, device=0, nranks=world, rank=r,
                     comm_id=cid) as g:
+            g.set_tuning(M.TUNE_TSTEPS, T)
             g.poisson_init(1.0, 1.0, 2)
             it, res = g.solve_rb()
             return g.loc, g.download(M.P), it
@@ -109,6 +114,34 @@ def test_poisson_par_converges_decomposed(golden, world):
     assert all(o[2] == 2388 for o in outs)
     got = assemble([(o[0], o[1]) for o in outs], z["p"].shape)
     assert np.array_equal(got, z["p"])  # corners included: the corner ranks own them
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("T", [2, 3, 4])
+def test_converges_mid_pass_decomposed(world, T):
+    """convergence inside a pass of T iterations: every rank recomputes its
+    last pass with fewer iterations from the untouched source buffer"""
+    ni, nj = 300, 190
+    p, rhs = orc.poisson_init(ni, nj)
+    want = p.copy()
+    eps = 3e-3
+    it_ref, res_ref = orc.solve_rb(want, rhs, 1.0 / ni, 1.0 / nj, 1.9, eps, 100000)
+    assert it_ref % 12 != 0  # ends mid-pass for at least two of T = 2, 3, 4
+
+    def rank_fn(r, cid, dims):
+        with M.Grid(ni, nj, 1.0 / ni, 1.0 / nj, 1.9, eps, 100000, device=0, nranks=world,
+                    rank=r, comm_id=cid) as g:
+            g.set_tuning(M.TUNE_TSTEPS, T)
+            g.poisson_init(1.0, 1.0, 2)
+            it, res = g.solve_rb()
+            return g.loc, g.download(M.P), it, res
+
+    outs = run_ranks(world, rank_fn)
+    for o in outs:
+        assert o[2] == it_ref
+        assert abs(o[3] - res_ref) <= 1e-12 * res_ref
+    got = assemble([(o[0], o[1]) for o in outs], p.shape)
+    assert np.array_equal(got, want)
 
 
 def test_rccl_single_rank_path(golden):

@@ -19,16 +19,27 @@ pytestmark = pytest.mark.gpu
 OMEGA, EPS = 1.9, 1e-6
 
 
-def make_grid(ni, nj, xl=1.0, yl=1.0, omega=OMEGA, eps=EPS, itermax=1000000,
-              variant=M.SOLVE_RB, small=1):
-    g = M.Grid(ni, nj, xl / ni, yl / nj, omega, eps, itermax, variant=variant)
-    # small=1: whole-solve LDS kernel where the grid fits; 0: always the
-    # multi-block sweep path (both must match the reference)
-    g.set_tuning(M.TUNE_SMALL_SOLVE, small)
+def set_mode(g, small):
+    """small = 1: whole-solve LDS kernel where the grid fits; 0: the
+    multi-block path with the default iterations per pass; "tN": the
+    multi-block path with N iterations per pass (1: single-iteration sweep
+    kernel, 2..4: temporally blocked kernel).  All must match the reference."""
+    if isinstance(small, str):
+        g.set_tuning(M.TUNE_SMALL_SOLVE, 0)
+        g.set_tuning(M.TUNE_TSTEPS, int(small[1:]))
+    else:
+        g.set_tuning(M.TUNE_SMALL_SOLVE, small)
     return g
 
 
-PATHS = pytest.mark.parametrize("small", [1, 0], ids=["lds", "blocks"])
+def make_grid(ni, nj, xl=1.0, yl=1.0, omega=OMEGA, eps=EPS, itermax=1000000,
+              variant=M.SOLVE_RB, small=1):
+    g = M.Grid(ni, nj, xl / ni, yl / nj, omega, eps, itermax, variant=variant)
+    return set_mode(g, small)
+
+
+PATHS = pytest.mark.parametrize("small", [1, "t1", "t2", "t3", "t4"],
+                                ids=["lds", "t1", "t2", "t3", "t4"])
 
 
 def test_poisson_init_bitwise():
@@ -103,7 +114,9 @@ def test_rba_variant(small):
 @pytest.mark.parametrize("ni,nj,k", [(3, 2, 5), (2, 7, 4), (127, 129, 3), (128, 128, 3),
                                      (129, 33, 4), (255, 17, 2), (256, 300, 3),
                                      (511, 40, 3), (512, 65, 2), (513, 513, 3),
-                                     (1000, 777, 2), (2049, 130, 2)])
+                                     (1000, 777, 2), (2049, 130, 2), (120, 9, 7),
+                                     (121, 300, 5), (240, 241, 6), (112, 113, 9),
+                                     (1001, 1537, 8)])
 @PATHS
 def test_random_fields_vs_oracle(ni, nj, k, small):
     rng = np.random.default_rng(ni * 7919 + nj)
@@ -113,7 +126,7 @@ def test_random_fields_vs_oracle(ni, nj, k, small):
     want = p.copy()
     it_ref, res_ref = orc.solve_rb(want, rhs, dx, dy, 1.7, 1e-300, k)
     with M.Grid(ni, nj, dx, dy, 1.7, 1e-300, k) as g:
-        g.set_tuning(M.TUNE_SMALL_SOLVE, small)
+        set_mode(g, small)
         g.upload(M.P, p)
         g.upload(M.RHS, rhs)
         it, res = g.solve_rb()
@@ -132,7 +145,7 @@ def test_consecutive_solves_track_buffers(small):
     rhs = rng.standard_normal((nj + 2, ni + 2))
     want = p.copy()
     with M.Grid(ni, nj, 1.0 / ni, 1.0 / nj, 1.5, 1e-300, 10) as g:
-        g.set_tuning(M.TUNE_SMALL_SOLVE, small)
+        set_mode(g, small)
         g.upload(M.P, p)
         g.upload(M.RHS, rhs)
         for k in (3, 4, 1, 6):
@@ -152,16 +165,40 @@ def test_zero_iterations():
         assert g.solve_rb() == (0, 1.0)
 
 
-def test_large_grid_two_sweeps():
-    """8192^2 (67M cells, 0.54 GB per field): bit-exact after 2 sweeps"""
+@pytest.mark.parametrize("k", [2, 3])
+def test_large_grid_few_sweeps(k):
+    """8192^2 (67M cells, 0.54 GB per field): bit-exact after 2 and 3 sweeps
+    (default path: temporally blocked, 3 = one full pass + one recomputed)"""
     n = 8192
     p, rhs = orc.poisson_init(n, n)
     want = p.copy()
-    it_ref, res_ref = orc.solve_rb(want, rhs, 1.0 / n, 1.0 / n, OMEGA, 1e-300, 2)
-    with make_grid(n, n, eps=1e-300, itermax=2) as g:
+    it_ref, res_ref = orc.solve_rb(want, rhs, 1.0 / n, 1.0 / n, OMEGA, 1e-300, k)
+    with make_grid(n, n, eps=1e-300, itermax=k) as g:
         g.poisson_init(1.0, 1.0, 2)
         it, res = g.solve_rb()
         got = g.download(M.P)
-    assert it == 2
+    assert it == k
+    assert np.array_equal(got, want)
+    # res sums 6.7e7 squares: the oracle left to right, the device in a tree,
+    # so only the rounding of the sum differs (p itself is bit-exact)
+    assert abs(res - res_ref) <= 1e-10 * res_ref
+
+
+@pytest.mark.parametrize("T", [2, 3, 4])
+def test_tb_converges_mid_pass(T):
+    """convergence inside a temporally blocked pass: the pass is recomputed
+    with fewer iterations, so the count and p equal solveRB's for every T"""
+    ni, nj = 300, 190
+    p, rhs = orc.poisson_init(ni, nj)
+    want = p.copy()
+    eps = 3e-3
+    it_ref, res_ref = orc.solve_rb(want, rhs, 1.0 / ni, 1.0 / nj, OMEGA, eps, 100000)
+    with make_grid(ni, nj, eps=eps, small="t%d" % T) as g:
+        g.poisson_init(1.0, 1.0, 2)
+        it, res = g.solve_rb()
+        got = g.download(M.P)
+        st = g.stats()
+    assert st["iters_per_pass"] == T
+    assert it == it_ref
     assert np.array_equal(got, want)
     assert abs(res - res_ref) <= 1e-12 * res_ref

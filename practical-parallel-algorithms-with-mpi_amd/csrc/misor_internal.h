@@ -60,11 +60,12 @@ int sweep_waves(int variant);
 struct TbVariant {
     int waves, ahead;
 };
-constexpr TbVariant kTbVariants[] = {{4, 2}, {8, 2}, {4, 3}, {8, 3}};
-constexpr int kNumTbVariants = 4;
-constexpr int kDefaultTsteps = 3;      // iterations per pass (tools/tune_sweep.py --tb)
+constexpr TbVariant kTbVariants[] = {{4, 2}, {8, 2}, {4, 3}, {8, 3},
+                                     {6, 2}, {12, 2}, {16, 2}, {16, 1}};
+constexpr int kNumTbVariants = 8;
+constexpr int kDefaultTsteps = 4;      // iterations per pass (tools/tune_sweep.py --tb)
 constexpr int kDefaultTbVariant = 0;   // 4 strips, 2 rows in flight
-constexpr int kDefaultTbRows = 256;    // cap of the automatic rows per block
+constexpr int kDefaultTbRows = 128;    // cap of the automatic rows per block
 int tb_waves(int variant);
 int tb_out_width(int T);
 int tb_partials(int ni, int nj, int T, int rows_per_block, int waves, int* nbx, int* nby);

@@ -48,6 +48,16 @@
 // (misor_api.hip), so the returned field is the one after exactly `it`
 // iterations.
 //
+// Instruction economy (the kernel is VALU-issue-bound once T >= 3):
+//  - strips whose 128 columns are all updated cells ("interior" strips: no
+//    physical ghost column, no padding) run a path with no per-lane masks,
+//    the row colour as a compile-time constant (rows unrolled by two) and the
+//    residual accumulated in every lane, non-owned lanes dropped at the end;
+//    only strips at a physical left/right side run the masked path;
+//  - lane shifts are DPP wave_shr:1 / wave_shl:1 moves, not LDS permutes;
+//  - r^2 is accumulated with an FMA (the residual's rounding is not part of
+//    the bit-exact contract; p is).
+//
 // Bit-exactness: same expression order as the reference, -ffp-contract=off.
 
 #include "misor_internal.h"
@@ -56,8 +66,20 @@ namespace misor {
 
 namespace {
 
-__device__ __forceinline__ double from_left(double v) { return __shfl_up(v, 1, 64); }
-__device__ __forceinline__ double from_right(double v) { return __shfl_down(v, 1, 64); }
+// Lane shifts by DPP wave_shr:1 / wave_shl:1 (bound_ctrl: the lane shifted in
+// from outside the wave reads 0).  Lanes 0 and 63 are never output lanes (the
+// T outermost lanes on each side are the strip's halo), so their value is
+// irrelevant; no copy of the old value is needed.
+// lane l receives lane l-1's value
+__device__ __forceinline__ double from_left(double v) {
+    return __hiloint2double(__builtin_amdgcn_mov_dpp(__double2hiint(v), 0x138, 0xf, 0xf, true),
+                            __builtin_amdgcn_mov_dpp(__double2loint(v), 0x138, 0xf, 0xf, true));
+}
+// lane l receives lane l+1's value
+__device__ __forceinline__ double from_right(double v) {
+    return __hiloint2double(__builtin_amdgcn_mov_dpp(__double2hiint(v), 0x130, 0xf, 0xf, true),
+                            __builtin_amdgcn_mov_dpp(__double2loint(v), 0x130, 0xf, 0xf, true));
+}
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -84,6 +106,7 @@ struct Lane {
     bool own_a, own_b;     // columns whose residual this lane counts
     bool fix0_b;           // ib == 0 on a physical left side: column 0 := column 1
     bool fixr_a, fixr_b;   // ia / ib == ni+1 on a physical right side
+    bool st_a, st_b;       // columns this lane stores
     int lo_j, hi_j;        // updated rows
     int j0, j1;            // owned rows
     int parity;
@@ -91,15 +114,29 @@ struct Lane {
     double idx2, idy2, coef;
 };
 
+// How a step is compiled:
+//  kEdge   general: colour from the row, per-lane update / residual masks,
+//          ghost-row and ghost-column copies, row tests.  Blocks whose cone
+//          reaches a physical side (first/last strip, first/last block row).
+//  kWarm   interior: colour a constant, every streamed row is an updatable
+//          row (rows outside the valid cone hold garbage that never reaches a
+//          stored value); only the residual (select on the row's ownership)
+//          and the store are row-tested.  The 4T+1 warm-up and 2T drain steps.
+//  kSteady interior, every row touched is owned: no tests at all.
+enum { kEdge = 0, kWarm = 1, kSteady = 2 };
+
 // One iteration stage.  In = row rin of the previous stage's output (stage 1:
 // of the field in memory).  Returns row rin-2 of this stage's output.
-// fixrows (stages 2..T; a constant after unrolling): complete the previous iteration's ghost-row copy on
-// the incoming stream.  Stage 1 reads the ghost rows as they are in memory --
-// the state after the previous pass, or whatever the caller uploaded, as the
-// reference's first iteration does.
+// fixrows (stages 2..T; a constant after unrolling): complete the previous
+// iteration's ghost-row copy on the incoming stream.  Stage 1 reads the ghost
+// rows as they are in memory -- the state after the previous pass, or
+// whatever the caller uploaded, as the reference's first iteration does.
+// Q: colour of the rows (0: column ia is red in row rin-1), -1 = from c.
+template <int Q, int MODE>
 __device__ __forceinline__ d2 stage(const Lane& c, bool fixrows, d2 In, int rin, d2& A, d2& M1,
                                     d2& M2, d2 Ra, d2 Rb, double& acc) {
-    if (fixrows) {
+    constexpr bool EDGE = MODE == kEdge;
+    if (EDGE && fixrows) {
         if (c.gb && rin == 1) {  // row 0 := row 1 (A holds row 0)
             if (c.up_a) A.x = In.x;
             if (c.up_b) A.y = In.y;
@@ -111,59 +148,178 @@ __device__ __forceinline__ d2 stage(const Lane& c, bool fixrows, d2 In, int rin,
     }
     const int rr = rin - 1;  // red row
     const int rb = rin - 2;  // black row
-    const int q = (c.parity + 1 + rr) & 1;  // 0: column ia is red in row rr (black in rb)
+    const int q = Q >= 0 ? Q : ((c.parity + 1 + rr) & 1);
     const double idx2 = c.idx2, idy2 = c.idy2, coef = c.coef;
+    // r^2 into the stage's residual if (row, column) is owned
+    auto tally = [&](double r, bool own_row, bool own_col) {
+        if (MODE == kSteady) {
+            acc = __builtin_fma(r, r, acc);
+        } else if (MODE == kWarm) {
+            const double rm = own_row ? r : 0.0;  // uniform select: no branch, NaN-safe
+            acc = __builtin_fma(rm, rm, acc);
+        } else if (own_row && own_col) {
+            acc = __builtin_fma(r, r, acc);
+        }
+    };
 
     // red pass on row rr
     d2 Mr = A;
-    if (rr >= c.lo_j && rr <= c.hi_j) {
+    if (!EDGE || (rr >= c.lo_j && rr <= c.hi_j)) {
         const bool own = (rr >= c.j0) && (rr < c.j1);
         if (q == 0) {
             const double Lf = from_left(A.y);
             const double cc = A.x;
             const double r = Ra.x - (((A.y - 2.0 * cc) + Lf) * idx2 +
                                      ((In.x - 2.0 * cc) + M1.x) * idy2);
-            if (c.up_a) Mr.x = cc - coef * r;
-            if (c.own_a && own) acc += r * r;
+            if (!EDGE || c.up_a) Mr.x = cc - coef * r;
+            tally(r, own, c.own_a);
         } else {
             const double Rf = from_right(A.x);
             const double cc = A.y;
             const double r = Ra.y - (((Rf - 2.0 * cc) + A.x) * idx2 +
                                      ((In.y - 2.0 * cc) + M1.y) * idy2);
-            if (c.up_b) Mr.y = cc - coef * r;
-            if (c.own_b && own) acc += r * r;
+            if (!EDGE || c.up_b) Mr.y = cc - coef * r;
+            tally(r, own, c.own_b);
         }
     }
 
     // black pass on row rb (+ the ghost column copy of this finished row)
     d2 F = M1;
-    if (rb >= c.lo_j && rb <= c.hi_j) {
+    if (!EDGE || (rb >= c.lo_j && rb <= c.hi_j)) {
         const bool own = (rb >= c.j0) && (rb < c.j1);
         if (q == 0) {
             const double Ln = from_left(M1.y);
             const double cc = M1.x;
             const double r = Rb.x - (((M1.y - 2.0 * cc) + Ln) * idx2 +
                                      ((Mr.x - 2.0 * cc) + M2.x) * idy2);
-            if (c.up_a) F.x = cc - coef * r;
-            if (c.own_a && own) acc += r * r;
+            if (!EDGE || c.up_a) F.x = cc - coef * r;
+            tally(r, own, c.own_a);
         } else {
             const double Rn = from_right(M1.x);
             const double cc = M1.y;
             const double r = Rb.y - (((Rn - 2.0 * cc) + M1.x) * idx2 +
                                      ((Mr.y - 2.0 * cc) + M2.y) * idy2);
-            if (c.up_b) F.y = cc - coef * r;
-            if (c.own_b && own) acc += r * r;
+            if (!EDGE || c.up_b) F.y = cc - coef * r;
+            tally(r, own, c.own_b);
         }
-        const double f1 = from_right(F.x);  // column ib+1 (lane l+1's ia)
-        const double fl = from_left(F.y);   // column ia-1 (lane l-1's ib)
-        if (c.fix0_b) F.y = f1;
-        if (c.fixr_a) F.x = fl;
-        if (c.fixr_b) F.y = F.x;
+        if (EDGE) {
+            const double f1 = from_right(F.x);  // column ib+1 (lane l+1's ia)
+            const double fl = from_left(F.y);   // column ia-1 (lane l-1's ib)
+            if (c.fix0_b) F.y = f1;
+            if (c.fixr_a) F.x = fl;
+            if (c.fixr_b) F.y = F.x;
+        }
     }
     M2 = F;
     M1 = Mr;
     A = In;
     return F;
+}
+
+// the registers of one wave's march
+template <int T, int D>
+struct March {
+    d2 A[T], M1[T], M2[T];
+    d2 R[2 * T];      // rhs ring: R[k] = rhs(r0 - 1 - k)
+    d2 Pq[D], Rq[D];  // rows in flight: p(r0 .. r0+D-1), rhs(r0-1 .. r0+D-2)
+    double acc[T];
+};
+
+struct Io {
+    const double* sp;
+    const double* rp;
+    double* dp;
+    long long pitch;
+};
+
+// one step of the march: stream in old row r0, push it through the T stages,
+// store the row the last stage finished (r0 - 2T) if this block owns it
+template <int T, int D, bool NT, int Q, int MODE>
+__device__ __forceinline__ void tb_step(March<T, D>& m, const Lane& c, const Io& io, int r0) {
+    const long long pitch = io.pitch;
+    const d2 nP = ldv(io.sp + (long long)(r0 + D) * pitch);
+    const d2 nR = ldv(io.rp + (long long)(r0 - 1 + D) * pitch);
+#pragma unroll
+    for (int k = 2 * T - 1; k > 0; --k) m.R[k] = m.R[k - 1];
+    m.R[0] = m.Rq[0];
+
+    d2 v = m.Pq[0];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const d2 prevM2 = m.M2[t];
+        v = stage<Q, MODE>(c, t > 0, v, r0 - 2 * t, m.A[t], m.M1[t], m.M2[t], m.R[2 * t],
+                           m.R[2 * t + 1], m.acc[t]);
+        if (t == T - 1) {
+            const int jw = r0 - 2 * T;  // row finished by the last stage
+            if (MODE == kSteady) {
+                if (c.st_a) stv<NT>(io.dp + (long long)jw * pitch, v);
+            } else if (MODE == kWarm) {
+                if (jw >= c.j0 && jw < c.j1 && c.st_a) stv<NT>(io.dp + (long long)jw * pitch, v);
+            } else if (jw >= c.j0 && jw < c.j1) {
+                double* drow = io.dp + (long long)jw * pitch;
+                auto put = [&](double* p, d2 o) {
+                    if (c.st_a && c.st_b) {
+                        stv<NT>(p, o);
+                    } else if (c.st_a) {
+                        p[0] = o.x;
+                    } else if (c.st_b) {
+                        p[1] = o.y;
+                    }
+                };
+                put(drow, v);
+                // ghost rows of the stored field: interior columns from the
+                // finished row, corners from the (unchanged) ghost row
+                if (c.gb && jw == 1) {
+                    const d2 g0 = prevM2;  // the stage's row 0
+                    put(drow - pitch, d2{c.up_a ? v.x : g0.x, c.up_b ? v.y : g0.y});
+                }
+                if (c.gt && jw == c.nj) {
+                    const d2 gn = m.M1[t];  // the stage's row nj+1 (after its fix)
+                    put(drow + pitch, d2{c.up_a ? v.x : gn.x, c.up_b ? v.y : gn.y});
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k + 1 < D; ++k) {
+        m.Pq[k] = m.Pq[k + 1];
+        m.Rq[k] = m.Rq[k + 1];
+    }
+    m.Pq[D - 1] = nP;
+    m.Rq[D - 1] = nR;
+}
+
+// Interior blocks: the colour alternates by row, so steps go in pairs with
+// the colour a constant (Q0 = colour of row r0).  Steps r0 in
+// [j0+2T+1, j1-1] touch only owned rows and store unconditionally (kSteady);
+// the 4T+1 warm-up steps before and the 2T drain steps after are kWarm.
+template <int T, int D, bool NT, int Q0>
+__device__ __forceinline__ void march_interior_q(March<T, D>& m, const Lane& c, const Io& io,
+                                                 int r0, int rend) {
+    const int sbeg = c.j0 + 2 * T + 1, send = c.j1 - 1;
+    // warm-up, in pairs (keeps the colour phase); may run into the steady range
+    for (; r0 + 1 < sbeg && r0 + 1 <= rend; r0 += 2) {
+        tb_step<T, D, NT, Q0, kWarm>(m, c, io, r0);
+        tb_step<T, D, NT, 1 - Q0, kWarm>(m, c, io, r0 + 1);
+    }
+    for (; r0 + 1 <= send; r0 += 2) {
+        tb_step<T, D, NT, Q0, kSteady>(m, c, io, r0);
+        tb_step<T, D, NT, 1 - Q0, kSteady>(m, c, io, r0 + 1);
+    }
+    for (; r0 + 1 <= rend; r0 += 2) {
+        tb_step<T, D, NT, Q0, kWarm>(m, c, io, r0);
+        tb_step<T, D, NT, 1 - Q0, kWarm>(m, c, io, r0 + 1);
+    }
+    if (r0 <= rend) tb_step<T, D, NT, Q0, kWarm>(m, c, io, r0);
+}
+
+template <int T, int D, bool NT>
+__device__ __forceinline__ void march_interior(March<T, D>& m, const Lane& c, const Io& io,
+                                               int rs, int rend) {
+    if (((c.parity + rs) & 1) == 0)
+        march_interior_q<T, D, NT, 0>(m, c, io, rs, rend);
+    else
+        march_interior_q<T, D, NT, 1>(m, c, io, rs, rend);
 }
 
 }  // namespace
@@ -198,10 +354,11 @@ __global__ __launch_bounds__(kLanes* WAVES) void rb_tb_kernel(
     const int wave = threadIdx.x >> 6;
     const int strip = bx * WAVES + wave;
     const int c_out = 1 + strip * OW;
+    const int c_ld = c_out - 2 * T;
     const long long pitch = prm.pitch;
 
     Lane c;
-    c.ia = c_out - 2 * T + 2 * lane;
+    c.ia = c_ld + 2 * lane;
     c.ib = c.ia + 1;
     c.up_a = c.ia >= prm.upd_lo_i && c.ia <= prm.upd_hi_i;
     c.up_b = c.ib >= prm.upd_lo_i && c.ib <= prm.upd_hi_i;
@@ -211,6 +368,9 @@ __global__ __launch_bounds__(kLanes* WAVES) void rb_tb_kernel(
     c.fix0_b = prm.ghost_left && c.ib == 0;
     c.fixr_a = prm.ghost_right && c.ia == ni + 1;
     c.fixr_b = prm.ghost_right && c.ib == ni + 1;
+    // columns this lane stores: owned interior + the physical ghost columns
+    c.st_a = c.own_a || c.fixr_a;
+    c.st_b = c.own_b || c.fix0_b || c.fixr_b;
     c.lo_j = prm.upd_lo_j;
     c.hi_j = prm.upd_hi_j;
     c.j0 = j0;
@@ -222,13 +382,10 @@ __global__ __launch_bounds__(kLanes* WAVES) void rb_tb_kernel(
     c.idx2 = prm.idx2;
     c.idy2 = prm.idy2;
     c.coef = prm.coef;
-    // columns this lane stores: owned interior + the physical ghost columns
-    const bool st_a = c.own_a || c.fixr_a;
-    const bool st_b = c.own_b || c.fix0_b || c.fixr_b;
 
-    double acc[T];
+    March<T, D> m;
 #pragma unroll
-    for (int t = 0; t < T; ++t) acc[t] = 0.0;
+    for (int t = 0; t < T; ++t) m.acc[t] = 0.0;
 
     // physical corners are never touched by solveRB; carry them into dst
     if (L == 0 && threadIdx.x < 4) {
@@ -244,79 +401,40 @@ __global__ __launch_bounds__(kLanes* WAVES) void rb_tb_kernel(
 
     if (c_out <= ni) {  // wave-uniform
         const long long base = (long long)kYOff * pitch + kXOff + c.ia;
-        const double* sp = src + base;
-        const double* rp = rhs + base;
-        double* dp = dst + base;
-        auto ldp = [&](int j) { return ldv(sp + (long long)j * pitch); };
-        auto ldr = [&](int j) { return ldv(rp + (long long)j * pitch); };
-
+        const Io io{src + base, rhs + base, dst + base, pitch};
         const int rs = j0 - 2 * T;  // first streamed row
-        d2 Pq[D], Rq[D];
+        const int rend = j1 - 1 + 2 * T;
 #pragma unroll
         for (int k = 0; k < D; ++k) {
-            Pq[k] = ldp(rs + k);
-            Rq[k] = ldr(rs - 1 + k);
+            m.Pq[k] = ldv(io.sp + (long long)(rs + k) * pitch);
+            m.Rq[k] = ldv(io.rp + (long long)(rs - 1 + k) * pitch);
         }
-        d2 A[T], M1[T], M2[T], R[2 * T];
 #pragma unroll
-        for (int t = 0; t < T; ++t) A[t] = M1[t] = M2[t] = d2{0.0, 0.0};
+        for (int t = 0; t < T; ++t) m.A[t] = m.M1[t] = m.M2[t] = d2{0.0, 0.0};
 #pragma unroll
-        for (int k = 0; k < 2 * T; ++k) R[k] = d2{0.0, 0.0};
+        for (int k = 0; k < 2 * T; ++k) m.R[k] = d2{0.0, 0.0};
 
-        for (int r0 = rs; r0 <= j1 - 1 + 2 * T; ++r0) {
-            const d2 nP = ldp(r0 + D);
-            const d2 nR = ldr(r0 - 1 + D);
-            // rhs ring: R[k] = rhs(r0 - 1 - k)
+        // every cell of the cone an updated cell (no masks, no ghost rows or
+        // columns) and every output column owned (on a neighbour side the strip
+        // may run into the halo: those columns are neither stored nor counted)
+        const bool interior = c_ld >= prm.upd_lo_i && c_ld + kStripCells - 1 <= prm.upd_hi_i &&
+                              c_out + OW - 1 <= ni && rs >= prm.upd_lo_j &&
+                              rend <= prm.upd_hi_j;
+        if (!interior) {
+            for (int r0 = rs; r0 <= rend; ++r0) tb_step<T, D, NT, -1, kEdge>(m, c, io, r0);
+        } else {
+            march_interior<T, D, NT>(m, c, io, rs, rend);
+            if (!own_lane) {
 #pragma unroll
-            for (int k = 2 * T - 1; k > 0; --k) R[k] = R[k - 1];
-            R[0] = Rq[0];
-
-            d2 v = Pq[0];
-#pragma unroll
-            for (int t = 0; t < T; ++t) {
-                const d2 prevM2 = M2[t];
-                v = stage(c, t > 0, v, r0 - 2 * t, A[t], M1[t], M2[t], R[2 * t], R[2 * t + 1], acc[t]);
-                if (t == T - 1) {
-                    const int jw = r0 - 2 * T;  // row finished by the last stage
-                    if (jw >= j0 && jw < j1) {
-                        double* drow = dp + (long long)jw * pitch;
-                        auto put = [&](double* p, d2 o) {
-                            if (st_a && st_b)
-                                stv<NT>(p, o);
-                            else if (st_a)
-                                p[0] = o.x;
-                            else if (st_b)
-                                p[1] = o.y;
-                        };
-                        put(drow, v);
-                        // ghost rows of the stored field: interior columns from
-                        // the finished row, corners from the (unchanged) ghost row
-                        if (c.gb && jw == 1) {
-                            const d2 g0 = prevM2;  // the stage's row 0
-                            put(drow - pitch, d2{c.up_a ? v.x : g0.x, c.up_b ? v.y : g0.y});
-                        }
-                        if (c.gt && jw == nj) {
-                            const d2 gn = M1[t];  // the stage's row nj+1 (after its fix)
-                            put(drow + pitch, d2{c.up_a ? v.x : gn.x, c.up_b ? v.y : gn.y});
-                        }
-                    }
-                }
+                for (int t = 0; t < T; ++t) m.acc[t] = 0.0;
             }
-
-#pragma unroll
-            for (int k = 0; k + 1 < D; ++k) {
-                Pq[k] = Pq[k + 1];
-                Rq[k] = Rq[k + 1];
-            }
-            Pq[D - 1] = nP;
-            Rq[D - 1] = nR;
         }
     }
 
     // deterministic reduction per stage: lane tree, then waves in order
 #pragma unroll
     for (int t = 0; t < T; ++t) {
-        const double s = wave_sum(acc[t]);
+        const double s = wave_sum(m.acc[t]);
         if (lane == 0) wsum[t][wave] = s;
     }
     __syncthreads();
@@ -351,7 +469,11 @@ void launch_tb(hipStream_t s, int T, const SweepParams& prm, const double* src, 
     case 0: TB(TT, 4, 2); break;              \
     case 1: TB(TT, 8, 2); break;              \
     case 2: TB(TT, 4, 3); break;              \
-    default: TB(TT, 8, 3); break;             \
+    case 3: TB(TT, 8, 3); break;              \
+    case 4: TB(TT, 6, 2); break;              \
+    case 5: TB(TT, 12, 2); break;             \
+    case 6: TB(TT, 16, 2); break;             \
+    default: TB(TT, 16, 1); break;            \
     }
     // must match kTbVariants (misor_internal.h)
     switch (T) {

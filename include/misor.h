@@ -176,11 +176,12 @@ enum {
     MISOR_TUNE_OVERLAP = 5,        /* decomposed: 1 (default) = halo exchange and residual
                                     * all-reduce on a second stream, overlapped with the
                                     * interior blocks of the sweep; 0 = serial */
-    MISOR_TUNE_TSTEPS = 6,         /* iterations per pass over HBM, 1..4: 1 = single-
+    MISOR_TUNE_TSTEPS = 6,         /* iterations per pass over HBM, 1..8: 1 = single-
                                     * iteration sweep kernel, T >= 2 = temporally blocked
                                     * kernel (T iterations per read of p and rhs); the
                                     * iteration count and every bit of p are unchanged */
-    MISOR_TUNE_TB_VARIANT = 7,     /* temporally blocked kernel: 0..3 strips x rows in flight */
+    MISOR_TUNE_TB_VARIANT = 7,     /* temporally blocked kernel: 0..7 strips x rows in flight
+                                    * x rhs ring in registers / LDS */
     MISOR_TUNE_TB_ROWS = 8         /* temporally blocked kernel: rows per block; <= 0: auto */
 };
 int misor_set_tuning(misor_grid* g, int key, int value);

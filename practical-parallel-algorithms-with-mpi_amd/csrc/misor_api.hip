@@ -71,7 +71,7 @@ int size_of_rank(int rank, int size, int n) { return n / size + ((n % size > ran
 struct LocalGroup {
     int n = 0;
     std::vector<misor_grid*> members;
-    std::vector<double> vals;  // n * 4 scratch for all-reduce
+    std::vector<double> vals;  // n * kMaxT scratch for all-reduce
     std::mutex m;
     std::condition_variable cv;
     int arrived = 0;
@@ -298,22 +298,22 @@ static int exchange(misor_grid* g, double* field, int d, hipStream_t s = nullptr
     return MISOR_OK;
 }
 
-// all-reduce of n <= 4 device doubles (sum or max) across the ranks
+// all-reduce of n <= kMaxT device doubles (sum or max) across the ranks
 static int allreduce(misor_grid* g, double* dev, int n, int is_max, hipStream_t s = nullptr) {
     if (!g->dist) return MISOR_OK;
     if (!s) s = g->stream;
     if (g->local) {
         LocalGroup& G = *g->local;
-        double v[4];
+        double v[kMaxT];
         HIPCHK(hipMemcpyAsync(v, dev, sizeof(double) * n, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         const int r = g->desc.rank;
-        for (int k = 0; k < n; ++k) G.vals[4 * r + k] = v[k];
+        for (int k = 0; k < n; ++k) G.vals[kMaxT * r + k] = v[k];
         G.barrier();
         for (int k = 0; k < n; ++k) {
             double a = G.vals[k];
             for (int q = 1; q < G.n; ++q) {
-                const double b = G.vals[4 * q + k];
+                const double b = G.vals[kMaxT * q + k];
                 a = is_max ? ((a > b) ? a : b) : a + b;
             }
             v[k] = a;
@@ -559,7 +559,7 @@ int misor_create(misor_grid** out, const misor_desc* d) {
                     G = std::make_shared<LocalGroup>();
                     G->n = nranks;
                     G->members.assign(nranks, nullptr);
-                    G->vals.assign(4 * (size_t)nranks, 0.0);
+                    G->vals.assign(kMaxT * (size_t)nranks, 0.0);
                 }
                 if (G->n != nranks || G->members[d->rank])
                     CREATE_FAIL(MISOR_EINVAL, "local group %s: bad rank/size", name);

@@ -29,7 +29,7 @@ namespace misor {
 // Padding cells are zero and never feed an interior result.
 // ---------------------------------------------------------------------------
 constexpr int kXOff = 15;
-constexpr int kMaxT = 4;                 // iterations per temporally blocked pass (max)
+constexpr int kMaxT = 8;                 // iterations per temporally blocked pass (max)
 constexpr int kYOff = 2 * kMaxT;
 constexpr int kLanes = 64;                 // wavefront
 constexpr int kStripCells = 2 * kLanes;    // 128 columns per wave (2 per lane)
@@ -56,16 +56,17 @@ constexpr int kNumSweepVariants = 15;
 constexpr int kDefaultSweepVariant = 7;  // 8 strips, 2 rows ahead, nt stores (tools/tune_sweep.py)
 int sweep_waves(int variant);
 
-// temporally blocked sweep (sor_tb.hip): strips per workgroup, rows in flight
+// temporally blocked sweep (sor_tb.hip): strips per workgroup, rows in flight,
+// rhs ring in registers (0) or in LDS (1), minimum waves per SIMD (0: none)
 struct TbVariant {
-    int waves, ahead;
+    int waves, ahead, lds_ring, min_waves;
 };
-constexpr TbVariant kTbVariants[] = {{4, 2}, {8, 2}, {4, 3}, {8, 3},
-                                     {6, 2}, {12, 2}, {16, 2}, {16, 1}};
+constexpr TbVariant kTbVariants[] = {{4, 2, 0, 0}, {8, 2, 0, 0}, {4, 3, 0, 0}, {4, 2, 1, 0},
+                                     {4, 2, 1, 4}, {4, 3, 1, 0}, {8, 2, 1, 0}, {6, 2, 1, 0}};
 constexpr int kNumTbVariants = 8;
-constexpr int kDefaultTsteps = 4;      // iterations per pass (tools/tune_sweep.py --tb)
-constexpr int kDefaultTbVariant = 0;   // 4 strips, 2 rows in flight
-constexpr int kDefaultTbRows = 128;    // cap of the automatic rows per block
+constexpr int kDefaultTsteps = 6;      // iterations per pass (tools/tune_sweep.py --tb)
+constexpr int kDefaultTbVariant = 2;   // 4 strips, 3 rows in flight, rhs ring in registers
+constexpr int kDefaultTbRows = 192;    // cap of the automatic rows per block
 int tb_waves(int variant);
 int tb_out_width(int T);
 int tb_partials(int ni, int nj, int T, int rows_per_block, int waves, int* nbx, int* nby);

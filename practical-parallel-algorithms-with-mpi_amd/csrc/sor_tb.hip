@@ -1,5 +1,5 @@
 // sor_tb.hip -- temporally blocked red-black SOR for gfx950: T complete
-// solveRB iterations (assignment-4/src/solver.c:197-229, T = 1..4) per pass
+// solveRB iterations (assignment-4/src/solver.c:197-229, T = 1..8) per pass
 // over HBM.
 //
 // The single-iteration sweep (sor_kernels.hip) already moves the algorithmic
@@ -27,8 +27,10 @@
 //          rin-2, emitting row rin-2 of iteration t.  Stage T's rows
 //          j0 .. j1-1 are stored.
 //   Every stage keeps 3 rows (A = row rin-1, M1 = rin-2 half updated, M2 =
-//   final rin-3) and the rhs rows it needs come from one ring of 2T rows, so
-//   the T stages cost ~20 VGPRs each and rhs is read once.
+//   final rin-3) and the rhs rows it needs come from one ring of the last 2T
+//   streamed rows, so rhs is read from HBM once.  The ring lives in registers
+//   (8 VGPRs per stage) or -- to keep 3-4 waves per SIMD at T >= 4 -- in a
+//   lane-private LDS ring (LDS_RING variants).
 //
 // Boundary handling per stage -- identical to the reference's end-of-
 // iteration ghost copy (:219-227), applied to every intermediate iteration:
@@ -217,11 +219,11 @@ __device__ __forceinline__ d2 stage(const Lane& c, bool fixrows, d2 In, int rin,
 }
 
 // the registers of one wave's march
-template <int T, int D>
+template <int T, int D, bool LR>
 struct March {
     d2 A[T], M1[T], M2[T];
-    d2 R[2 * T];      // rhs ring: R[k] = rhs(r0 - 1 - k)
-    d2 Pq[D], Rq[D];  // rows in flight: p(r0 .. r0+D-1), rhs(r0-1 .. r0+D-2)
+    d2 R[LR ? 1 : 2 * T];  // register rhs ring: R[k] = rhs(r0 - 1 - k)
+    d2 Pq[D], Rq[D];       // rows in flight: p(r0 .. r0+D-1), rhs(r0-1 .. r0+D-2)
     double acc[T];
 };
 
@@ -230,25 +232,52 @@ struct Io {
     const double* rp;
     double* dp;
     long long pitch;
+    // LDS rhs ring (LDS_RING variants): this lane's element (row slot k,
+    // component c) at ring[k * 128 + c * 64].  Lane-private (a lane reads back
+    // only what it wrote: no barrier), component-major so each wave access is
+    // one contiguous 512-byte ds_*_b64.  Row x lives in slot x mod 2T.
+    double* ring;
 };
+
+// slot of row x in a ring of 2T rows (x >= -kYOff - 2T - 1; scalar arithmetic)
+template <int T>
+__device__ __forceinline__ int ring_slot(int x) {
+    return (x + 2 * T * 64) % (2 * T);
+}
 
 // one step of the march: stream in old row r0, push it through the T stages,
 // store the row the last stage finished (r0 - 2T) if this block owns it
-template <int T, int D, bool NT, int Q, int MODE>
-__device__ __forceinline__ void tb_step(March<T, D>& m, const Lane& c, const Io& io, int r0) {
+template <int T, int D, bool LR, bool NT, int Q, int MODE>
+__device__ __forceinline__ void tb_step(March<T, D, LR>& m, const Lane& c, const Io& io, int r0) {
     const long long pitch = io.pitch;
     const d2 nP = ldv(io.sp + (long long)(r0 + D) * pitch);
     const d2 nR = ldv(io.rp + (long long)(r0 - 1 + D) * pitch);
+    if (LR) {  // rhs(r0 - 1) joins the LDS ring
+        double* w = io.ring + ring_slot<T>(r0 - 1) * 128;
+        w[0] = m.Rq[0].x;
+        w[64] = m.Rq[0].y;
+    } else {
 #pragma unroll
-    for (int k = 2 * T - 1; k > 0; --k) m.R[k] = m.R[k - 1];
-    m.R[0] = m.Rq[0];
+        for (int k = 2 * T - 1; k > 0; --k) m.R[k] = m.R[k - 1];
+        m.R[0] = m.Rq[0];
+    }
 
     d2 v = m.Pq[0];
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         const d2 prevM2 = m.M2[t];
-        v = stage<Q, MODE>(c, t > 0, v, r0 - 2 * t, m.A[t], m.M1[t], m.M2[t], m.R[2 * t],
-                           m.R[2 * t + 1], m.acc[t]);
+        d2 Ra, Rb;
+        if (LR) {  // only component q of rows r0-2t-1 (red) and r0-2t-2 (black) is used
+            const int q = Q >= 0 ? Q : ((c.parity + r0) & 1);
+            const double ra = io.ring[ring_slot<T>(r0 - 2 * t - 1) * 128 + q * 64];
+            const double rb = io.ring[ring_slot<T>(r0 - 2 * t - 2) * 128 + q * 64];
+            Ra = d2{ra, ra};
+            Rb = d2{rb, rb};
+        } else {
+            Ra = m.R[2 * t];
+            Rb = m.R[2 * t + 1];
+        }
+        v = stage<Q, MODE>(c, t > 0, v, r0 - 2 * t, m.A[t], m.M1[t], m.M2[t], Ra, Rb, m.acc[t]);
         if (t == T - 1) {
             const int jw = r0 - 2 * T;  // row finished by the last stage
             if (MODE == kSteady) {
@@ -293,44 +322,45 @@ __device__ __forceinline__ void tb_step(March<T, D>& m, const Lane& c, const Io&
 // the colour a constant (Q0 = colour of row r0).  Steps r0 in
 // [j0+2T+1, j1-1] touch only owned rows and store unconditionally (kSteady);
 // the 4T+1 warm-up steps before and the 2T drain steps after are kWarm.
-template <int T, int D, bool NT, int Q0>
-__device__ __forceinline__ void march_interior_q(March<T, D>& m, const Lane& c, const Io& io,
-                                                 int r0, int rend) {
+template <int T, int D, bool LR, bool NT, int Q0>
+__device__ __forceinline__ void march_interior_q(March<T, D, LR>& m, const Lane& c,
+                                                 const Io& io, int r0, int rend) {
     const int sbeg = c.j0 + 2 * T + 1, send = c.j1 - 1;
     // warm-up, in pairs (keeps the colour phase); may run into the steady range
     for (; r0 + 1 < sbeg && r0 + 1 <= rend; r0 += 2) {
-        tb_step<T, D, NT, Q0, kWarm>(m, c, io, r0);
-        tb_step<T, D, NT, 1 - Q0, kWarm>(m, c, io, r0 + 1);
+        tb_step<T, D, LR, NT, Q0, kWarm>(m, c, io, r0);
+        tb_step<T, D, LR, NT, 1 - Q0, kWarm>(m, c, io, r0 + 1);
     }
     for (; r0 + 1 <= send; r0 += 2) {
-        tb_step<T, D, NT, Q0, kSteady>(m, c, io, r0);
-        tb_step<T, D, NT, 1 - Q0, kSteady>(m, c, io, r0 + 1);
+        tb_step<T, D, LR, NT, Q0, kSteady>(m, c, io, r0);
+        tb_step<T, D, LR, NT, 1 - Q0, kSteady>(m, c, io, r0 + 1);
     }
     for (; r0 + 1 <= rend; r0 += 2) {
-        tb_step<T, D, NT, Q0, kWarm>(m, c, io, r0);
-        tb_step<T, D, NT, 1 - Q0, kWarm>(m, c, io, r0 + 1);
+        tb_step<T, D, LR, NT, Q0, kWarm>(m, c, io, r0);
+        tb_step<T, D, LR, NT, 1 - Q0, kWarm>(m, c, io, r0 + 1);
     }
-    if (r0 <= rend) tb_step<T, D, NT, Q0, kWarm>(m, c, io, r0);
+    if (r0 <= rend) tb_step<T, D, LR, NT, Q0, kWarm>(m, c, io, r0);
 }
 
-template <int T, int D, bool NT>
-__device__ __forceinline__ void march_interior(March<T, D>& m, const Lane& c, const Io& io,
+template <int T, int D, bool LR, bool NT>
+__device__ __forceinline__ void march_interior(March<T, D, LR>& m, const Lane& c, const Io& io,
                                                int rs, int rend) {
     if (((c.parity + rs) & 1) == 0)
-        march_interior_q<T, D, NT, 0>(m, c, io, rs, rend);
+        march_interior_q<T, D, LR, NT, 0>(m, c, io, rs, rend);
     else
-        march_interior_q<T, D, NT, 1>(m, c, io, rs, rend);
+        march_interior_q<T, D, LR, NT, 1>(m, c, io, rs, rend);
 }
 
 }  // namespace
 
-template <int T, int WAVES, int D, bool NT>
-__global__ __launch_bounds__(kLanes* WAVES) void rb_tb_kernel(
+template <int T, int WAVES, int D, bool LR, int MINW, bool NT>
+__global__ __launch_bounds__(kLanes* WAVES, MINW) void rb_tb_kernel(
     SweepParams prm, const double* __restrict__ src, double* __restrict__ dst,
     const double* __restrict__ rhs, double* __restrict__ partials,
     const DevState* __restrict__ st, int force) {
     constexpr int OW = kStripCells - 4 * T;
     __shared__ double wsum[T][WAVES];
+    __shared__ double ring[LR ? WAVES : 1][LR ? 2 * T * kStripCells : 1];
     if (!force && st->done) return;
 
     int L = blockIdx.x;
@@ -383,7 +413,7 @@ __global__ __launch_bounds__(kLanes* WAVES) void rb_tb_kernel(
     c.idy2 = prm.idy2;
     c.coef = prm.coef;
 
-    March<T, D> m;
+    March<T, D, LR> m;
 #pragma unroll
     for (int t = 0; t < T; ++t) m.acc[t] = 0.0;
 
@@ -401,7 +431,8 @@ __global__ __launch_bounds__(kLanes* WAVES) void rb_tb_kernel(
 
     if (c_out <= ni) {  // wave-uniform
         const long long base = (long long)kYOff * pitch + kXOff + c.ia;
-        const Io io{src + base, rhs + base, dst + base, pitch};
+        const Io io{src + base, rhs + base, dst + base, pitch,
+                    LR ? &ring[LR ? wave : 0][LR ? lane : 0] : nullptr};
         const int rs = j0 - 2 * T;  // first streamed row
         const int rend = j1 - 1 + 2 * T;
 #pragma unroll
@@ -411,8 +442,13 @@ __global__ __launch_bounds__(kLanes* WAVES) void rb_tb_kernel(
         }
 #pragma unroll
         for (int t = 0; t < T; ++t) m.A[t] = m.M1[t] = m.M2[t] = d2{0.0, 0.0};
+        if (LR) {
 #pragma unroll
-        for (int k = 0; k < 2 * T; ++k) m.R[k] = d2{0.0, 0.0};
+            for (int k = 0; k < 4 * T; ++k) io.ring[k * 64] = 0.0;
+        } else {
+#pragma unroll
+            for (int k = 0; k < 2 * T; ++k) m.R[k] = d2{0.0, 0.0};
+        }
 
         // every cell of the cone an updated cell (no masks, no ghost rows or
         // columns) and every output column owned (on a neighbour side the strip
@@ -421,9 +457,9 @@ __global__ __launch_bounds__(kLanes* WAVES) void rb_tb_kernel(
                               c_out + OW - 1 <= ni && rs >= prm.upd_lo_j &&
                               rend <= prm.upd_hi_j;
         if (!interior) {
-            for (int r0 = rs; r0 <= rend; ++r0) tb_step<T, D, NT, -1, kEdge>(m, c, io, r0);
+            for (int r0 = rs; r0 <= rend; ++r0) tb_step<T, D, LR, NT, -1, kEdge>(m, c, io, r0);
         } else {
-            march_interior<T, D, NT>(m, c, io, rs, rend);
+            march_interior<T, D, LR, NT>(m, c, io, rs, rend);
             if (!own_lane) {
 #pragma unroll
                 for (int t = 0; t < T; ++t) m.acc[t] = 0.0;
@@ -461,26 +497,30 @@ int tb_partials(int ni, int nj, int T, int rows_per_block, int waves, int* nbx, 
 
 void launch_tb(hipStream_t s, int T, const SweepParams& prm, const double* src, double* dst,
                const double* rhs, double* partials, const DevState* st, int force) {
-#define TB(TT, W, DD)                                                                      \
-    hipLaunchKernelGGL((rb_tb_kernel<TT, W, DD, true>), dim3(prm.nblocks), dim3(kLanes * W), \
-                       0, s, prm, src, dst, rhs, partials, st, force)
+#define TB(TT, W, DD, LR, MW)                                                  \
+    hipLaunchKernelGGL((rb_tb_kernel<TT, W, DD, LR, MW, true>), dim3(prm.nblocks), \
+                       dim3(kLanes * W), 0, s, prm, src, dst, rhs, partials, st, force)
 #define TB_T(TT)                              \
     switch (prm.variant) {                    \
-    case 0: TB(TT, 4, 2); break;              \
-    case 1: TB(TT, 8, 2); break;              \
-    case 2: TB(TT, 4, 3); break;              \
-    case 3: TB(TT, 8, 3); break;              \
-    case 4: TB(TT, 6, 2); break;              \
-    case 5: TB(TT, 12, 2); break;             \
-    case 6: TB(TT, 16, 2); break;             \
-    default: TB(TT, 16, 1); break;            \
+    case 0: TB(TT, 4, 2, false, 1); break;    \
+    case 1: TB(TT, 8, 2, false, 1); break;    \
+    case 2: TB(TT, 4, 3, false, 1); break;    \
+    case 3: TB(TT, 4, 2, true, 1); break;     \
+    case 4: TB(TT, 4, 2, true, 4); break;     \
+    case 5: TB(TT, 4, 3, true, 1); break;     \
+    case 6: TB(TT, 8, 2, true, 1); break;     \
+    default: TB(TT, 6, 2, true, 1); break;    \
     }
     // must match kTbVariants (misor_internal.h)
     switch (T) {
     case 1: TB_T(1); break;
     case 2: TB_T(2); break;
     case 3: TB_T(3); break;
-    default: TB_T(4); break;
+    case 4: TB_T(4); break;
+    case 5: TB_T(5); break;
+    case 6: TB_T(6); break;
+    case 7: TB_T(7); break;
+    default: TB_T(8); break;
     }
 #undef TB_T
 #undef TB

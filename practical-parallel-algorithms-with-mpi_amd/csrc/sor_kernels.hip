@@ -313,36 +313,53 @@ __global__ __launch_bounds__(kLanes* WAVES) void rb_sweep_kernel(
 __global__ __launch_bounds__(1024) void rb_finish_kernel(const double* __restrict__ partials,
                                                          int n, int T, DevState* st,
                                                          double cells, int decide) {
-    __shared__ double sh[1024];
+    __shared__ double sh[kMaxT][1024];
+    __shared__ double tot[kMaxT];
     if (st->done) return;
     const int t = threadIdx.x;
-    for (int s_ = 0; s_ < T; ++s_) {
-        const double* pp = partials + (long long)s_ * n;
-        double s = 0.0;
-        for (int k = t; k < n; k += 1024) s += pp[k];
-        sh[t] = s;
-        __syncthreads();
+    // all T groups in one strided pass (T independent loads in flight per thread)
+    double s[kMaxT];
 #pragma unroll
-        for (int w = 512; w >= 64; w >>= 1) {
-            if (t < w) sh[t] += sh[t + w];
-            __syncthreads();
+    for (int g = 0; g < kMaxT; ++g) s[g] = 0.0;
+    for (int k = t; k < n; k += 1024) {
+#pragma unroll
+        for (int g = 0; g < kMaxT; ++g)
+            if (g < T) s[g] += partials[(long long)g * n + k];
+    }
+#pragma unroll
+    for (int g = 0; g < kMaxT; ++g)
+        if (g < T) sh[g][t] = s[g];
+    __syncthreads();
+#pragma unroll
+    for (int w = 512; w >= 64; w >>= 1) {
+        if (t < w) {
+#pragma unroll
+            for (int g = 0; g < kMaxT; ++g)
+                if (g < T) sh[g][t] += sh[g][t + w];
         }
-        if (t < 64) {
-            double v = sh[t];
-            v = wave_sum(v);
-            if (t == 0) {
-                if (!decide) {
-                    st->sum[s_] = v;  // decomposed: all-reduce, then decide
-                } else if (!st->done) {
-                    const double res = v / cells;
-                    const int it = st->it + 1;
-                    st->res = res;
-                    st->it = it;
-                    st->done = !((res >= st->epssq) && (it < st->itermax));
-                }
+        __syncthreads();
+    }
+    if (t < 64) {
+#pragma unroll
+        for (int g = 0; g < kMaxT; ++g) {
+            if (g < T) {
+                const double v = wave_sum(sh[g][t]);
+                if (t == 0) tot[g] = v;
             }
         }
-        __syncthreads();
+    }
+    if (t == 0) {
+        for (int g = 0; g < T; ++g) {
+            if (!decide) {
+                st->sum[g] = tot[g];  // decomposed: all-reduce, then decide
+            } else if (!st->done) {
+                const double res = tot[g] / cells;
+                const int it = st->it + 1;
+                st->res = res;
+                st->it = it;
+                st->done = !((res >= st->epssq) && (it < st->itermax));
+            }
+        }
     }
 }
 

@@ -135,6 +135,14 @@ int misor_synchronize(misor_grid* g);
 
 int misor_upload(misor_grid* g, int field, const double* host);
 int misor_download(misor_grid* g, int field, double* host);
+/* collectResult / assembleResult (assignment-5/skeleton/src/solver.c:234-359):
+ * collective over the ranks of a decomposed grid.  Rank 0 receives the whole
+ * field, (imax+2) x (jmax+2) doubles in the reference layout, in `host_global`;
+ * every rank contributes its interior plus the ghost layer on its physical
+ * sides; other ranks pass NULL.  With one rank it is misor_download. */
+int misor_gather(misor_grid* g, int field, double* host_global);
+/* number of visible GPUs (host programs map rank -> device) */
+int misor_device_count(int* n);
 /* fill a field (incl. ghosts) with a constant; initSolver of NS (solver.c:92-99) */
 int misor_fill(misor_grid* g, int field, double value);
 

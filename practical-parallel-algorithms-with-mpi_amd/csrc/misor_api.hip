@@ -142,6 +142,8 @@ struct misor_grid {
     hipEvent_t ev_s = nullptr, ev_x = nullptr, ev_d = nullptr;
     double* sendbuf = nullptr;
     double* recvbuf = nullptr;
+    double* gbuf = nullptr;  // misor_gather: this rank's owned block, packed
+    long long gbuf_cap = 0;
 
     // stats
     bool timing = false;
@@ -215,6 +217,7 @@ void misor_destroy(misor_grid* g) {
     (void)hipHostFree(g->red_host);
     (void)hipFree(g->sendbuf);
     (void)hipFree(g->recvbuf);
+    (void)hipFree(g->gbuf);
     if (g->cstream) (void)hipStreamSynchronize(g->cstream);
     if (g->cstream) (void)hipStreamDestroy(g->cstream);
     if (g->ev_s) (void)hipEventDestroy(g->ev_s);
@@ -654,6 +657,113 @@ int misor_download(misor_grid* g, int field, double* host) {
     HIPCHK(hipMemcpy2DAsync(host, w, origin(g, field_ptr(g, field)), g->pitch * sizeof(double), w,
                             h, hipMemcpyDeviceToHost, g->stream));
     HIPCHK(hipStreamSynchronize(g->stream));
+    return MISOR_OK;
+}
+
+// The block a rank contributes to the assembled global field: its interior
+// plus the ghost layer on its physical sides (assembleResult,
+// assignment-5/skeleton/src/solver.c:234-300), in local indices.
+struct OwnedBlock {
+    int i0, j0, w, h;    // first local cell and extent
+    int gi0, gj0;        // first global cell
+};
+static OwnedBlock owned_block(const misor_local& L) {
+    OwnedBlock b{};
+    b.i0 = L.neighbours[0] < 0 ? 0 : 1;
+    b.j0 = L.neighbours[2] < 0 ? 0 : 1;
+    const int i1 = L.neighbours[1] < 0 ? L.ni + 1 : L.ni;
+    const int j1 = L.neighbours[3] < 0 ? L.nj + 1 : L.nj;
+    b.w = i1 - b.i0 + 1;
+    b.h = j1 - b.j0 + 1;
+    b.gi0 = L.ioff + b.i0;
+    b.gj0 = L.joff + b.j0;
+    return b;
+}
+
+int misor_gather(misor_grid* g, int field, double* host) {
+    if (!g || !field_ptr(g, field)) return fail(MISOR_EINVAL, "bad gather");
+    const int rank = g->dist ? g->desc.rank : 0;
+    if (rank == 0 && !host) return fail(MISOR_EINVAL, "gather: rank 0 needs the global array");
+    if (g->desc.nranks == 1) return misor_download(g, field, host);
+    HIPCHK(hipSetDevice(g->device));
+    const size_t gw = (size_t)(g->desc.imax + 2);  // global row length (doubles)
+    const OwnedBlock mine = owned_block(g->loc);
+    // every rank packs its block contiguously (a strided 2D copy on the device)
+    long long need = (long long)(g->loc.ni + 2) * (g->loc.nj + 2);
+    if (rank == 0) {
+        for (int r = 0; r < g->desc.nranks; ++r) {
+            misor_local L{};
+            int rc = misor_decompose(g->desc.nranks, r, g->desc.imax, g->desc.jmax,
+                                     g->loc.dims, &L);
+            if (rc) return rc;
+            need = std::max(need, (long long)(L.ni + 2) * (L.nj + 2));
+        }
+    }
+    if (need > g->gbuf_cap) {
+        (void)hipFree(g->gbuf);
+        g->gbuf = nullptr;
+        g->gbuf_cap = 0;
+        HIPCHK(hipMalloc(&g->gbuf, sizeof(double) * (size_t)need));
+        g->gbuf_cap = need;
+    }
+    const double* f = field_ptr(g, field);
+    const double* src = origin(g, const_cast<double*>(f)) + (long long)mine.j0 * g->pitch + mine.i0;
+    HIPCHK(hipMemcpy2DAsync(g->gbuf, sizeof(double) * mine.w, src, sizeof(double) * g->pitch,
+                            sizeof(double) * mine.w, mine.h, hipMemcpyDeviceToDevice, g->stream));
+    HIPCHK(hipStreamSynchronize(g->stream));
+    auto to_host = [&](const double* dev, const OwnedBlock& b) -> int {
+        HIPCHK(hipMemcpy2DAsync(host + (size_t)b.gj0 * gw + b.gi0, sizeof(double) * gw, dev,
+                                sizeof(double) * b.w, sizeof(double) * b.w, b.h,
+                                hipMemcpyDeviceToHost, g->stream));
+        HIPCHK(hipStreamSynchronize(g->stream));
+        return MISOR_OK;
+    };
+    if (g->local) {
+        g->local->barrier();  // every block packed
+        if (rank == 0) {
+            for (int r = 0; r < g->desc.nranks; ++r) {
+                const misor_grid* q = g->local->members[r];
+                const OwnedBlock b = owned_block(q->loc);
+                int rc = to_host(q->gbuf, b);  // unified addressing: any member's device
+                if (rc) return rc;
+            }
+        }
+        g->local->barrier();  // nobody repacks before rank 0 has read
+        return MISOR_OK;
+    }
+    // RCCL: rank r sends its packed block to rank 0, one peer at a time
+    double* stage = nullptr;
+    if (rank == 0) {
+        int rc = to_host(g->gbuf, mine);
+        if (rc) return rc;
+        HIPCHK(hipMalloc(&stage, sizeof(double) * (size_t)need));
+    }
+    int rc = MISOR_OK;
+    for (int r = 1; r < g->desc.nranks && rc == MISOR_OK; ++r) {
+        misor_local L{};
+        rc = misor_decompose(g->desc.nranks, r, g->desc.imax, g->desc.jmax, g->loc.dims, &L);
+        if (rc) break;
+        const OwnedBlock b = owned_block(L);
+        const size_t count = (size_t)b.w * b.h;
+        if (rank == r) {
+            if (ncclSend(g->gbuf, count, ncclDouble, 0, g->comm, g->stream) != ncclSuccess)
+                rc = fail(MISOR_ECOMM, "gather: ncclSend failed");
+        } else if (rank == 0) {
+            if (ncclRecv(stage, count, ncclDouble, r, g->comm, g->stream) != ncclSuccess)
+                rc = fail(MISOR_ECOMM, "gather: ncclRecv failed");
+            else
+                rc = to_host(stage, b);
+        }
+    }
+    if (stage) (void)hipFree(stage);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(g->stream));
+    return MISOR_OK;
+}
+
+int misor_device_count(int* n) {
+    if (!n) return fail(MISOR_EINVAL, "null argument");
+    HIPCHK(hipGetDeviceCount(n));
     return MISOR_OK;
 }
 

@@ -506,7 +506,7 @@ void launch_tb(hipStream_t s, int T, const SweepParams& prm, const double* src, 
     case 1: TB(TT, 8, 2, false, 1); break;    \
     case 2: TB(TT, 4, 3, false, 1); break;    \
     case 3: TB(TT, 4, 2, true, 1); break;     \
-    case 4: TB(TT, 4, 2, true, 4); break;     \
+    case 4: TB(TT, 4, 2, true, (TT <= 4 ? 4 : 1)); break; \
     case 5: TB(TT, 4, 3, true, 1); break;     \
     case 6: TB(TT, 8, 2, true, 1); break;     \
     default: TB(TT, 6, 2, true, 1); break;    \

@@ -4,6 +4,9 @@
  * notes): dt from max|u|,|v| over all cells incl. ghosts, normalizePressure
  * over all cells, dcavity lid for i < imax, canal parabolic inflow.  The
  * pressure solve is red-black SOR (solveRB); `solve` maps to it.
+ * Decomposed runs (host/ranks.h): each rank owns a block of the 2D
+ * decomposition; writeResult first assembles p, u, v on rank 0 (collectResult,
+ * assignment-5/skeleton/src/solver.c:320-359) and only rank 0 writes.
  */
 #include "solver_ns.h"
 
@@ -12,6 +15,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "ranks.h"
 #include "util.h"
 
 void initSolver(Solver* solver, Parameter* params)
@@ -52,8 +56,13 @@ void initSolver(Solver* solver, Parameter* params)
     d.eps = solver->eps;
     d.itermax = solver->itermax;
     d.variant = MISOR_SOLVE_RB;
-    d.device = -1;
-    d.nranks = 1;
+    const RankCtx* rk = currentRank();
+    d.device = rk->device;
+    d.nranks = rk->size;
+    d.rank = rk->rank;
+    d.comm_id = rk->comm_id;
+    solver->rank = rk->rank;
+    solver->size = rk->size;
     misorCheck(misor_create(&solver->dev, &d), "misor_create");
 
     misor_ns_desc n = { 0 };
@@ -123,7 +132,7 @@ void solveRB(Solver* solver)
     misorCheck(misor_solve_rb(solver->dev, &it, &res), "misor_solve_rb");
     solver->lastIterations = it;
 #ifdef VERBOSE
-    printf("Solver took %d iterations to reach %f\n", it, sqrt(res));
+    if (solver->rank == 0) printf("Solver took %d iterations to reach %f\n", it, sqrt(res));
 #endif
 }
 
@@ -135,18 +144,20 @@ void adaptUV(Solver* solver)
     misorCheck(misor_adapt_uv(solver->dev), "misor_adapt_uv");
 }
 
-/* solver.c:457-505 */
+/* solver.c:457-505; collective in a decomposed run (collectResult) */
 void writeResult(Solver* solver)
 {
     int imax = solver->imax, jmax = solver->jmax;
     double dx = solver->dx, dy = solver->dy;
     size_t n = (size_t)(imax + 2) * (size_t)(jmax + 2);
-    if (!solver->p) solver->p = allocate(64, n * sizeof(double));
-    if (!solver->u) solver->u = allocate(64, n * sizeof(double));
-    if (!solver->v) solver->v = allocate(64, n * sizeof(double));
-    misorCheck(misor_download(solver->dev, MISOR_P, solver->p), "misor_download");
-    misorCheck(misor_download(solver->dev, MISOR_U, solver->u), "misor_download");
-    misorCheck(misor_download(solver->dev, MISOR_V, solver->v), "misor_download");
+    const int root = solver->rank == 0;
+    if (root && !solver->p) solver->p = allocate(64, n * sizeof(double));
+    if (root && !solver->u) solver->u = allocate(64, n * sizeof(double));
+    if (root && !solver->v) solver->v = allocate(64, n * sizeof(double));
+    misorCheck(misor_gather(solver->dev, MISOR_P, root ? solver->p : NULL), "misor_gather");
+    misorCheck(misor_gather(solver->dev, MISOR_U, root ? solver->u : NULL), "misor_gather");
+    misorCheck(misor_gather(solver->dev, MISOR_V, root ? solver->v : NULL), "misor_gather");
+    if (!root) return;
 #define AT(a, i, j) (a)[(size_t)(j) * (size_t)(imax + 2) + (size_t)(i)]
     FILE* fp = fopen("pressure.dat", "w");
     if (fp == NULL) {

@@ -31,6 +31,7 @@ typedef struct {
     int bcLeft, bcRight, bcBottom, bcTop;
     misor_grid* dev; /* device-resident state (added) */
     int lastIterations; /* iterations of the last pressure solve (added) */
+    int rank, size;     /* this rank of a decomposed run (added; 0 of 1 on one GPU) */
 } Solver;
 
 extern void initSolver(Solver*, Parameter*);

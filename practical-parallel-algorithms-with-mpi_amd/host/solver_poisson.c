@@ -9,13 +9,34 @@
  *   solve       : the reference's lexicographic SOR has no data-parallel form;
  *                 on the GPU it runs solveRB (red-black ordering)
  *   writeResult : "%f " for every cell incl. ghosts, '\n' per row, solver.c:301-323
+ * Decomposed runs (host/ranks.h): every rank owns a block of the 2D
+ * decomposition; getResult assembles p on rank 0 (the collectResult of
+ * assignment-5/skeleton/src/solver.c:234-359), which alone prints and writes.
  */
 #include "solver_poisson.h"
 
 #include <stdio.h>
 #include <stdlib.h>
 
+#include "ranks.h"
 #include "util.h"
+
+static void fill_desc(misor_desc* d, const Solver* solver, int variant)
+{
+    const RankCtx* rk = currentRank();
+    d->imax = solver->imax;
+    d->jmax = solver->jmax;
+    d->dx = solver->dx;
+    d->dy = solver->dy;
+    d->omega = solver->omega;
+    d->eps = solver->eps;
+    d->itermax = solver->itermax;
+    d->variant = variant;
+    d->device = rk->device;
+    d->nranks = rk->size;
+    d->rank = rk->rank;
+    d->comm_id = rk->comm_id;
+}
 
 void initSolver(Solver* solver, Parameter* params, int problem)
 {
@@ -26,25 +47,18 @@ void initSolver(Solver* solver, Parameter* params, int problem)
     solver->eps = params->eps;
     solver->omega = params->omg;
     solver->itermax = params->itermax;
-    solver->rank = 0;
-    solver->size = 1;
-    solver->jmaxLocal = solver->jmax;
+    solver->rank = currentRank()->rank;
+    solver->size = currentRank()->size;
     solver->ys = 0.0;
     solver->p = NULL;
     solver->rhs = NULL;
 
     misor_desc d = { 0 };
-    d.imax = solver->imax;
-    d.jmax = solver->jmax;
-    d.dx = solver->dx;
-    d.dy = solver->dy;
-    d.omega = solver->omega;
-    d.eps = solver->eps;
-    d.itermax = solver->itermax;
-    d.variant = MISOR_SOLVE_RB;
-    d.device = -1;
-    d.nranks = 1;
+    fill_desc(&d, solver, MISOR_SOLVE_RB);
     misorCheck(misor_create(&solver->dev, &d), "misor_create");
+    misor_local loc;
+    misorCheck(misor_local_info(solver->dev, &loc), "misor_local_info");
+    solver->jmaxLocal = loc.nj;
     misorCheck(misor_poisson_init(solver->dev, params->xlength, params->ylength, problem),
                "misor_poisson_init");
 }
@@ -55,7 +69,7 @@ static void run(Solver* solver, int variant)
     double res = 0.0;
     (void)variant;
     misorCheck(misor_solve_rb(solver->dev, &it, &res), "misor_solve_rb");
-    printf("%d ", it);
+    if (solver->rank == 0) printf("%d ", it);
 }
 
 void solveRB(Solver* solver) { run(solver, MISOR_SOLVE_RB); }
@@ -65,24 +79,17 @@ void solve(Solver* solver) { run(solver, MISOR_SOLVE_RB); }
 void solveRBA(Solver* solver)
 {
     /* the update form is a property of the device grid: rebuild it as RBA,
-     * carrying the current p and rhs over */
-    size_t n = (size_t)(solver->imax + 2) * (size_t)(solver->jmax + 2);
+     * carrying this rank's current p and rhs over */
+    misor_local loc;
+    misorCheck(misor_local_info(solver->dev, &loc), "misor_local_info");
+    size_t n = (size_t)(loc.ni + 2) * (size_t)(loc.nj + 2);
     double* p = allocate(64, n * sizeof(double));
     double* rhs = allocate(64, n * sizeof(double));
     misorCheck(misor_download(solver->dev, MISOR_P, p), "misor_download");
     misorCheck(misor_download(solver->dev, MISOR_RHS, rhs), "misor_download");
     misor_destroy(solver->dev);
     misor_desc d = { 0 };
-    d.imax = solver->imax;
-    d.jmax = solver->jmax;
-    d.dx = solver->dx;
-    d.dy = solver->dy;
-    d.omega = solver->omega;
-    d.eps = solver->eps;
-    d.itermax = solver->itermax;
-    d.variant = MISOR_SOLVE_RBA;
-    d.device = -1;
-    d.nranks = 1;
+    fill_desc(&d, solver, MISOR_SOLVE_RBA);
     misorCheck(misor_create(&solver->dev, &d), "misor_create");
     misorCheck(misor_upload(solver->dev, MISOR_P, p), "misor_upload");
     misorCheck(misor_upload(solver->dev, MISOR_RHS, rhs), "misor_upload");
@@ -91,11 +98,13 @@ void solveRBA(Solver* solver)
     run(solver, MISOR_SOLVE_RBA);
 }
 
+/* collective: rank 0 receives the whole p (assembled from every rank's block) */
 void getResult(Solver* solver)
 {
     size_t n = (size_t)(solver->imax + 2) * (size_t)(solver->jmax + 2);
-    if (!solver->p) solver->p = allocate(64, n * sizeof(double));
-    misorCheck(misor_download(solver->dev, MISOR_P, solver->p), "misor_download");
+    if (solver->rank == 0 && !solver->p) solver->p = allocate(64, n * sizeof(double));
+    misorCheck(misor_gather(solver->dev, MISOR_P, solver->rank == 0 ? solver->p : NULL),
+               "misor_gather");
 }
 
 void writeResult(Solver* solver, char* filename)
@@ -103,6 +112,7 @@ void writeResult(Solver* solver, char* filename)
     int imax = solver->imax;
     int jmax = solver->jmax;
     getResult(solver);
+    if (solver->rank != 0) return;
     double* p = solver->p;
 
     FILE* fp = fopen(filename, "w");

@@ -70,6 +70,8 @@ SIGNATURES = {
     "misor_upload": (C.c_int, [C.c_void_p, C.c_int, _dp]),
     "misor_download": (C.c_int, [C.c_void_p, C.c_int, _dp]),
     "misor_fill": (C.c_int, [C.c_void_p, C.c_int, C.c_double]),
+    "misor_gather": (C.c_int, [C.c_void_p, C.c_int, _dp]),
+    "misor_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "misor_poisson_init": (C.c_int, [C.c_void_p, C.c_double, C.c_double, C.c_int]),
     "misor_solve_rb": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), _dp]),
     "misor_solve_rb_n": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_int), _dp]),
@@ -153,6 +155,7 @@ class Grid:
         self.loc = Local()
         _check(lib().misor_local_info(self.h, C.byref(self.loc)))
         self.shape = (self.loc.nj + 2, self.loc.ni + 2)
+        self.imax, self.jmax, self.rank, self.nranks = imax, jmax, rank, nranks
 
     def close(self):
         if self.h:
@@ -180,6 +183,16 @@ class Grid:
         a = np.empty(self.shape)
         _check(lib().misor_download(self.h, field, _ptr(a)))
         return a
+
+    def gather(self, field):
+        """collectResult: the global (jmax+2, imax+2) field on rank 0, None elsewhere
+        (collective: every rank of the grid must call it)"""
+        if self.rank == 0:
+            out = np.empty((self.jmax + 2, self.imax + 2))
+            _check(lib().misor_gather(self.h, field, _ptr(out)))
+            return out
+        _check(lib().misor_gather(self.h, field, C.cast(None, _dp)))
+        return None
 
     def fill(self, field, value):
         _check(lib().misor_fill(self.h, field, value))

@@ -144,6 +144,31 @@ def test_converges_mid_pass_decomposed(world, T):
     assert np.array_equal(got, want)
 
 
+@pytest.mark.parametrize("world,dims", [(2, (0, 0)), (4, (0, 0)), (6, (3, 2)), (4, (1, 4))])
+def test_gather_assembles_global_field(world, dims):
+    """misor_gather (collectResult): rank 0 receives every rank's block incl.
+    the physical ghost layer -- the whole (jmax+2) x (imax+2) field"""
+    ni, nj = 97, 61
+    rng = np.random.default_rng(world)
+    p = rng.standard_normal((nj + 2, ni + 2))
+    rhs = rng.standard_normal((nj + 2, ni + 2))
+    want = p.copy()
+    orc.solve_rb(want, rhs, 1.0 / ni, 1.0 / nj, 1.7, 1e-300, 5)
+
+    def rank_fn(r, cid, dims):
+        with M.Grid(ni, nj, 1.0 / ni, 1.0 / nj, 1.7, 1e-300, 5, device=0, nranks=world, rank=r,
+                    dims=dims, comm_id=cid) as g:
+            g.upload(M.P, local_window(p, g.loc))
+            g.upload(M.RHS, local_window(rhs, g.loc))
+            g.solve_rb()
+            return g.gather(M.P), g.gather(M.RHS)
+
+    outs = run_ranks(world, rank_fn, dims)
+    assert all(o[0] is None and o[1] is None for o in outs[1:])
+    assert np.array_equal(outs[0][0], want)
+    assert np.array_equal(outs[0][1], rhs)
+
+
 def test_rccl_single_rank_path(golden):
     """nranks=1 with a real RCCL id: the decomposed code path (RCCL init and
     all-reduce on the comm stream, interior/boundary split launches) on the

@@ -52,3 +52,48 @@ def test_exe_ns_dcavity(golden, tmp_path):
     vc = ((v[1:-1, 1:-1] + v[:-2, 1:-1]) / 2.0).ravel()
     assert np.abs(ve[:, 2] - uc).max() <= 1e-6
     assert np.abs(ve[:, 3] - vc).max() <= 1e-6
+
+
+@pytest.mark.parametrize("ranks", [2, 3, 4])
+def test_exe_poisson_decomposed(golden, tmp_path, ranks):
+    """MISOR_RANKS=N: N ranks (threads, in-process transport) on a 2D
+    decomposition, p assembled on rank 0 (collectResult) -> the same p.dat"""
+    shutil.copy(os.path.join(golden, "a4_poisson.par"), tmp_path / "poisson.par")
+    env = dict(os.environ, MISOR_RANKS=str(ranks))
+    out = subprocess.run([os.path.join(BIN, "exe-poisson"), "poisson.par"], cwd=tmp_path,
+                         env=env, capture_output=True, text=True, timeout=120, check=True).stdout
+    assert out.count("Parameters:") == 1 and out.count("Walltime") == 1
+    assert re.search(r"(^|\s)2388 ", out), out
+    z = np.load(os.path.join(golden, "rb_poisson100.npz"))
+    assert (tmp_path / "p.dat").read_text() == fmt_pdat(z["p"])
+
+
+@pytest.mark.parametrize("par,ranks", [("a6_dcavity.par", 4), ("a6_canal.par", 2),
+                                       ("a6_canal.par", 4)])
+def test_exe_ns_decomposed_matches_single(golden, tmp_path, par, ranks):
+    """the NS program decomposed over N ranks writes the same pressure.dat /
+    velocity.dat as on one GPU and takes the same pressure iterations per step"""
+    name = par[3:]
+    txt = open(os.path.join(golden, par)).read()
+    txt = re.sub(r"(?m)^te .*$", "te       0.3", txt)
+    runs = {}
+    for n in (1, ranks):
+        d = tmp_path / ("r%d" % n)
+        d.mkdir()
+        (d / name).write_text(txt)
+        env = dict(os.environ, MISOR_RANKS=str(n), MISOR_ITERLOG=str(d / "iters.log"))
+        out = subprocess.run([os.path.join(BIN, "exe-ns"), name], cwd=d, env=env,
+                             capture_output=True, text=True, timeout=300, check=True).stdout
+        assert out.count("Solution took") == 1
+        runs[n] = d
+    a, b = runs[1], runs[ranks]
+    la, lb = np.loadtxt(a / "iters.log"), np.loadtxt(b / "iters.log")
+    assert la.shape == lb.shape and len(la) > 3
+    assert np.array_equal(la[:, 3], lb[:, 3])  # pressure iterations per step
+    # dt is a max-reduction (order-free), but normalizePressure's mean is a sum:
+    # its rounding depends on the partition, so p, u and hence dt agree to ~1 ulp
+    assert np.allclose(la[:, 2], lb[:, 2], rtol=1e-12, atol=0)
+    for f in ("pressure.dat", "velocity.dat"):
+        ta, tb = (a / f).read_text(), (b / f).read_text()
+        if ta != tb:  # at most one unit in the last printed digit ("%f")
+            assert np.abs(np.loadtxt(a / f) - np.loadtxt(b / f)).max() <= 1.01e-6, f

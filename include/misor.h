@@ -159,6 +159,13 @@ int misor_poisson_init(misor_grid* g, double xlength, double ylength, int proble
 int misor_solve_rb(misor_grid* g, int* iters, double* res);
 /* the same with an explicit cap that overrides desc.itermax for this call */
 int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res);
+/* The reference's lexicographic Gauss-Seidel SOR `solve` (what its programs
+ * call): assignment-4/src/solver.c:126-177 (xorder = MISOR_LEX_A4) and
+ * assignment-5/sequential/src/solver.c:140-191 (xorder = MISOR_LEX_SEQ; the
+ * two differ only in the order of the stencil terms), bit for bit, as an
+ * anti-diagonal wavefront in one workgroup.  Single rank, variant RB only. */
+enum { MISOR_LEX_A4 = 0, MISOR_LEX_SEQ = 1 };
+int misor_solve_lex(misor_grid* g, int xorder, int* iters, double* res);
 
 /* NS step kernels (assignment-5/sequential/src/solver.c) */
 int misor_ns_setup(misor_grid* g, const misor_ns_desc* ns);

@@ -1018,6 +1018,36 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
     return MISOR_OK;
 }
 
+int misor_solve_lex(misor_grid* g, int xorder, int* iters, double* res) {
+    if (!g) return fail(MISOR_EINVAL, "null grid");
+    if (g->desc.nranks != 1)
+        return fail(MISOR_ESTATE, "lexicographic SOR has no decomposed form (use red-black)");
+    if (g->desc.variant != MISOR_SOLVE_RB)
+        return fail(MISOR_ESTATE, "lexicographic SOR uses the solveRB factor (variant RB)");
+    HIPCHK(hipSetDevice(g->device));
+    const double epssq = g->desc.eps * g->desc.eps;
+    DevState s0{};
+    s0.res = 1.0;
+    s0.epssq = epssq;
+    s0.itermax = g->desc.itermax;
+    *g->st_host = s0;
+    HIPCHK(hipMemcpyAsync(g->st, g->st_host, sizeof(DevState), hipMemcpyHostToDevice,
+                          g->stream));
+    const double cells = (double)g->desc.imax * (double)g->desc.jmax;
+    launch_solve_lex(g->stream, g->fld[g->cur], g->fld[kRhs], g->loc.ni, g->loc.nj, g->pitch,
+                     g->sp.idx2, g->sp.idy2, g->sp.coef, cells, xorder != 0, g->st);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(g->st_host, g->st, sizeof(DevState), hipMemcpyDeviceToHost,
+                          g->stream));
+    HIPCHK(hipStreamSynchronize(g->stream));
+    const int it = g->st_host->it;
+    g->last_iters = it;
+    g->stats.sweeps += it;
+    if (iters) *iters = it;
+    if (res) *res = g->st_host->res;
+    return MISOR_OK;
+}
+
 int misor_solve_rb(misor_grid* g, int* iters, double* res) {
     if (!g) return fail(MISOR_EINVAL, "null grid");
     return misor_solve_rb_n(g, g->desc.itermax, iters, res);

@@ -118,6 +118,10 @@ void launch_finish(hipStream_t s, const double* partials, int nparts, int T, Dev
 void launch_decide(hipStream_t s, DevState* st, int T, double cells);
 void launch_tb(hipStream_t s, int T, const SweepParams& prm, const double* src, double* dst,
                const double* rhs, double* partials, const DevState* st, int force);
+// lexicographic Gauss-Seidel SOR, whole solve in one workgroup (lex_kernels.hip)
+void launch_solve_lex(hipStream_t s, double* p, const double* rhs, int ni, int nj,
+                      long long pitch, double idx2, double idy2, double factor, double cells,
+                      int xorder, DevState* st);
 // whole-solve single-workgroup kernel for grids whose p fits in LDS
 int small_solve_fits(int ni, int nj);
 void launch_solve_small(hipStream_t s, double* p, const double* rhs, int ni, int nj,

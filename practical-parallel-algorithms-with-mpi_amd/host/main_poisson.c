@@ -21,7 +21,7 @@ static int rank_main(const RankCtx* rk, void* arg)
 
     initSolver(&solver, &params, 2);
     startTime = getTimeStamp();
-    solveRB(&solver);
+    solve(&solver); /* assignment-4/src/main.c:34 */
     endTime = getTimeStamp();
     writeResult(&solver, "p.dat");
 

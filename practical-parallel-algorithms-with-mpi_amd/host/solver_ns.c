@@ -3,7 +3,8 @@
  * wrappers over libmisor.  Semantics are the sequential solver's (SURVEY 8a
  * notes): dt from max|u|,|v| over all cells incl. ghosts, normalizePressure
  * over all cells, dcavity lid for i < imax, canal parabolic inflow.  The
- * pressure solve is red-black SOR (solveRB); `solve` maps to it.
+ * pressure solve is red-black SOR (solveRB); `solve` maps to it unless
+ * MISOR_SOLVER=lex selects the reference's lexicographic solve.
  * Decomposed runs (host/ranks.h): each rank owns a block of the 2D
  * decomposition; writeResult first assembles p, u, v on rank 0 (collectResult,
  * assignment-5/skeleton/src/solver.c:320-359) and only rank 0 writes.
@@ -136,7 +137,23 @@ void solveRB(Solver* solver)
 #endif
 }
 
-void solve(Solver* solver) { solveRB(solver); }
+/* red-black by default; MISOR_SOLVER=lex: the reference's own lexicographic
+ * solve (assignment-5/sequential/src/solver.c:140-191), bit for bit */
+void solve(Solver* solver)
+{
+    const char* s = getenv("MISOR_SOLVER");
+    if (!(s && strcmp(s, "lex") == 0)) {
+        solveRB(solver);
+        return;
+    }
+    int it = 0;
+    double res = 0.0;
+    misorCheck(misor_solve_lex(solver->dev, MISOR_LEX_SEQ, &it, &res), "misor_solve_lex");
+    solver->lastIterations = it;
+#ifdef VERBOSE
+    if (solver->rank == 0) printf("Solver took %d iterations to reach %f\n", it, sqrt(res));
+#endif
+}
 
 void adaptUV(Solver* solver)
 {

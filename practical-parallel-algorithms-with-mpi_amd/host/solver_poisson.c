@@ -6,8 +6,10 @@
  *   solveRB     : red-black SOR until res < eps^2 or itermax, prints "%d "
  *                 (the iteration count), solver.c:179-238
  *   solveRBA    : the omega-outside variant, solver.c:240-299
- *   solve       : the reference's lexicographic SOR has no data-parallel form;
- *                 on the GPU it runs solveRB (red-black ordering)
+ *   solve       : red-black SOR by default (the data-parallel production path,
+ *                 DESIGN.md); MISOR_SOLVER=lex runs the reference's own
+ *                 lexicographic SOR (solver.c:126-177) bit for bit instead
+ *                 (single rank: misor_solve_lex)
  *   writeResult : "%f " for every cell incl. ghosts, '\n' per row, solver.c:301-323
  * Decomposed runs (host/ranks.h): every rank owns a block of the 2D
  * decomposition; getResult assembles p on rank 0 (the collectResult of
@@ -17,6 +19,7 @@
 
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "ranks.h"
 #include "util.h"
@@ -74,7 +77,23 @@ static void run(Solver* solver, int variant)
 
 void solveRB(Solver* solver) { run(solver, MISOR_SOLVE_RB); }
 
-void solve(Solver* solver) { run(solver, MISOR_SOLVE_RB); }
+int useLexicographic(void)
+{
+    const char* s = getenv("MISOR_SOLVER");
+    return s && strcmp(s, "lex") == 0;
+}
+
+void solve(Solver* solver)
+{
+    if (!useLexicographic()) {
+        run(solver, MISOR_SOLVE_RB);
+        return;
+    }
+    int it = 0;
+    double res = 0.0;
+    misorCheck(misor_solve_lex(solver->dev, MISOR_LEX_A4, &it, &res), "misor_solve_lex");
+    if (solver->rank == 0) printf("%d ", it);
+}
 
 void solveRBA(Solver* solver)
 {

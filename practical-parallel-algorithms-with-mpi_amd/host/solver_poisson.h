@@ -27,4 +27,6 @@ extern void writeResult(Solver*, char*);
 extern void solve(Solver*);
 extern void solveRB(Solver*);
 extern void solveRBA(Solver*);
+/* MISOR_SOLVER=lex: solve() is the reference's lexicographic SOR (added) */
+extern int useLexicographic(void);
 #endif

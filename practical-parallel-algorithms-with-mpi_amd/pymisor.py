@@ -22,6 +22,7 @@ P, RHS, U, V, F, G = range(6)
 NOSLIP, SLIP, OUTFLOW, PERIODIC = 1, 2, 3, 4
 PROBLEM_NONE, PROBLEM_DCAVITY, PROBLEM_CANAL = 0, 1, 2
 SOLVE_RB, SOLVE_RBA = 0, 1
+LEX_A4, LEX_SEQ = 0, 1
 (TUNE_SWEEP_VARIANT, TUNE_ROWS_PER_BLOCK, TUNE_XCD_REMAP, TUNE_SMALL_SOLVE, TUNE_OVERLAP,
  TUNE_TSTEPS, TUNE_TB_VARIANT, TUNE_TB_ROWS) = 1, 2, 3, 4, 5, 6, 7, 8
 COMM_ID_BYTES = 128
@@ -75,6 +76,7 @@ SIGNATURES = {
     "misor_poisson_init": (C.c_int, [C.c_void_p, C.c_double, C.c_double, C.c_int]),
     "misor_solve_rb": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), _dp]),
     "misor_solve_rb_n": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_int), _dp]),
+    "misor_solve_lex": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_int), _dp]),
     "misor_ns_setup": (C.c_int, [C.c_void_p, C.POINTER(NsDesc)]),
     "misor_compute_timestep": (C.c_int, [C.c_void_p, C.c_double, C.c_double, _dp]),
     "misor_set_dt": (C.c_int, [C.c_void_p, C.c_double]),
@@ -207,6 +209,13 @@ class Grid:
             _check(lib().misor_solve_rb(self.h, C.byref(it), C.byref(res)))
         else:
             _check(lib().misor_solve_rb_n(self.h, itermax, C.byref(it), C.byref(res)))
+        return it.value, res.value
+
+    def solve_lex(self, xorder=0):
+        """lexicographic SOR (the reference's `solve`); xorder 0 = assignment-4,
+        1 = assignment-5 sequential"""
+        it, res = C.c_int(0), C.c_double(0.0)
+        _check(lib().misor_solve_lex(self.h, xorder, C.byref(it), C.byref(res)))
         return it.value, res.value
 
     def synchronize(self):

@@ -16,8 +16,11 @@ Fixtures:
   ns_dcavity_rb_short.npz  composed RB-NS, a6 dcavity.par, te=0.5
   ns_canal_rb_short.npz    composed RB-NS, a6 canal.par, te=2
   ns_dcavity_rb_full.npz   composed RB-NS, a6 dcavity.par, te=10 (per-step iters + fields)
+  ns_seq_dcavity_lex_short.npz  the reference's own NS (assignment-5/sequential, its
+                           lexicographic `solve`) on its dcavity.par, te=0.05
 plus reference data files copied verbatim (they are the reference's own
-fixtures): a4_p.dat, a4_init.dat.
+fixtures): a4_p.dat, a4_init.dat, and assignment-5/sequential's dcavity.par,
+pressure.dat and velocity.dat (seq_*; the committed output of its te=10 run).
 """
 import json
 import os
@@ -34,8 +37,23 @@ REF = "/root/reference"
 A6 = os.path.join(REF, "assignment-6")
 
 
+SEQ = os.path.join(REF, "assignment-5/sequential")
+
+
+def lex_fixtures():
+    """the reference's lexicographic NS (its actual `solve`)"""
+    for name in ("dcavity.par", "pressure.dat", "velocity.dat"):
+        shutil.copyfile(os.path.join(SEQ, name), os.path.join(HERE, "seq_" + name))
+    te = 0.05
+    n, iters, p, u, v, t = orc.ref_ns(os.path.join(SEQ, "dcavity.par"), te=te, solver=0)
+    np.savez_compressed(os.path.join(HERE, "ns_seq_dcavity_lex_short.npz"), steps=n,
+                        p=p, u=u, v=v, t=t, te=te)
+    print("ns_seq_dcavity_lex_short.npz", n, "steps")
+
+
 def main(full=True):
     assert orc.have_ref(), "build oracle/_ref first: make -C oracle ref"
+    lex_fixtures()
 
     # reference data fixtures
     shutil.copyfile(os.path.join(REF, "assignment-4/p.dat"), os.path.join(HERE, "a4_p.dat"))
@@ -87,4 +105,7 @@ def main(full=True):
 
 
 if __name__ == "__main__":
-    main(full="--short" not in sys.argv)
+    if "--lex-only" in sys.argv:
+        lex_fixtures()
+    else:
+        main(full="--short" not in sys.argv)

@@ -28,8 +28,10 @@ def dt_bound(prm):
     return 0.5 * prm["re"] * 1.0 / inv
 
 
-def run(g, prm, max_steps=-1):
-    """returns (steps, per-step iterations, t)"""
+def run(g, prm, max_steps=-1, solver="rb"):
+    """returns (steps, per-step iterations, t); solver "rb" = solveRB (the
+    production path), "lex" = the reference's lexicographic `solve`
+    (assignment-5/sequential/src/solver.c:140-191)"""
     tau, te = prm["tau"], prm["te"]
     dtb = dt_bound(prm)
     dt = prm["dt"]
@@ -43,7 +45,7 @@ def run(g, prm, max_steps=-1):
         g.call("compute_rhs")
         if nt % 100 == 0:
             g.call("normalize_pressure")
-        it, _ = g.solve_rb()
+        it, _ = g.solve_rb() if solver == "rb" else g.solve_lex(M.LEX_SEQ)
         iters.append(it)
         g.call("adapt_uv")
         t += dt

@@ -97,3 +97,33 @@ def test_exe_ns_decomposed_matches_single(golden, tmp_path, par, ranks):
         ta, tb = (a / f).read_text(), (b / f).read_text()
         if ta != tb:  # at most one unit in the last printed digit ("%f")
             assert np.abs(np.loadtxt(a / f) - np.loadtxt(b / f)).max() <= 1.01e-6, f
+
+
+def test_exe_poisson_lexicographic_reproduces_committed_pdat(golden, tmp_path):
+    """MISOR_SOLVER=lex: the reference's own solve (assignment-4/src/main.c:34
+    calls the lexicographic SOR) -> its committed p.dat, byte for byte"""
+    shutil.copy(os.path.join(golden, "a4_poisson.par"), tmp_path / "poisson.par")
+    env = dict(os.environ, MISOR_SOLVER="lex")
+    out = subprocess.run([os.path.join(BIN, "exe-poisson"), "poisson.par"], cwd=tmp_path,
+                         env=env, capture_output=True, text=True, timeout=120, check=True).stdout
+    assert re.search(r"(^|\s)2388 ", out), out
+    assert (tmp_path / "p.dat").read_text() == open(os.path.join(golden, "a4_p.dat")).read()
+
+
+def test_exe_ns_lexicographic_short(golden, tmp_path):
+    """MISOR_SOLVER=lex: the reference's sequential NS on its dcavity.par
+    (400 steps) -> pressure.dat / velocity.dat of the reference build's fields"""
+    z = np.load(os.path.join(golden, "ns_seq_dcavity_lex_short.npz"))
+    txt = open(os.path.join(golden, "seq_dcavity.par")).read()
+    txt = re.sub(r"(?m)^te .*$", "te       %r" % float(z["te"]), txt)
+    (tmp_path / "dcavity.par").write_text(txt)
+    env = dict(os.environ, MISOR_SOLVER="lex", MISOR_ITERLOG=str(tmp_path / "iters.log"))
+    subprocess.run([os.path.join(BIN, "exe-ns"), "dcavity.par"], cwd=tmp_path, env=env,
+                   capture_output=True, text=True, timeout=300, check=True)
+    assert len(np.loadtxt(tmp_path / "iters.log")) == int(z["steps"])
+    pr = np.loadtxt(tmp_path / "pressure.dat")
+    assert np.abs(pr[:, 2] - z["p"][1:-1, 1:-1].ravel()).max() <= 1e-6
+    ve = np.loadtxt(tmp_path / "velocity.dat")
+    u, v = z["u"], z["v"]
+    assert np.abs(ve[:, 2] - ((u[1:-1, 1:-1] + u[1:-1, :-2]) / 2.0).ravel()).max() <= 1e-6
+    assert np.abs(ve[:, 3] - ((v[1:-1, 1:-1] + v[:-2, 1:-1]) / 2.0).ravel()).max() <= 1e-6

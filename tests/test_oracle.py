@@ -152,3 +152,16 @@ def test_ns_step_functions_vs_reference_bc_variants(golden, tmp_path):
         ns.run(solver=1, max_steps=6)
         for fld, ref in (("p", p), ("u", u), ("v", v)):
             assert np.array_equal(getattr(ns, fld), ref), (combo, fld)
+
+
+def test_lex_ns_oracle_vs_reference_fixture(golden):
+    """the oracle's lexicographic NS against the reference build's own run
+    (assignment-5/sequential with its shipped solve, te=0.05): bit-exact"""
+    z = np.load(os.path.join(golden, "ns_seq_dcavity_lex_short.npz"))
+    prm = orc.read_par(os.path.join(golden, "seq_dcavity.par"))
+    prm["te"] = float(z["te"])
+    ns = orc.NS(prm)
+    steps, iters, t = ns.run(solver=0)
+    assert steps == int(z["steps"])
+    for k in ("p", "u", "v"):
+        assert np.array_equal(getattr(ns, k), z[k]), k

@@ -101,6 +101,105 @@ def pmc_traffic(size, nranks, T):
     return best
 
 
+# assignment-6/dcavity.par read as 2D, sizes set per GPU
+DCAVITY = dict(name="dcavity", xlength=1.0, ylength=1.0, re=1000.0, gx=0.0, gy=0.0,
+               u_init=0.0, v_init=0.0, p_init=0.0, dt=0.02, tau=0.5, eps=1e-3, omg=1.8,
+               gamma=0.9, bcLeft=1, bcRight=1, bcBottom=1, bcTop=1)
+
+
+def run_ns(args, world, rank, local_rank, dist, torch):
+    """BASELINE config 5: dcavity NS weak scaling, size^2 cells per GPU, the
+    pressure solve capped at --itermax iterations, fixed time steps.  A step is
+    one time step of assignment-5/sequential/src/main.c:43-60 (dt all-reduce,
+    BCs, computeFG, computeRHS, normalizePressure every 100 steps, solve,
+    adaptUV) over the whole global grid."""
+    import pymisor as M
+
+    dims = list(M.decompose(world, 0, 1 << 20, 1 << 20).dims)
+    imax, jmax = args.size * dims[0], args.size * dims[1]
+    prm = dict(DCAVITY, imax=imax, jmax=jmax, itermax=args.itermax)
+    dx, dy = prm["xlength"] / imax, prm["ylength"] / jmax
+    comm_id = None
+    if world > 1:
+        obj = [M.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        comm_id = obj[0]
+    g = M.Grid(imax, jmax, dx, dy, prm["omg"], prm["eps"], prm["itermax"], device=local_rank,
+               nranks=world, rank=rank, comm_id=comm_id)
+    if args.tsteps > 0:
+        g.set_tuning(M.TUNE_TSTEPS, args.tsteps)
+    g.ns_setup(prm)
+    for f, v in ((M.U, prm["u_init"]), (M.V, prm["v_init"]), (M.P, prm["p_init"])):
+        g.fill(f, v)
+    g.set_dt(prm["dt"])
+    inv = 1.0 / (dx * dx) + 1.0 / (dy * dy)
+    dt_bound = 0.5 * prm["re"] * 1.0 / inv  # solver.c:113-116
+    state = {"nt": 0, "iters": 0}
+
+    def step():
+        g.compute_timestep(dt_bound, prm["tau"])
+        g.call("set_boundary_conditions")
+        g.call("set_special_boundary_condition")
+        g.call("compute_fg")
+        g.call("compute_rhs")
+        if state["nt"] % 100 == 0:
+            g.call("normalize_pressure")
+        it, _ = g.solve_rb()
+        g.call("adapt_uv")
+        state["nt"] += 1
+        return it
+
+    def barrier():
+        torch.cuda.synchronize()
+        g.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    g.enable_timing(True)
+    g.reset_stats()
+    barrier()
+    t0 = time.perf_counter()
+    iters = 0
+    for _ in range(args.steps):
+        iters += step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    st = g.stats()
+    solve_ms = st["sweep_ms"]
+    if dist is not None:
+        tt = torch.tensor([elapsed, solve_ms], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed, solve_ms = tt.tolist()
+    cells = float(imax) * float(jmax)
+    out = {
+        "metric": "dcavity NS weak scaling: pressure-solve MLUP/s within full time steps",
+        "value": round(cells * iters / elapsed / 1e6, 1),
+        "unit": "MLUP/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (dcavity initial state u = v = p = 0, generated on device)",
+        "config": {"workload": "2D NS lid-driven cavity (assignment-6 dcavity.par as 2D), "
+                               "%dx%d global = %d^2 per GPU, pressure solve capped at %d "
+                               "iterations, 1 time step = 1 step" % (imax, jmax, args.size,
+                                                                       args.itermax),
+                   "imax": imax, "jmax": jmax, "decomposition": "%dx%d" % tuple(dims),
+                   "baseline_config": 5},
+        "pressure_iterations": iters,
+        "solve_kernel_ms_per_step": round(solve_ms / args.steps, 3),
+        "other_ms_per_step": round(elapsed / args.steps * 1e3 - solve_ms / args.steps, 3),
+    }
+    g.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -110,6 +209,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--tsteps", type=int, default=0,
                     help="iterations per kernel launch (0: library default)")
+    ap.add_argument("--workload", choices=("poisson", "ns"), default="poisson",
+                    help="poisson: the headline metric (config 4); ns: config 5, "
+                         "dcavity NS weak scaling (--size cells^2 per GPU)")
+    ap.add_argument("--itermax", type=int, default=100, help="ns: pressure-solve cap")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -126,6 +229,17 @@ def main():
 
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    if args.workload == "ns":
+        if args.size == 32768 and "--size" not in sys.argv:
+            args.size = 16384
+        out = run_ns(args, world, rank, local_rank, dist, torch)
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        return
 
     import pymisor as M
 

@@ -900,6 +900,19 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
         if (rc) return rc;
     }
     const long long max_passes = (itermax + T - 1) / T;
+    // iterations pass k performs: T, except that the last pass of the cap does
+    // only what is left of itermax (no pass overshoots the cap)
+    auto t_of = [&](long long k) -> int {
+        return k == max_passes - 1 ? (int)(itermax - k * T) : T;
+    };
+    auto nparts_of = [&](int Tk) -> int {
+        if (T == 1 || Tk == T) return nparts;
+        SweepParams tp = g->tp;
+        tb_geometry(g, Tk, tp);
+        return tp.nblocks;
+    };
+    // iterations covered by the first p passes
+    auto covered = [&](long long p) -> long long { return std::min(p * T, (long long)itermax); };
     int batch = g->last_iters / T > 8 ? g->last_iters / T : 8;
     for (;;) {
         if (batch > max_passes - launched) batch = (int)(max_passes - launched);
@@ -919,14 +932,15 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
             // it), so the interior blocks wait for decide k-1; the exchange still
             // overlaps them.
             const long long k = launched + b;
+            const int Tk = t_of(k);
             const double* src = g->fld[kP0 + ((cur0 + k) & 1)];
             double* dst = g->fld[kP0 + ((cur0 + k + 1) & 1)];
             HIPCHK(hipEventRecord(g->ev_s, g->stream));
             HIPCHK(hipStreamWaitEvent(g->cstream, g->ev_s, 0));
             if (b > 0) {  // pass k-1 of this batch (the previous batch closed its own)
-                int rc = allreduce(g, g->st->sum, T, 0, g->cstream);
+                int rc = allreduce(g, g->st->sum, t_of(k - 1), 0, g->cstream);
                 if (rc) return rc;
-                launch_decide(g->cstream, g->st, T, cells);
+                launch_decide(g->cstream, g->st, t_of(k - 1), cells);
                 if (T > 1) {
                     HIPCHK(hipEventRecord(g->ev_d, g->cstream));
                     HIPCHK(hipStreamWaitEvent(g->stream, g->ev_d, 0));
@@ -936,23 +950,24 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
             if (rc) return rc;
             HIPCHK(hipEventRecord(g->ev_x, g->cstream));
             if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b], g->stream));
-            pass(g->stream, 1, src, dst, T, 0);
+            pass(g->stream, 1, src, dst, Tk, 0);
             HIPCHK(hipStreamWaitEvent(g->stream, g->ev_x, 0));
-            pass(g->stream, 2, src, dst, T, 0);
+            pass(g->stream, 2, src, dst, Tk, 0);
             if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b + 1], g->stream));
-            launch_finish(g->stream, g->partials, nparts, T, g->st, cells, 0);
+            launch_finish(g->stream, g->partials, nparts_of(Tk), Tk, g->st, cells, 0);
             if (b == batch - 1) {  // close the batch: all-reduce + decide of the last one
                 HIPCHK(hipEventRecord(g->ev_s, g->stream));
                 HIPCHK(hipStreamWaitEvent(g->cstream, g->ev_s, 0));
-                rc = allreduce(g, g->st->sum, T, 0, g->cstream);
+                rc = allreduce(g, g->st->sum, Tk, 0, g->cstream);
                 if (rc) return rc;
-                launch_decide(g->cstream, g->st, T, cells);
+                launch_decide(g->cstream, g->st, Tk, cells);
                 HIPCHK(hipEventRecord(g->ev_x, g->cstream));
                 HIPCHK(hipStreamWaitEvent(g->stream, g->ev_x, 0));
             }
         }
         for (int b = 0; b < batch && !(g->dist && g->overlap); ++b) {
             const long long k = launched + b;
+            const int Tk = t_of(k);
             const double* src = g->fld[kP0 + ((cur0 + k) & 1)];
             double* dst = g->fld[kP0 + ((cur0 + k + 1) & 1)];
             if (g->dist) {  // 2T-deep halo of src: one exchange per pass
@@ -960,15 +975,15 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
                 if (rc) return rc;
             }
             if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b], g->stream));
-            pass(g->stream, 0, src, dst, T, 0);
+            pass(g->stream, 0, src, dst, Tk, 0);
             if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b + 1], g->stream));
             if (g->dist) {
-                launch_finish(g->stream, g->partials, nparts, T, g->st, cells, 0);
-                int rc = allreduce(g, g->st->sum, T, 0);
+                launch_finish(g->stream, g->partials, nparts_of(Tk), Tk, g->st, cells, 0);
+                int rc = allreduce(g, g->st->sum, Tk, 0);
                 if (rc) return rc;
-                launch_decide(g->stream, g->st, T, cells);
+                launch_decide(g->stream, g->st, Tk, cells);
             } else {
-                launch_finish(g->stream, g->partials, nparts, T, g->st, cells, 1);
+                launch_finish(g->stream, g->partials, nparts_of(Tk), Tk, g->st, cells, 1);
             }
         }
         HIPCHK(hipGetLastError());
@@ -980,13 +995,14 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
         if (g->timing) {
             // passes after convergence exit at once; count only the real ones
             const long long real_before = launched - batch;
-            const long long real_end = (g->st_host->it + T - 1) / T;
+            const long long real_end =
+                std::min((long long)(g->st_host->it + T - 1) / T, max_passes);
             for (int b = 0; b < batch; ++b) {
                 if (real_before + b >= real_end) break;
                 float ms = 0.f;
                 HIPCHK(hipEventElapsedTime(&ms, g->ev[2 * b], g->ev[2 * b + 1]));
                 g->stats.sweep_ms += ms;
-                g->stats.timed_sweeps += T;
+                g->stats.timed_sweeps += t_of(real_before + b);
                 g->stats.timed_passes++;
             }
         }
@@ -995,14 +1011,14 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
         batch = batch < 512 ? 2 * batch : 1024;
     }
     const int it = g->st_host->it;
-    const long long passes = (it + T - 1) / T;
-    const int over = (int)(passes * T - it);
+    const long long passes = std::min((long long)(it + T - 1) / T, max_passes);
+    const int over = (int)(covered(passes) - it);
     g->cur = (int)((cur0 + passes) & 1);
     if (over > 0) {
         // the last pass ran past the iteration that ended the loop: redo it
         // with T - over iterations from its source (untouched since)
         const double* src = g->fld[kP0 + ((cur0 + passes - 1) & 1)];
-        pass(g->stream, 0, src, g->fld[g->cur], T - over, 1);
+        pass(g->stream, 0, src, g->fld[g->cur], t_of(passes - 1) - over, 1);
         HIPCHK(hipGetLastError());
     }
     if (g->dist) {  // leave the halo of the final field consistent (adaptUV reads it)

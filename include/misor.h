@@ -206,6 +206,55 @@ int misor_enable_timing(misor_grid* g, int on);
 int misor_get_stats(const misor_grid* g, misor_stats* out);
 int misor_reset_stats(misor_grid* g);
 
+/* ------------------------------------------------------------------ 3D ---
+ * assignment-6's 3D Navier-Stokes solver (assignment-6/src/solver.c) on one
+ * GPU: the same step as solver.h's computeTimestep / setBoundaryConditions /
+ * setSpecialBoundaryCondition / computeFG / computeRHS / solve / adaptUV, with
+ * a 7-point red-black pressure solve.  Fields keep the reference layout:
+ * (imax+2)(jmax+2)(kmax+2) doubles, i fastest, then j, then k (solver.c:19-34).
+ * Every cell value is bit-identical to the reference's; the solve's residual
+ * is summed in a fixed tree order (the reference sums sequentially). */
+typedef struct misor_grid3 misor_grid3;
+
+typedef struct {
+    int imax, jmax, kmax;               /* interior cells */
+    double xlength, ylength, zlength;   /* domain size */
+    double re, gamma, tau, omega, eps;  /* Reynolds number, upwind factor, CFL
+                                         * safety, SOR relaxation, tolerance */
+    double gx, gy, gz;                  /* body force */
+    int itermax;                        /* solve iteration cap */
+    int bcTop, bcBottom, bcLeft, bcRight, bcFront, bcBack; /* MISOR_NOSLIP ... */
+    int problem;                        /* MISOR_PROBLEM_* */
+    int device;                         /* HIP device; < 0: the current one */
+} misor3_desc;
+
+/* field ids of misor3_upload / misor3_download / misor3_fill */
+enum { MISOR3_P = 0, MISOR3_RHS = 1, MISOR3_U = 2, MISOR3_V = 3, MISOR3_W = 4,
+       MISOR3_F = 5, MISOR3_G = 6, MISOR3_H = 7 };
+
+/* initSolver (solver.c:60-143): device fields, all zero; dx = xlength/imax ... */
+int misor3_create(misor_grid3** out, const misor3_desc* d);
+void misor3_destroy(misor_grid3* g);
+/* whole field incl. ghosts, (imax+2)(jmax+2)(kmax+2) doubles */
+int misor3_upload(misor_grid3* g, int field, const double* host);
+int misor3_download(misor_grid3* g, int field, double* host);
+int misor3_fill(misor_grid3* g, int field, double value);
+int misor3_set_dt(misor_grid3* g, double dt);
+/* computeTimestep (solver.c:340-362): dt = tau * min(dtBound, dx/umax, dy/vmax,
+ * dz/wmax), dtBound = 0.5*re/(1/dx^2+1/dy^2+1/dz^2) (solver.c:136-139) */
+int misor3_compute_timestep(misor_grid3* g, double* dt_out);
+/* max |u|, |v|, |w| over every cell incl. ghosts (maxElement, solver.c:299-310) */
+int misor3_max_uvw(misor_grid3* g, double* mx3);
+int misor3_set_boundary_conditions(misor_grid3* g);       /* solver.c:364-577 */
+int misor3_set_special_boundary_condition(misor_grid3* g); /* solver.c:579-604 */
+int misor3_compute_fg(misor_grid3* g);                    /* solver.c:606-824 */
+int misor3_compute_rhs(misor_grid3* g);                   /* solver.c:145-173 */
+/* solve (solver.c:175-297): red-black SOR until res < eps^2 or itermax */
+int misor3_solve(misor_grid3* g, int* iters, double* res);
+int misor3_adapt_uvw(misor_grid3* g);                     /* solver.c:826-853 */
+int misor3_normalize_pressure(misor_grid3* g);            /* solver.c:312-338 */
+int misor3_synchronize(misor_grid3* g);
+
 #ifdef __cplusplus
 }
 #endif

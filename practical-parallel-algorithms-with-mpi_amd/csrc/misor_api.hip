@@ -96,6 +96,8 @@ constexpr char kLocalPrefix[] = "LOCAL:";
 
 }  // namespace
 
+void misor::set_last_error(const char* msg) { g_err = msg; }
+
 struct misor_grid {
     int device = 0;
     hipStream_t stream = nullptr;

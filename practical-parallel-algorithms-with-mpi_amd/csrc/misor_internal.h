@@ -146,6 +146,8 @@ void launch_unpack(hipStream_t s, double* field, long long pitch, const HaloPlan
 int sweep_partials(int ni, int nj, int rows_per_block, int waves, int* nbx, int* nby);
 
 void launch_fill(hipStream_t s, double* a, long long count, double v);
+// the message misor_last_error() returns (thread-local, shared by the 2D and 3D ABI)
+void set_last_error(const char* msg);
 void launch_poisson_init(hipStream_t s, double* p, double* rhs, const double* sx,
                          const double* sy, const double* rx, int ni, int nj,
                          long long pitch, int problem);
@@ -176,5 +178,40 @@ void launch_finish_reduce(hipStream_t s, const double* partials, int n, int op, 
 // p -= (*sum) / cells over the whole local array (normalizePressure)
 void launch_sub_mean(const NsLaunch& L, double* p, const double* sum, double cells);
 enum { kReduceSum = 0, kReduceMax = 1 };
+
+// ---------------------------------------------------------------------------
+// 3D (assignment-6): dense reference layout (imax+2)(jmax+2)(kmax+2), i fastest
+// ---------------------------------------------------------------------------
+struct G3 {
+    int I, J, K;        // interior cells
+    long long sx, sxy;  // strides of j and k: (I+2), (I+2)(J+2)
+    __host__ __device__ long long ix(int i, int j, int k) const {
+        return (long long)k * sxy + (long long)j * sx + i;
+    }
+};
+struct Fg3 {  // computeFG's scalars (solver.c:620-629)
+    double gamma, ix, iy, iz, iRe, dt, gx, gy, gz;
+};
+int ns3_partials(const G3& g);
+void launch3_rhs(hipStream_t s, const G3& g, const double* f, const double* gg, const double* h,
+                 double* rhs, double idx, double idy, double idz, double idt);
+// one solve iteration (both colour passes, ghost copy, finish); returns the
+// number of partials per pass
+int launch3_rb_iteration(hipStream_t s, const G3& g, double* p, const double* rhs, double idx2,
+                         double idy2, double idz2, double factor, double* partials, DevState* st,
+                         double cells);
+void launch3_fg(hipStream_t s, const G3& g, const double* u, const double* v, const double* w,
+                double* f, double* gg, double* h, const Fg3& c);
+void launch3_adapt(hipStream_t s, const G3& g, const double* f, const double* gg,
+                   const double* h, const double* p, double* u, double* v, double* w, double fx,
+                   double fy, double fz);
+void launch3_wall(hipStream_t s, const G3& g, double* n, double* t1, double* t2, int axis,
+                  int gh, int in, int on, int onin, int bc);
+void launch3_special(hipStream_t s, const G3& g, double* u, int problem);
+int absmax3_blocks();
+void launch3_absmax(hipStream_t s, const double* u, const double* v, const double* w,
+                    long long n, double* partials, double* out);
+void launch3_normalize(hipStream_t s, const G3& g, double* p, double* partials, double* sum,
+                       double cells);
 
 }  // namespace misor

@@ -26,6 +26,8 @@ LEX_A4, LEX_SEQ = 0, 1
 (TUNE_SWEEP_VARIANT, TUNE_ROWS_PER_BLOCK, TUNE_XCD_REMAP, TUNE_SMALL_SOLVE, TUNE_OVERLAP,
  TUNE_TSTEPS, TUNE_TB_VARIANT, TUNE_TB_ROWS) = 1, 2, 3, 4, 5, 6, 7, 8
 COMM_ID_BYTES = 128
+# 3D field ids (misor3_*)
+P3, RHS3, U3, V3, W3, F3, G3, H3 = range(8)
 
 _dp = C.POINTER(C.c_double)
 
@@ -54,6 +56,18 @@ class Stats(C.Structure):
     _fields_ = [("sweeps", C.c_longlong), ("launches", C.c_longlong), ("sweep_ms", C.c_double),
                 ("timed_sweeps", C.c_longlong), ("timed_passes", C.c_longlong),
                 ("iters_per_pass", C.c_int), ("pad_", C.c_int)]
+
+
+class Desc3(C.Structure):
+    _fields_ = [("imax", C.c_int), ("jmax", C.c_int), ("kmax", C.c_int),
+                ("xlength", C.c_double), ("ylength", C.c_double), ("zlength", C.c_double),
+                ("re", C.c_double), ("gamma", C.c_double), ("tau", C.c_double),
+                ("omega", C.c_double), ("eps", C.c_double),
+                ("gx", C.c_double), ("gy", C.c_double), ("gz", C.c_double),
+                ("itermax", C.c_int),
+                ("bcTop", C.c_int), ("bcBottom", C.c_int), ("bcLeft", C.c_int),
+                ("bcRight", C.c_int), ("bcFront", C.c_int), ("bcBack", C.c_int),
+                ("problem", C.c_int), ("device", C.c_int)]
 
 
 # every exported symbol of include/misor.h, with its ctypes signature
@@ -92,6 +106,22 @@ SIGNATURES = {
     "misor_enable_timing": (C.c_int, [C.c_void_p, C.c_int]),
     "misor_get_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
     "misor_reset_stats": (C.c_int, [C.c_void_p]),
+    "misor3_create": (C.c_int, [C.POINTER(C.c_void_p), C.POINTER(Desc3)]),
+    "misor3_destroy": (None, [C.c_void_p]),
+    "misor3_upload": (C.c_int, [C.c_void_p, C.c_int, _dp]),
+    "misor3_download": (C.c_int, [C.c_void_p, C.c_int, _dp]),
+    "misor3_fill": (C.c_int, [C.c_void_p, C.c_int, C.c_double]),
+    "misor3_set_dt": (C.c_int, [C.c_void_p, C.c_double]),
+    "misor3_compute_timestep": (C.c_int, [C.c_void_p, _dp]),
+    "misor3_max_uvw": (C.c_int, [C.c_void_p, _dp]),
+    "misor3_set_boundary_conditions": (C.c_int, [C.c_void_p]),
+    "misor3_set_special_boundary_condition": (C.c_int, [C.c_void_p]),
+    "misor3_compute_fg": (C.c_int, [C.c_void_p]),
+    "misor3_compute_rhs": (C.c_int, [C.c_void_p]),
+    "misor3_solve": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), _dp]),
+    "misor3_adapt_uvw": (C.c_int, [C.c_void_p]),
+    "misor3_normalize_pressure": (C.c_int, [C.c_void_p]),
+    "misor3_synchronize": (C.c_int, [C.c_void_p]),
 }
 
 _lib = None
@@ -274,3 +304,80 @@ class Grid:
 
     def reset_stats(self):
         _check(lib().misor_reset_stats(self.h))
+
+
+_PROBLEMS = {"dcavity": PROBLEM_DCAVITY, "canal": PROBLEM_CANAL}
+
+
+class Grid3:
+    """The 3D solver (assignment-6/src/solver.c) on one GPU: fields of shape
+    (kmax+2, jmax+2, imax+2), A(i,j,k) = a[k, j, i] (solver.c:19-34)."""
+
+    def __init__(self, prm: dict, device=-1):
+        d = Desc3()
+        d.imax, d.jmax, d.kmax = int(prm["imax"]), int(prm["jmax"]), int(prm["kmax"])
+        d.xlength, d.ylength, d.zlength = prm["xlength"], prm["ylength"], prm["zlength"]
+        d.re, d.gamma, d.tau = prm["re"], prm["gamma"], prm["tau"]
+        d.omega, d.eps, d.itermax = prm["omg"], prm["eps"], int(prm["itermax"])
+        d.gx, d.gy, d.gz = prm["gx"], prm["gy"], prm["gz"]
+        for k in ("bcTop", "bcBottom", "bcLeft", "bcRight", "bcFront", "bcBack"):
+            setattr(d, k, int(prm[k]))
+        d.problem = _PROBLEMS.get(prm.get("name") or "", PROBLEM_NONE)
+        d.device = device
+        self.h = C.c_void_p()
+        _check(lib().misor3_create(C.byref(self.h), C.byref(d)))
+        self.desc = d
+        self.shape = (d.kmax + 2, d.jmax + 2, d.imax + 2)
+
+    def close(self):
+        if self.h:
+            lib().misor3_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def upload(self, field, arr):
+        a = np.ascontiguousarray(arr, dtype=np.float64)
+        assert a.shape == self.shape, (a.shape, self.shape)
+        _check(lib().misor3_upload(self.h, field, _ptr(a)))
+
+    def download(self, field):
+        a = np.empty(self.shape)
+        _check(lib().misor3_download(self.h, field, _ptr(a)))
+        return a
+
+    def fill(self, field, value):
+        _check(lib().misor3_fill(self.h, field, value))
+
+    def set_dt(self, dt):
+        _check(lib().misor3_set_dt(self.h, dt))
+
+    def compute_timestep(self):
+        dt = C.c_double(0.0)
+        _check(lib().misor3_compute_timestep(self.h, C.byref(dt)))
+        return dt.value
+
+    def max_uvw(self):
+        m = (C.c_double * 3)()
+        _check(lib().misor3_max_uvw(self.h, C.cast(m, _dp)))
+        return tuple(m)
+
+    def solve(self):
+        it, res = C.c_int(0), C.c_double(0.0)
+        _check(lib().misor3_solve(self.h, C.byref(it), C.byref(res)))
+        return it.value, res.value
+
+    def call(self, name):
+        """set_boundary_conditions, set_special_boundary_condition, compute_fg,
+        compute_rhs, adapt_uvw, normalize_pressure, synchronize"""
+        _check(getattr(lib(), "misor3_" + name)(self.h))

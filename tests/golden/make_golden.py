@@ -16,6 +16,9 @@ Fixtures:
   ns_dcavity_rb_short.npz  composed RB-NS, a6 dcavity.par, te=0.5
   ns_canal_rb_short.npz    composed RB-NS, a6 canal.par, te=2
   ns_dcavity_rb_full.npz   composed RB-NS, a6 dcavity.par, te=10 (per-step iters + fields)
+  ns3d_dcavity_short.npz / ns3d_canal_short.npz  the reference's 3D NS (assignment-6/src,
+                           oracle/_ref/libref3d.so) on its dcavity/canal .par at reduced
+                           grids, 16 time steps: per-step iterations, p, u, v, w, t
   ns_seq_dcavity_lex_short.npz  the reference's own NS (assignment-5/sequential, its
                            lexicographic `solve`) on its dcavity.par, te=0.05
 plus reference data files copied verbatim (they are the reference's own
@@ -51,9 +54,23 @@ def lex_fixtures():
     print("ns_seq_dcavity_lex_short.npz", n, "steps")
 
 
+def ns3d_fixtures():
+    """the reference's 3D NS (assignment-6/src/main.c loop) at reduced grids"""
+    import orc3
+    assert orc3.have_ref3(), "build oracle/_ref first: make -C oracle ref"
+    for par, dims, out in (("dcavity.par", (24, 20, 16), "ns3d_dcavity_short.npz"),
+                           ("canal.par", (40, 12, 10), "ns3d_canal_short.npz")):
+        n, iters, p, u, v, w, t = orc3.ref3_run(os.path.join(A6, par), dims=dims,
+                                                max_steps=16)
+        np.savez_compressed(os.path.join(HERE, out), steps=n, iters=iters, p=p, u=u, v=v,
+                            w=w, t=t, dims=np.array(dims))
+        print(out, n, "steps", int(iters.sum()), "iterations")
+
+
 def main(full=True):
     assert orc.have_ref(), "build oracle/_ref first: make -C oracle ref"
     lex_fixtures()
+    ns3d_fixtures()
 
     # reference data fixtures
     shutil.copyfile(os.path.join(REF, "assignment-4/p.dat"), os.path.join(HERE, "a4_p.dat"))
@@ -107,5 +124,7 @@ def main(full=True):
 if __name__ == "__main__":
     if "--lex-only" in sys.argv:
         lex_fixtures()
+    elif "--3d-only" in sys.argv:
+        ns3d_fixtures()
     else:
         main(full="--short" not in sys.argv)

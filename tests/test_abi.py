@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def declared_symbols():
     txt = open(os.path.join(ROOT, "include", "misor.h")).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(misor_[a-z_0-9]+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(misor3?_[a-z_0-9]+)\s*\(", txt)))
 
 
 def test_library_exports_every_declared_symbol():
@@ -81,3 +81,11 @@ def test_create_rejects_bad_descriptors():
         M.Grid(1, 10, 1.0, 0.1, 1.9, 1e-6, 10)
     with pytest.raises(M.MisorError):
         M.Grid(10, 10, 0.0, 0.1, 1.9, 1e-6, 10)
+
+
+def test_create3_rejects_bad_descriptors():
+    prm = dict(imax=1, jmax=4, kmax=4, xlength=1.0, ylength=1.0, zlength=1.0, re=100.0,
+               gamma=0.9, tau=0.5, omg=1.7, eps=1e-3, itermax=10, gx=0.0, gy=0.0, gz=0.0,
+               bcTop=1, bcBottom=1, bcLeft=1, bcRight=1, bcFront=1, bcBack=1, name="dcavity")
+    with pytest.raises(M.MisorError):
+        M.Grid3(prm)

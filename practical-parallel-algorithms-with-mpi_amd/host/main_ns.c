@@ -15,33 +15,10 @@
 #include <string.h>
 
 #include "parameter.h"
+#include "progress.h"
 #include "ranks.h"
 #include "solver_ns.h"
 #include "util.h"
-
-static double progEnd;
-static int progCur;
-
-static void initProgress(double end)
-{
-    progEnd = end;
-    progCur = 0;
-    printf("[          ]");
-    fflush(stdout);
-}
-
-static void printProgress(double current)
-{
-    int now = (int)rint((current / progEnd) * 10.0);
-    if (now > progCur) {
-        char bar[11];
-        progCur = now;
-        for (int i = 0; i < 10; i++) bar[i] = (i < progCur) ? '#' : ' ';
-        bar[10] = '\0';
-        printf("\r[%s]", bar);
-    }
-    fflush(stdout);
-}
 
 static int rank_main(const RankCtx* rk, void* arg)
 {

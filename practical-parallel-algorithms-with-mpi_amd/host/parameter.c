@@ -139,3 +139,28 @@ void printParameter(Parameter* param)
     printf("\tgamma (stopping tolerance) : %f\n", param->gamma);
     printf("\tomega (SOR relaxation): %f\n", param->omg);
 }
+
+/* assignment-6/src/parameter.c:95-126 */
+void printParameter3D(Parameter* param)
+{
+    printf("Parameters for %s\n", param->name ? param->name : "(null)");
+    printf("Boundary conditions Left:%d Right:%d Bottom:%d Top:%d Front:%d "
+           "Back:%d\n",
+           param->bcLeft, param->bcRight, param->bcBottom, param->bcTop, param->bcFront,
+           param->bcBack);
+    printf("\tReynolds number: %.2f\n", param->re);
+    printf("\tInit arrays: U:%.2f V:%.2f W:%.2f P:%.2f\n", param->u_init, param->v_init,
+           param->w_init, param->p_init);
+    printf("Geometry data:\n");
+    printf("\tDomain box size (x, y, z): %.2f, %.2f, %.2f\n", param->xlength, param->ylength,
+           param->zlength);
+    printf("\tCells (x, y, z): %d, %d, %d\n", param->imax, param->jmax, param->kmax);
+    printf("Timestep parameters:\n");
+    printf("\tDefault stepsize: %.2f, Final time %.2f\n", param->dt, param->te);
+    printf("\tTau factor: %.2f\n", param->tau);
+    printf("Iterative solver parameters:\n");
+    printf("\tMax iterations: %d\n", param->itermax);
+    printf("\tepsilon (stopping tolerance) : %f\n", param->eps);
+    printf("\tgamma (stopping tolerance) : %f\n", param->gamma);
+    printf("\tomega (SOR relaxation): %f\n", param->omg);
+}

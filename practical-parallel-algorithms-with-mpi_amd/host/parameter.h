@@ -29,5 +29,7 @@ void initParameter(Parameter*);
 void readParameter(Parameter*, const char* filename);
 void printParameterPoisson(Parameter*);
 void printParameter(Parameter*);
+/* assignment-6/src/parameter.c:95-126 (the 3D solver) */
+void printParameter3D(Parameter*);
 
 #endif

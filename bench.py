@@ -200,6 +200,128 @@ def run_ns(args, world, rank, local_rank, dist, torch):
     return out
 
 
+# assignment-6/dcavity.par (the 3D solver's own configuration)
+DCAVITY3D = dict(name="dcavity", xlength=1.0, ylength=1.0, zlength=1.0, re=1000.0, gx=0.0,
+                 gy=0.0, gz=0.0, u_init=0.0, v_init=0.0, w_init=0.0, p_init=0.0, dt=0.02,
+                 te=10.0, tau=0.5, itermax=1000, eps=1e-3, omg=1.8, gamma=0.9, bcLeft=1,
+                 bcRight=1, bcBottom=1, bcTop=1, bcFront=1, bcBack=1)
+
+
+def cpu_baseline3d(n, iters=100):
+    """the reference's own 3D solve (assignment-6/src/solver.c:175-297 compiled
+    in place, oracle/_ref/libref3d.so) on one host core, n^3 cells x `iters`
+    iterations from a random state; None where the build is absent"""
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import numpy as np
+        import orc3
+        if not orc3.have_ref3():
+            return None
+    except Exception as e:  # pragma: no cover
+        log("cpu_baseline3d unavailable: %s" % e)
+        return None
+    import tempfile
+    rng = np.random.default_rng(0)
+    shape = (n + 2, n + 2, n + 2)
+    st = {f: rng.standard_normal(shape) * 1e-3 for f in orc3.FIELDS}
+    with tempfile.NamedTemporaryFile("w", suffix=".par", delete=False) as fh:
+        fh.write("name dcavity\nimax %d\njmax %d\nkmax %d\nitermax %d\neps 1e-300\n"
+                 "omg 1.8\nre 1000\n" % (n, n, n, iters))
+        par = fh.name
+    t0 = time.perf_counter()
+    _, it = orc3.ref3_call(par, (0, 0, 0), "solve", 0.02, st)
+    el = time.perf_counter() - t0
+    os.unlink(par)
+    return {"value": round(float(n) ** 3 * it / el / 1e6, 1), "unit": "MLUP/s", "cores": 1,
+            "kind": "reference",
+            "sample": "assignment-6 solve (oracle/_ref/libref3d.so), %d^3 cells x %d "
+                      "iterations, random state" % (n, it)}
+
+
+def run_ns3d(args, world, rank, local_rank, dist, torch):
+    """assignment-6's 3D NS (dcavity.par, --size^3 cells) on one GPU per rank:
+    the 3D path is not decomposed, so N ranks run N independent replicas
+    (replicas only).  A step is one time step of
+    assignment-6/src/main.c:45-60."""
+    import pymisor as M
+
+    n = args.size
+    prm = dict(DCAVITY3D, imax=n, jmax=n, kmax=n, itermax=args.itermax or 1000)
+    g = M.Grid3(prm, device=local_rank)
+    for f, v in ((M.U3, prm["u_init"]), (M.V3, prm["v_init"]), (M.W3, prm["w_init"]),
+                 (M.P3, prm["p_init"])):
+        g.fill(f, v)
+    g.set_dt(prm["dt"])
+
+    def step():
+        g.compute_timestep()
+        for fn in ("set_boundary_conditions", "set_special_boundary_condition", "compute_fg",
+                   "compute_rhs"):
+            g.call(fn)
+        it, _ = g.solve()
+        g.call("adapt_uvw")
+        return it
+
+    def barrier():
+        torch.cuda.synchronize()
+        g.call("synchronize")
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    g.enable_timing(True)
+    barrier()
+    t0 = time.perf_counter()
+    iters = 0
+    for _ in range(args.steps):
+        iters += step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    solve_ms, solve_iters = g.solve_time()
+    if dist is not None:
+        tt = torch.tensor([elapsed, float(iters)], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = tt.tolist()[0]
+        it_all = torch.tensor([float(iters)], dtype=torch.float64, device="cuda")
+        dist.all_reduce(it_all, op=dist.ReduceOp.SUM)
+        iters_all = it_all.item()
+    else:
+        iters_all = iters
+    cells = float(n) ** 3
+    out = {
+        "metric": "3D dcavity NS (assignment-6): pressure-solve MLUP/s within full time steps",
+        "value": round(cells * iters_all / elapsed / 1e6, 1),
+        "unit": "MLUP/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (dcavity initial state u = v = w = p = 0, generated on device)",
+        "config": {"workload": "3D NS lid-driven cavity (assignment-6 dcavity.par), %d^3 "
+                               "cells per GPU (replicas), 1 time step = 1 step" % n,
+                   "imax": n, "jmax": n, "kmax": n, "itermax": prm["itermax"]},
+        "pressure_iterations": iters,
+    }
+    if solve_ms > 0:
+        # the solve's kernels (two colour passes + loop test per iteration),
+        # HIP events on the library's stream; 24 B/LUP algorithmic (p in, rhs
+        # in, p out), one LUP = one cell updated once
+        ach = 24.0 * cells * solve_iters / (solve_ms / 1e3) / 1e9
+        out["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": 8000.0,
+                           "unit": "GB/s", "frac": round(ach / 8000.0, 4), "traffic": None,
+                           "kernel": "3D solve: k3_rb_pass x2 + k3_finish per iteration",
+                           "solve_ms_per_iteration": round(solve_ms / solve_iters, 5)}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline3d(min(n, 128))
+    g.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -209,10 +331,12 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--tsteps", type=int, default=0,
                     help="iterations per kernel launch (0: library default)")
-    ap.add_argument("--workload", choices=("poisson", "ns"), default="poisson",
+    ap.add_argument("--workload", choices=("poisson", "ns", "ns3d"), default="poisson",
                     help="poisson: the headline metric (config 4); ns: config 5, "
-                         "dcavity NS weak scaling (--size cells^2 per GPU)")
-    ap.add_argument("--itermax", type=int, default=100, help="ns: pressure-solve cap")
+                         "dcavity NS weak scaling (--size cells^2 per GPU); ns3d: "
+                         "assignment-6's 3D dcavity (--size cells^3, default 128)")
+    ap.add_argument("--itermax", type=int, default=0,
+                    help="ns: pressure-solve cap (default 100); ns3d: default 1000 (.par)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -230,10 +354,14 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
-    if args.workload == "ns":
+    if args.workload in ("ns", "ns3d"):
         if args.size == 32768 and "--size" not in sys.argv:
-            args.size = 16384
-        out = run_ns(args, world, rank, local_rank, dist, torch)
+            args.size = 16384 if args.workload == "ns" else 128
+        if args.workload == "ns":
+            args.itermax = args.itermax or 100
+            out = run_ns(args, world, rank, local_rank, dist, torch)
+        else:
+            out = run_ns3d(args, world, rank, local_rank, dist, torch)
         if dist is not None:
             dist.barrier()
             dist.destroy_process_group()

@@ -254,6 +254,11 @@ int misor3_solve(misor_grid3* g, int* iters, double* res);
 int misor3_adapt_uvw(misor_grid3* g);                     /* solver.c:826-853 */
 int misor3_normalize_pressure(misor_grid3* g);            /* solver.c:312-338 */
 int misor3_synchronize(misor_grid3* g);
+/* device time of the solves (HIP events on the grid's stream around each
+ * misor3_solve: its colour-pass and loop-test kernels), accumulated while
+ * timing is on; enabling resets the counters */
+int misor3_enable_timing(misor_grid3* g, int on);
+int misor3_get_solve_time(const misor_grid3* g, double* ms, long long* iters);
 
 #ifdef __cplusplus
 }

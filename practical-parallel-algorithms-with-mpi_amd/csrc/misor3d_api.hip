@@ -50,6 +50,10 @@ struct misor_grid3 {
     DevState* st = nullptr;
     DevState* st_host = nullptr;
     int last_iters = 0;
+    bool timing = false;          // misor3_enable_timing
+    hipEvent_t ev[2] = {};        // around each solve, on the grid's stream
+    double solve_ms = 0;          // accumulated device time of timed solves
+    long long solve_iters = 0;    // iterations of the timed solves
 };
 
 extern "C" {
@@ -65,6 +69,8 @@ void misor3_destroy(misor_grid3* g) {
     (void)hipHostFree(g->out_host);
     (void)hipFree(g->st);
     (void)hipHostFree(g->st_host);
+    for (auto& e : g->ev)
+        if (e) (void)hipEventDestroy(e);
     if (g->stream) (void)hipStreamDestroy(g->stream);
     delete g;
 }
@@ -119,6 +125,7 @@ int misor3_create(misor_grid3** out, const misor3_desc* d) {
         hipMalloc(&g->out, sizeof(double) * 4) != hipSuccess ||
         hipHostMalloc(&g->out_host, sizeof(double) * 4, hipHostMallocDefault) != hipSuccess ||
         hipMalloc(&g->st, sizeof(DevState)) != hipSuccess ||
+
         hipHostMalloc(&g->st_host, sizeof(DevState), hipHostMallocDefault) != hipSuccess)
         CF(MISOR_ENOMEM, "allocation failed");
     if (hipStreamSynchronize(g->stream) != hipSuccess) CF(MISOR_EHIP, "sync failed");
@@ -290,6 +297,7 @@ int misor3_solve(misor_grid3* g, int* iters, double* res) {
         return MISOR_OK;
     }
     *g->st_host = s0;
+    if (g->timing) HIPCHK3(hipEventRecord(g->ev[0], g->stream));
     HIPCHK3(hipMemcpyAsync(g->st, g->st_host, sizeof(DevState), hipMemcpyHostToDevice,
                            g->stream));
     long long launched = 0;
@@ -303,6 +311,7 @@ int misor3_solve(misor_grid3* g, int* iters, double* res) {
                                  cells);
         HIPCHK3(hipGetLastError());
         launched += batch;
+        if (g->timing) HIPCHK3(hipEventRecord(g->ev[1], g->stream));
         HIPCHK3(hipMemcpyAsync(g->st_host, g->st, sizeof(DevState), hipMemcpyDeviceToHost,
                                g->stream));
         HIPCHK3(hipStreamSynchronize(g->stream));
@@ -310,8 +319,32 @@ int misor3_solve(misor_grid3* g, int* iters, double* res) {
         batch = batch < 512 ? 2 * batch : 1024;
     }
     g->last_iters = g->st_host->it;
+    if (g->timing) {
+        float ms = 0.f;
+        HIPCHK3(hipEventElapsedTime(&ms, g->ev[0], g->ev[1]));
+        g->solve_ms += ms;
+        g->solve_iters += g->st_host->it;
+    }
     if (iters) *iters = g->st_host->it;
     if (res) *res = g->st_host->res;
+    return MISOR_OK;
+}
+
+int misor3_enable_timing(misor_grid3* g, int on) {
+    if (!g) return fail3(MISOR_EINVAL, "null grid");
+    HIPCHK3(hipSetDevice(g->device));
+    if (on && !g->ev[0])
+        for (auto& e : g->ev) HIPCHK3(hipEventCreate(&e));
+    g->timing = on != 0;
+    g->solve_ms = 0;
+    g->solve_iters = 0;
+    return MISOR_OK;
+}
+
+int misor3_get_solve_time(const misor_grid3* g, double* ms, long long* iters) {
+    if (!g) return fail3(MISOR_EINVAL, "null grid");
+    if (ms) *ms = g->solve_ms;
+    if (iters) *iters = g->solve_iters;
     return MISOR_OK;
 }
 

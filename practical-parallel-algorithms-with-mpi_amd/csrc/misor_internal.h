@@ -195,8 +195,8 @@ struct Fg3 {  // computeFG's scalars (solver.c:620-629)
 int ns3_partials(const G3& g);
 void launch3_rhs(hipStream_t s, const G3& g, const double* f, const double* gg, const double* h,
                  double* rhs, double idx, double idy, double idz, double idt);
-// one solve iteration (both colour passes, ghost copy, finish); returns the
-// number of partials per pass
+// one solve iteration: two colour-pass launches (the ghost copy fused in) and
+// the loop test; returns the number of partials per pass
 int launch3_rb_iteration(hipStream_t s, const G3& g, double* p, const double* rhs, double idx2,
                          double idy2, double idz2, double factor, double* partials, DevState* st,
                          double cells);

@@ -75,7 +75,14 @@ __global__ __launch_bounds__(256) void k3_rhs(G3 g, const double* __restrict__ f
 }
 
 // one colour pass of solve (solver.c:203-231): pass 0 updates the cells with
-// i+j+k odd, pass 1 the even ones; r^2 of the block into partials[block]
+// i+j+k odd, pass 1 the even ones; r^2 of the block into partials[block].
+//
+// The Neumann ghost copy that ends each iteration (solver.c:237-278: faces
+// only, interior index ranges) is fused into the update: a face ghost is read
+// only by the interior cell next to it, and that cell is updated in exactly
+// one of the two passes and never again in the iteration, so the thread that
+// updates it writes its mirror(s) right away -- the same values the separate
+// copy would write, after the neighbour has read the old ghost.
 __global__ __launch_bounds__(256) void k3_rb_pass(G3 g, double* __restrict__ p,
                                                   const double* __restrict__ rhs, int pass,
                                                   double idx2, double idy2, double idz2,
@@ -94,33 +101,19 @@ __global__ __launch_bounds__(256) void k3_rb_pass(G3 g, double* __restrict__ p,
         const double ty = (p[q + g.sx] - 2.0 * c) + p[q - g.sx];
         const double tz = (p[q + g.sxy] - 2.0 * c) + p[q - g.sxy];
         const double r = rhs[q] - ((tx * idx2 + ty * idy2) + tz * idz2);
-        p[q] = c - (factor * r);
+        const double np = c - (factor * r);
+        p[q] = np;
         acc = r * r;
+        if (i == 1) p[q - 1] = np;
+        if (i == g.I) p[q + 1] = np;
+        if (j == 1) p[q - g.sx] = np;
+        if (j == g.J) p[q + g.sx] = np;
+        if (k == 1) p[q - g.sxy] = np;
+        if (k == g.K) p[q + g.sxy] = np;
     }
     const double s = block_sum256(acc, sh);
     if (threadIdx.x == 0 && threadIdx.y == 0)
         partials[((long long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x] = s;
-}
-
-// the Neumann ghost copy after each iteration (solver.c:237-278): z = 0 the
-// k faces (loop over i, j), z = 1 the j faces (i, k), z = 2 the i faces (j, k)
-__global__ void k3_ghost(G3 g, double* __restrict__ p, const DevState* __restrict__ st) {
-    if (st->done) return;
-    const int a = 1 + blockIdx.x * blockDim.x + threadIdx.x;
-    const int b = 1 + blockIdx.y;
-    if (blockIdx.z == 0) {
-        if (a > g.I || b > g.J) return;
-        p[g.ix(a, b, 0)] = p[g.ix(a, b, 1)];
-        p[g.ix(a, b, g.K + 1)] = p[g.ix(a, b, g.K)];
-    } else if (blockIdx.z == 1) {
-        if (a > g.I || b > g.K) return;
-        p[g.ix(a, 0, b)] = p[g.ix(a, 1, b)];
-        p[g.ix(a, g.J + 1, b)] = p[g.ix(a, g.J, b)];
-    } else {
-        if (a > g.J || b > g.K) return;
-        p[g.ix(0, a, b)] = p[g.ix(1, a, b)];
-        p[g.ix(g.I + 1, a, b)] = p[g.ix(g.I, a, b)];
-    }
 }
 
 // end of one solve iteration: the reference never resets `res` (it is 1.0
@@ -314,12 +307,23 @@ __global__ __launch_bounds__(256) void k3_absmax3(const double* __restrict__ u,
     }
 }
 
-__global__ void k3_max_finish(const double* __restrict__ partials, int nb, double* out) {
-    const int t = threadIdx.x;  // 3 threads
-    if (t >= 3) return;
-    double m = DBL_MIN;
-    for (int q = 0; q < nb; ++q) m = (m > partials[3 * q + t]) ? m : partials[3 * q + t];
-    out[t] = m;
+__global__ __launch_bounds__(256) void k3_max_finish(const double* __restrict__ partials, int nb,
+                                                     double* out) {
+    __shared__ double sh[3][4];
+    const int t = threadIdx.x;
+    double m[3] = {DBL_MIN, DBL_MIN, DBL_MIN};
+    for (int q = t; q < nb; q += 256)
+        for (int c = 0; c < 3; ++c) m[c] = (m[c] > partials[3 * q + c]) ? m[c] : partials[3 * q + c];
+    for (int c = 0; c < 3; ++c) {
+        m[c] = wave_max(m[c]);
+        if ((t & 63) == 0) sh[c][t >> 6] = m[c];
+    }
+    __syncthreads();
+    if (t < 3) {
+        double v = sh[t][0];
+        for (int x = 1; x < 4; ++x) v = (v > sh[t][x]) ? v : sh[t][x];
+        out[t] = v;
+    }
 }
 
 // normalizePressure (solver.c:312-338): interior sum (fixed order), then subtract
@@ -391,10 +395,6 @@ int launch3_rb_iteration(hipStream_t s, const G3& g, double* p, const double* rh
     for (int pass = 0; pass < 2; ++pass)
         hipLaunchKernelGGL(k3_rb_pass, grid, dim3(kBx, kBy), 0, s, g, p, rhs, pass, idx2, idy2,
                            idz2, factor, partials + (long long)pass * nb, st);
-    const int mx = g.I > g.J ? g.I : g.J;
-    const int my = g.J > g.K ? g.J : g.K;
-    hipLaunchKernelGGL(k3_ghost, dim3((unsigned)((mx + 127) / 128), (unsigned)my, 3), dim3(128),
-                       0, s, g, p, st);
     hipLaunchKernelGGL(k3_finish, dim3(1), dim3(1024), 0, s, partials, nb, st, cells);
     return nb;
 }
@@ -435,7 +435,7 @@ void launch3_absmax(hipStream_t s, const double* u, const double* v, const doubl
                     long long n, double* partials, double* out) {
     hipLaunchKernelGGL(k3_absmax3, dim3(absmax3_blocks()), dim3(256), 0, s, u, v, w, n,
                        partials);
-    hipLaunchKernelGGL(k3_max_finish, dim3(1), dim3(64), 0, s, partials, absmax3_blocks(), out);
+    hipLaunchKernelGGL(k3_max_finish, dim3(1), dim3(256), 0, s, partials, absmax3_blocks(), out);
 }
 
 void launch3_normalize(hipStream_t s, const G3& g, double* p, double* partials, double* sum,

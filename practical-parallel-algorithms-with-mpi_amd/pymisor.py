@@ -122,6 +122,8 @@ SIGNATURES = {
     "misor3_adapt_uvw": (C.c_int, [C.c_void_p]),
     "misor3_normalize_pressure": (C.c_int, [C.c_void_p]),
     "misor3_synchronize": (C.c_int, [C.c_void_p]),
+    "misor3_enable_timing": (C.c_int, [C.c_void_p, C.c_int]),
+    "misor3_get_solve_time": (C.c_int, [C.c_void_p, _dp, C.POINTER(C.c_longlong)]),
 }
 
 _lib = None
@@ -376,6 +378,15 @@ class Grid3:
         it, res = C.c_int(0), C.c_double(0.0)
         _check(lib().misor3_solve(self.h, C.byref(it), C.byref(res)))
         return it.value, res.value
+
+    def enable_timing(self, on=True):
+        _check(lib().misor3_enable_timing(self.h, 1 if on else 0))
+
+    def solve_time(self):
+        """(device ms, iterations) of the solves timed since enable_timing"""
+        ms, it = C.c_double(0.0), C.c_longlong(0)
+        _check(lib().misor3_get_solve_time(self.h, C.byref(ms), C.byref(it)))
+        return ms.value, it.value
 
     def call(self, name):
         """set_boundary_conditions, set_special_boundary_condition, compute_fg,

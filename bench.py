@@ -312,9 +312,18 @@ def run_ns3d(args, world, rank, local_rank, dist, torch):
         # HIP events on the library's stream; 24 B/LUP algorithmic (p in, rhs
         # in, p out), one LUP = one cell updated once
         ach = 24.0 * cells * solve_iters / (solve_ms / 1e3) / 1e9
+        traffic = None
+        for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc3d*.json"))):
+            d = json.load(open(path))
+            if d.get("size") == n and "bytes_per_launch" in d:
+                traffic = d["bytes_per_launch"]
+        fused = g.get_tuning(M.TUNE3_SWEEP) == 1
         out["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": 8000.0,
-                           "unit": "GB/s", "frac": round(ach / 8000.0, 4), "traffic": None,
-                           "kernel": "3D solve: k3_rb_pass x2 + k3_finish per iteration",
+                           "unit": "GB/s", "frac": round(ach / 8000.0, 4),
+                           "traffic": traffic if fused else None,
+                           "kernel": ("3D solve: k3_sweep (one fused red+black launch) + "
+                                      "k3_finish per iteration" if fused else
+                                      "3D solve: k3_rb_pass x2 + k3_finish per iteration"),
                            "solve_ms_per_iteration": round(solve_ms / solve_iters, 5)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline3d(min(n, 128))

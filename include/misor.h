@@ -258,6 +258,17 @@ int misor3_synchronize(misor_grid3* g);
  * misor3_solve: its colour-pass and loop-test kernels), accumulated while
  * timing is on; enabling resets the counters */
 int misor3_enable_timing(misor_grid3* g, int on);
+/* launch-geometry knobs of the 3D solve; results are bit-identical for every
+ * setting */
+enum {
+    MISOR3_TUNE_SWEEP = 1,  /* 1 (default): one fused red+black sweep launch per iteration
+                             * (k-march, LDS plane ring, ping-pong p); 0: two colour-pass
+                             * launches, in place */
+    MISOR3_TUNE_ROWS = 2,   /* fused sweep: rows per workgroup tile, 4 / 8 / 12 */
+    MISOR3_TUNE_KCHUNK = 3  /* fused sweep: planes per workgroup (>= 4; 0: automatic) */
+};
+int misor3_set_tuning(misor_grid3* g, int key, int value);
+int misor3_get_tuning(const misor_grid3* g, int key, int* value);
 int misor3_get_solve_time(const misor_grid3* g, double* ms, long long* iters);
 
 #ifdef __cplusplus

@@ -42,6 +42,11 @@ struct misor_grid3 {
     G3 g{};
     long long n = 0;           // cells incl. ghosts
     double* fld[8] = {};       // MISOR3_P .. MISOR3_H
+    double* p_alt = nullptr;   // ping-pong partner of fld[P] for the fused sweep
+    bool alt_stale = true;     // p_alt's edge/corner ghosts may differ from fld[P]'s
+    int sweep = 1;             // MISOR3_TUNE_SWEEP
+    int rows = 8;              // MISOR3_TUNE_ROWS
+    int kchunk = 0;            // MISOR3_TUNE_KCHUNK (0: automatic)
     double dx = 0, dy = 0, dz = 0, dt = 0, dt_bound = 0;
     double* partials = nullptr;  // 2 * ns3_partials (solve), also reductions
     long long partials_cap = 0;
@@ -64,6 +69,7 @@ void misor3_destroy(misor_grid3* g) {
     if (g->stream) (void)hipStreamSynchronize(g->stream);
     for (auto& f : g->fld)
         if (f) (void)hipFree(f);
+    (void)hipFree(g->p_alt);
     (void)hipFree(g->partials);
     (void)hipFree(g->out);
     (void)hipHostFree(g->out_host);
@@ -119,13 +125,16 @@ int misor3_create(misor_grid3** out, const misor3_desc* d) {
         if (hipMemsetAsync(f, 0, sizeof(double) * (size_t)g->n, g->stream) != hipSuccess)
             CF(MISOR_EHIP, "hipMemset failed");
     }
+    if (hipMalloc(&g->p_alt, sizeof(double) * (size_t)g->n) != hipSuccess)
+        CF(MISOR_ENOMEM, "hipMalloc of %lld doubles failed", g->n);
     g->partials_cap = 2LL * ns3_partials(g->g);
     if (g->partials_cap < 3LL * absmax3_blocks()) g->partials_cap = 3LL * absmax3_blocks();
+    // the fused sweep's partials: the smallest rows / kchunk settings
+    if (g->partials_cap < sweep3_blocks(g->g, 4, 4)) g->partials_cap = sweep3_blocks(g->g, 4, 4);
     if (hipMalloc(&g->partials, sizeof(double) * (size_t)g->partials_cap) != hipSuccess ||
         hipMalloc(&g->out, sizeof(double) * 4) != hipSuccess ||
         hipHostMalloc(&g->out_host, sizeof(double) * 4, hipHostMallocDefault) != hipSuccess ||
         hipMalloc(&g->st, sizeof(DevState)) != hipSuccess ||
-
         hipHostMalloc(&g->st_host, sizeof(DevState), hipHostMallocDefault) != hipSuccess)
         CF(MISOR_ENOMEM, "allocation failed");
     if (hipStreamSynchronize(g->stream) != hipSuccess) CF(MISOR_EHIP, "sync failed");
@@ -144,6 +153,7 @@ int misor3_upload(misor_grid3* g, int field, const double* host) {
     HIPCHK3(hipMemcpyAsync(fld3(g, field), host, sizeof(double) * (size_t)g->n,
                            hipMemcpyHostToDevice, g->stream));
     HIPCHK3(hipStreamSynchronize(g->stream));
+    if (field == MISOR3_P) g->alt_stale = true;
     return MISOR_OK;
 }
 
@@ -161,6 +171,7 @@ int misor3_fill(misor_grid3* g, int field, double value) {
     HIPCHK3(hipSetDevice(g->device));
     launch_fill(g->stream, fld3(g, field), g->n, value);
     HIPCHK3(hipGetLastError());
+    if (field == MISOR3_P) g->alt_stale = true;
     return MISOR_OK;
 }
 
@@ -276,9 +287,21 @@ int misor3_normalize_pressure(misor_grid3* g) {
     return MISOR_OK;
 }
 
+static int auto_kchunk(const G3& g, int rows) {
+    // enough workgroups to fill 256 CUs twice over, chunks of at least 8 planes
+    int kc = 64;
+    while (kc > 8 && sweep3_blocks(g, rows, kc) < 2048) kc /= 2;
+    return kc;
+}
+
 // solve, solver.c:175-297: red-black SOR with the reference's residual
 // (carried over between iterations); batches of iterations are enqueued and
-// the device-resident state is read once per batch.
+// the device-resident state is read once per batch.  Default: the fused
+// sweep, one launch per iteration, ping-ponging between fld[P] and p_alt
+// (launches after the loop test fails are no-ops, so the result is in the
+// buffer of parity `it`; the pointers are swapped so fld[P] holds it).  The
+// edge and corner ghosts are never written by a sweep, so p_alt gets a copy
+// of fld[P] whenever P was set from outside.
 int misor3_solve(misor_grid3* g, int* iters, double* res) {
     if (!g) return fail3(MISOR_EINVAL, "null grid");
     HIPCHK3(hipSetDevice(g->device));
@@ -300,15 +323,31 @@ int misor3_solve(misor_grid3* g, int* iters, double* res) {
     if (g->timing) HIPCHK3(hipEventRecord(g->ev[0], g->stream));
     HIPCHK3(hipMemcpyAsync(g->st, g->st_host, sizeof(DevState), hipMemcpyHostToDevice,
                            g->stream));
+    const bool fused = g->sweep != 0;
+    const int kc = g->kchunk > 0 ? g->kchunk : auto_kchunk(g->g, g->rows);
+    if (fused && g->alt_stale) {
+        HIPCHK3(hipMemcpyAsync(g->p_alt, g->fld[MISOR3_P], sizeof(double) * (size_t)g->n,
+                               hipMemcpyDeviceToDevice, g->stream));
+        g->alt_stale = false;
+    }
+    double* buf[2] = {g->fld[MISOR3_P], g->p_alt};
     long long launched = 0;
     int batch = g->last_iters > 8 ? g->last_iters : 8;
     for (;;) {
         if (batch > d.itermax - launched) batch = (int)(d.itermax - launched);
         if (batch < 1) batch = 1;
-        for (int b = 0; b < batch; ++b)
-            launch3_rb_iteration(g->stream, g->g, g->fld[MISOR3_P], g->fld[MISOR3_RHS],
-                                 1.0 / dx2, 1.0 / dy2, 1.0 / dz2, factor, g->partials, g->st,
-                                 cells);
+        for (int b = 0; b < batch; ++b) {
+            if (fused) {
+                const long long m = launched + b;
+                launch3_sweep(g->stream, g->g, buf[m & 1], buf[(m + 1) & 1], g->fld[MISOR3_RHS],
+                              1.0 / dx2, 1.0 / dy2, 1.0 / dz2, factor, g->rows, kc, g->partials,
+                              g->st, cells);
+            } else {
+                launch3_rb_iteration(g->stream, g->g, g->fld[MISOR3_P], g->fld[MISOR3_RHS],
+                                     1.0 / dx2, 1.0 / dy2, 1.0 / dz2, factor, g->partials,
+                                     g->st, cells);
+            }
+        }
         HIPCHK3(hipGetLastError());
         launched += batch;
         if (g->timing) HIPCHK3(hipEventRecord(g->ev[1], g->stream));
@@ -319,6 +358,10 @@ int misor3_solve(misor_grid3* g, int* iters, double* res) {
         batch = batch < 512 ? 2 * batch : 1024;
     }
     g->last_iters = g->st_host->it;
+    if (fused && (g->st_host->it & 1)) {
+        g->fld[MISOR3_P] = buf[1];
+        g->p_alt = buf[0];
+    }
     if (g->timing) {
         float ms = 0.f;
         HIPCHK3(hipEventElapsedTime(&ms, g->ev[0], g->ev[1]));
@@ -328,6 +371,38 @@ int misor3_solve(misor_grid3* g, int* iters, double* res) {
     if (iters) *iters = g->st_host->it;
     if (res) *res = g->st_host->res;
     return MISOR_OK;
+}
+
+int misor3_set_tuning(misor_grid3* g, int key, int value) {
+    if (!g) return fail3(MISOR_EINVAL, "null grid");
+    switch (key) {
+    case MISOR3_TUNE_SWEEP:
+        if (value != 0 && value != 1) return fail3(MISOR_EINVAL, "sweep must be 0 or 1");
+        g->sweep = value;
+        return MISOR_OK;
+    case MISOR3_TUNE_ROWS:
+        if (value != 4 && value != 8 && value != 12)
+            return fail3(MISOR_EINVAL, "rows must be 4, 8 or 12");
+        g->rows = value;
+        return MISOR_OK;
+    case MISOR3_TUNE_KCHUNK:
+        if (value != 0 && value < 4) return fail3(MISOR_EINVAL, "kchunk must be 0 or >= 4");
+        g->kchunk = value;
+        return MISOR_OK;
+    }
+    return fail3(MISOR_EINVAL, "unknown tuning key %d", key);
+}
+
+int misor3_get_tuning(const misor_grid3* g, int key, int* value) {
+    if (!g || !value) return fail3(MISOR_EINVAL, "null argument");
+    switch (key) {
+    case MISOR3_TUNE_SWEEP: *value = g->sweep; return MISOR_OK;
+    case MISOR3_TUNE_ROWS: *value = g->rows; return MISOR_OK;
+    case MISOR3_TUNE_KCHUNK:
+        *value = g->kchunk > 0 ? g->kchunk : auto_kchunk(g->g, g->rows);
+        return MISOR_OK;
+    }
+    return fail3(MISOR_EINVAL, "unknown tuning key %d", key);
 }
 
 int misor3_enable_timing(misor_grid3* g, int on) {

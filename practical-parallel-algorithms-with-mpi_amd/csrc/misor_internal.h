@@ -200,6 +200,12 @@ void launch3_rhs(hipStream_t s, const G3& g, const double* f, const double* gg, 
 int launch3_rb_iteration(hipStream_t s, const G3& g, double* p, const double* rhs, double idx2,
                          double idy2, double idz2, double factor, double* partials, DevState* st,
                          double cells);
+// one solve iteration as ONE sweep launch (red then black, src -> dst) plus
+// the loop test; rows in {4, 8, 12}, kc planes per workgroup
+int sweep3_blocks(const G3& g, int rows, int kc);
+int launch3_sweep(hipStream_t s, const G3& g, const double* src, double* dst, const double* rhs,
+                  double idx2, double idy2, double idz2, double factor, int rows, int kc,
+                  double* partials, DevState* st, double cells);
 void launch3_fg(hipStream_t s, const G3& g, const double* u, const double* v, const double* w,
                 double* f, double* gg, double* h, const Fg3& c);
 void launch3_adapt(hipStream_t s, const G3& g, const double* f, const double* gg,

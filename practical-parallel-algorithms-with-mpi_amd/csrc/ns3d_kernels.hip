@@ -118,15 +118,16 @@ __global__ __launch_bounds__(256) void k3_rb_pass(G3 g, double* __restrict__ p,
 
 // end of one solve iteration: the reference never resets `res` (it is 1.0
 // before the first iteration only, solver.c:196), so
-//   res = (res + sum r^2 of pass 0 + sum r^2 of pass 1) / (imax*jmax*kmax)
-// then it++ and the loop test (solver.c:199, 280-282, 291)
+//   res = (res + sum r^2 of pass 0 [+ sum r^2 of pass 1]) / (imax*jmax*kmax)
+// then it++ and the loop test (solver.c:199, 280-282, 291).  npass = 2 for
+// the two colour-pass form, 1 for the fused sweep (one partial per block).
 __global__ __launch_bounds__(1024) void k3_finish(const double* __restrict__ partials, int nb,
-                                                  DevState* st, double cells) {
+                                                  int npass, DevState* st, double cells) {
     __shared__ double sh[1024];
     __shared__ double tot[2];
     if (st->done) return;
     const int t = threadIdx.x;
-    for (int ps = 0; ps < 2; ++ps) {
+    for (int ps = 0; ps < npass; ++ps) {
         double s = 0.0;
         for (int q = t; q < nb; q += 1024) s += partials[(long long)ps * nb + q];
         sh[t] = s;
@@ -142,12 +143,288 @@ __global__ __launch_bounds__(1024) void k3_finish(const double* __restrict__ par
         __syncthreads();
     }
     if (t == 0) {
-        const double res = ((st->res + tot[0]) + tot[1]) / cells;
+        double res = st->res + tot[0];
+        if (npass > 1) res = res + tot[1];
+        res = res / cells;
         const int it = st->it + 1;
         st->res = res;
         st->it = it;
         st->done = !((res >= st->epssq) && (it < st->itermax));
     }
+}
+
+// ------------------------------------------------- fused red-black sweep
+// One launch = one whole solve iteration (red of every cell, then black),
+// read from `src`, written to `dst` (ping-pong: blocks never see another
+// block's new values).  A workgroup owns a tile of kSwOwn columns x R rows and
+// a chunk of planes, and marches up k: at step k it updates the red cells of
+// plane k and then the black cells of plane k-1, whose red neighbours
+// (planes k-2, k-1, k) are all new by then -- exactly the values the
+// reference's two passes use.
+//
+// * Planes live in an LDS ring of 5 slots of (R+4) x 128 doubles: the tile
+//   plus a 2-cell ring, on which red is computed redundantly (black on the
+//   tile's edge needs red one cell outside).  Within a row the columns are
+//   stored split by parity (even columns, then odd ones), so the cells of one
+//   colour -- and each of their x-neighbours -- are 64 consecutive doubles:
+//   every LDS access of a wave is contiguous.
+// * Software pipeline: step k issues the loads of plane k+3 and of the rhs
+//   of step k+1, and writes plane k+2 (issued one step earlier) to LDS at
+//   its end; the k loop is unrolled by two so the register sets alternate
+//   with compile-time indices.  Loads are unconditional (addresses clamped
+//   into the array), so the compiler waits for each with a counted vmcnt.
+// * Everything per-thread that does not change along k (cell columns, LDS
+//   positions, in-plane offsets, validity and boundary flags, for the two
+//   parities of k) is computed once; a step adds scalar plane offsets.
+// * New values go straight from registers to dst; the Neumann face copy is
+//   fused as in k3_rb_pass.  Per-cell arithmetic is the reference's, term by
+//   term; the residual of the owned cells is summed per workgroup in a fixed
+//   order.
+constexpr int kSwCols = 128;           // loaded columns per strip
+constexpr int kSwOwn = kSwCols - 4;    // owned columns per strip
+constexpr int kSwSlots = 5;
+constexpr int kSwOdd = 80;             // LDS position of odd column 1 in a row: the odd half
+                                       // starts 32 banks after the even half
+constexpr int kSwRow = kSwOdd + 64;    // doubles per LDS row
+
+namespace {
+struct SwCell {
+    int lds;    // row offset + position of the cell in the split row
+    int nb;     // row offset + position of its left x-neighbour (right = nb + 1)
+    int go;     // j*sx + i (clamped into the plane when the cell is not valid)
+    int flags;  // 1 valid, 2 owned, 4 i==1, 8 i==I, 16 j==1, 32 j==J
+};
+
+// red (colour offset 1: i+j+k odd) or black (0) cell of LDS row t for planes
+// of parity q
+__device__ __forceinline__ SwCell sw_cell(const G3& g, int c_ld, int j_ld, int t, int lane,
+                                          int q, int colour, bool need_own_cols, int R) {
+    const int j = j_ld + t;
+    const int sel = ((c_ld + j + q) & 1) ^ colour;  // parity of the cell's LDS column
+    const int x = 2 * lane + sel, i = c_ld + x;
+    SwCell c;
+    c.lds = t * kSwRow + sel * kSwOdd + lane;
+    c.nb = t * kSwRow + (1 - sel) * kSwOdd + lane + sel - 1;
+    const bool inside = i >= 1 && i <= g.I && j >= 1 && j <= g.J;
+    const bool owned = inside && t >= 2 && t <= R + 1 && x >= 2 && x <= kSwCols - 3;
+    const bool valid = need_own_cols ? owned : (inside && x >= 1 && x <= kSwCols - 2);
+    c.go = valid ? j * (int)g.sx + i : 0;
+    c.flags = (valid ? 1 : 0) | (owned ? 2 : 0) | (i == 1 ? 4 : 0) | (i == g.I ? 8 : 0) |
+              (j == 1 ? 16 : 0) | (j == g.J ? 32 : 0);
+    return c;
+}
+}  // namespace
+
+template <int R>
+__global__ __launch_bounds__(256) void k3_sweep(G3 g, const double* __restrict__ src,
+                                                double* __restrict__ dst,
+                                                const double* __restrict__ rhs, double idx2,
+                                                double idy2, double idz2, double factor,
+                                                int nstrips, int nrowb, int kc,
+                                                double* __restrict__ partials,
+                                                const DevState* __restrict__ st) {
+    constexpr int NR = R + 4;  // rows per plane in LDS
+    static_assert(R % 4 == 0, "R must be a multiple of 4");
+    constexpr int LR = NR / 4;           // rows each wave loads
+    constexpr int RR = (R + 2 + 3) / 4;  // red rows per wave (LDS rows 1..R+2)
+    constexpr int BR = R / 4;            // black rows per wave (LDS rows 2..R+1)
+    constexpr int PL = NR * kSwRow;      // doubles per LDS plane
+    __shared__ double L[kSwSlots * PL];
+    __shared__ double sh[4];
+    if (st->done) return;
+
+    // XCD-aware order: the hardware deals workgroups round-robin to the 8 XCDs
+    // (each with its own L2); give XCD x a contiguous run of tiles so that
+    // neighbouring tiles -- which re-read each other's halo rows -- share an L2
+    int b;
+    {
+        const int nb = (int)gridDim.x, x = (int)blockIdx.x % 8, q = nb / 8, rem = nb % 8;
+        b = x * q + min(x, rem) + (int)blockIdx.x / 8;
+    }
+    const int strip = b % nstrips;
+    b /= nstrips;
+    const int rb = b % nrowb;
+    const int kb = b / nrowb;
+    const int c_ld = strip * kSwOwn - 1;  // global column of LDS column 0
+    const int j_ld = rb * R - 1;          // global row of LDS row 0 (owned rows j_ld+2 ..)
+    const int k0 = 1 + kb * kc;           // owned planes k0 .. kend
+    const int kend = min(g.K, k0 + kc - 1);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const long long sxy = g.sxy;
+    const int sx = (int)g.sx;
+
+    // loads: in-plane offsets (clamped) and LDS positions (parity split)
+    int lo[LR][2], ls[LR][2];
+#pragma unroll
+    for (int m = 0; m < LR; ++m) {
+        const int t = w + 4 * m;
+        const int j = min(max(j_ld + t, 0), g.J + 1);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int x = lane + 64 * h;
+            lo[m][h] = j * sx + min(max(c_ld + x, 0), g.I + 1);
+            ls[m][h] = t * kSwRow + (x & 1) * kSwOdd + (x >> 1);
+        }
+    }
+    // cells for the two parities of k: A = parity of the first step (k0-1)
+    const int qa = (k0 - 1) & 1;
+    SwCell redA[RR], redB[RR], blkA[BR], blkB[BR];
+#pragma unroll
+    for (int m = 0; m < RR; ++m) {
+        const int t = 1 + w + 4 * m;
+        redA[m] = sw_cell(g, c_ld, j_ld, t, lane, qa, 1, false, R);
+        redB[m] = sw_cell(g, c_ld, j_ld, t, lane, qa ^ 1, 1, false, R);
+        if (t > R + 2) redA[m].flags = redB[m].flags = 0;
+    }
+#pragma unroll
+    for (int m = 0; m < BR; ++m) {
+        const int t = 2 + w + 4 * m;
+        // the black cells of step k are in plane k-1: parity q ^ 1
+        blkA[m] = sw_cell(g, c_ld, j_ld, t, lane, qa ^ 1, 0, true, R);
+        blkB[m] = sw_cell(g, c_ld, j_ld, t, lane, qa, 0, true, R);
+    }
+
+    auto slot = [](int kk) { return (kk + kSwSlots) % kSwSlots; };
+    auto plane = [&](int kk) { return (long long)min(max(kk, 0), g.K + 1) * sxy; };
+    auto load_plane = [&](int kk, double (&v)[LR][2]) {
+        const double* sp = src + plane(kk);
+#pragma unroll
+        for (int m = 0; m < LR; ++m)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) v[m][h] = sp[lo[m][h]];
+    };
+    auto store_plane = [&](int kk, const double (&v)[LR][2]) {
+        double* Ls = L + slot(kk) * PL;
+#pragma unroll
+        for (int m = 0; m < LR; ++m)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) Ls[ls[m][h]] = v[m][h];
+    };
+    // the rhs of step k: red cells of plane k, black cells of plane k-1
+    auto load_rhs = [&](int k, const SwCell (&rc)[RR], const SwCell (&bc)[BR], double (&rr)[RR],
+                        double (&rbk)[BR]) {
+        const double* rp = rhs + plane(k);
+        const double* bp = rhs + plane(k - 1);
+#pragma unroll
+        for (int m = 0; m < RR; ++m) rr[m] = rp[rc[m].go];
+#pragma unroll
+        for (int m = 0; m < BR; ++m) rbk[m] = bp[bc[m].go];
+    };
+    double acc = 0.0;
+    // one update: the reference's arithmetic on LDS neighbours; returns the new value
+    auto update = [&](const double* Lc, const double* Lm, const double* Lp, const SwCell& c,
+                      double rh, double& r) {
+        const double cc = Lc[c.lds];
+        const double tx = (Lc[c.nb + 1] - 2.0 * cc) + Lc[c.nb];
+        const double ty = (Lc[c.lds + kSwRow] - 2.0 * cc) + Lc[c.lds - kSwRow];
+        const double tz = (Lp[c.lds] - 2.0 * cc) + Lm[c.lds];
+        r = rh - ((tx * idx2 + ty * idy2) + tz * idz2);
+        return cc - (factor * r);
+    };
+    // owned cells of a finished plane (both colours) from LDS to dst in whole
+    // rows -- full 128-B lines, one write per line -- with the Neumann face
+    // mirrors of the boundary cells (solver.c:237-278)
+    int so[BR][2], sl[BR][2], sf[BR][2];
+#pragma unroll
+    for (int m = 0; m < BR; ++m) {
+        const int t = 2 + w + 4 * m, j = j_ld + t;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int x = lane + 64 * h, i = c_ld + x;
+            const bool own = x >= 2 && x <= kSwCols - 3 && i >= 1 && i <= g.I && j >= 1 &&
+                             j <= g.J;
+            so[m][h] = own ? j * sx + i : 0;
+            sl[m][h] = t * kSwRow + (x & 1) * kSwOdd + (x >> 1);
+            sf[m][h] = own ? (1 | (i == 1 ? 4 : 0) | (i == g.I ? 8 : 0) | (j == 1 ? 16 : 0) |
+                              (j == g.J ? 32 : 0))
+                           : 0;
+        }
+    }
+    auto store_final = [&](int kk) {
+        const double* Ls = L + slot(kk) * PL;
+        double* dk = dst + (long long)kk * sxy;
+#pragma unroll
+        for (int m = 0; m < BR; ++m)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int f = sf[m][h];
+                if (f & 1) {
+                    const double v = Ls[sl[m][h]];
+                    const int o = so[m][h];
+                    dk[o] = v;
+                    if (f & 4) dk[o - 1] = v;
+                    if (f & 8) dk[o + 1] = v;
+                    if (f & 16) dk[o - sx] = v;
+                    if (f & 32) dk[o + sx] = v;
+                    if (kk == 1) dk[o - sxy] = v;
+                    if (kk == g.K) dk[o + sxy] = v;
+                }
+            }
+    };
+    auto step = [&](const int k, double (&pl_in)[LR][2], const double (&pl_out)[LR][2],
+                    const SwCell (&rc)[RR], const SwCell (&bc)[BR], const double (&rr)[RR],
+                    const double (&rbk)[BR], const SwCell (&rc_n)[RR], const SwCell (&bc_n)[BR],
+                    double (&rr_n)[RR], double (&rbk_n)[BR]) {
+        load_plane(k + 3, pl_in);
+        load_rhs(k + 1, rc_n, bc_n, rr_n, rbk_n);
+        __syncthreads();  // plane k+1 in LDS, plane k-2 final; the slot reused below is free
+        if (k - 2 >= k0 && k - 2 <= kend) store_final(k - 2);
+        if (k >= 1 && k <= g.K) {
+            double* Lc = L + slot(k) * PL;
+            const double* Lm = L + slot(k - 1) * PL;
+            const double* Lp = L + slot(k + 1) * PL;
+            const bool own_k = k >= k0 && k <= kend;
+#pragma unroll
+            for (int m = 0; m < RR; ++m) {
+                if (rc[m].flags & 1) {
+                    double r;
+                    const double np = update(Lc, Lm, Lp, rc[m], rr[m], r);
+                    Lc[rc[m].lds] = np;
+                    if (own_k && (rc[m].flags & 2)) acc += r * r;
+                }
+            }
+        }
+        __syncthreads();  // red of plane k visible
+        if (k - 1 >= k0 && k - 1 <= kend) {
+            const int kb1 = k - 1;
+            double* Lc = L + slot(kb1) * PL;
+            const double* Lm = L + slot(kb1 - 1) * PL;
+            const double* Lp = L + slot(k) * PL;
+#pragma unroll
+            for (int m = 0; m < BR; ++m) {
+                if (bc[m].flags & 1) {
+                    double r;
+                    const double np = update(Lc, Lm, Lp, bc[m], rbk[m], r);
+                    Lc[bc[m].lds] = np;
+                    acc += r * r;
+                }
+            }
+        }
+        store_plane(k + 2, pl_out);
+    };
+
+    // preload planes k0-2 .. k0 into LDS, plane k0+1 into registers
+    {
+        double v[LR][2];
+        for (int kk = k0 - 2; kk <= k0; ++kk) {
+            load_plane(kk, v);
+            store_plane(kk, v);
+        }
+    }
+    double pl[2][LR][2];
+    double rrs[2][RR], rbs[2][BR];
+    load_plane(k0 + 1, pl[0]);
+    load_rhs(k0 - 1, redA, blkA, rrs[0], rbs[0]);
+    // pl[0] holds plane k0+1 (written at the end of step k0-1), pl[1] receives k0+2
+    for (int k = k0 - 1; k <= kend + 1; k += 2) {
+        step(k, pl[1], pl[0], redA, blkA, rrs[0], rbs[0], redB, blkB, rrs[1], rbs[1]);
+        if (k + 1 <= kend + 1)
+            step(k + 1, pl[0], pl[1], redB, blkB, rrs[1], rbs[1], redA, blkA, rrs[0], rbs[0]);
+    }
+    __syncthreads();  // black of plane kend done
+    store_final(kend);
+    const double s = block_sum256(acc, sh);
+    if (threadIdx.x == 0) partials[blockIdx.x] = s;
 }
 
 // computeFG, solver.c:606-772 (interior cells)
@@ -395,7 +672,36 @@ int launch3_rb_iteration(hipStream_t s, const G3& g, double* p, const double* rh
     for (int pass = 0; pass < 2; ++pass)
         hipLaunchKernelGGL(k3_rb_pass, grid, dim3(kBx, kBy), 0, s, g, p, rhs, pass, idx2, idy2,
                            idz2, factor, partials + (long long)pass * nb, st);
-    hipLaunchKernelGGL(k3_finish, dim3(1), dim3(1024), 0, s, partials, nb, st, cells);
+    hipLaunchKernelGGL(k3_finish, dim3(1), dim3(1024), 0, s, partials, nb, 2, st, cells);
+    return nb;
+}
+
+int sweep3_blocks(const G3& g, int rows, int kc) {
+    const long long nstr = (g.I + kSwOwn - 1) / kSwOwn, nrb = (g.J + rows - 1) / rows,
+                    nkc = (g.K + kc - 1) / kc;
+    return (int)(nstr * nrb * nkc);
+}
+
+int launch3_sweep(hipStream_t s, const G3& g, const double* src, double* dst, const double* rhs,
+                  double idx2, double idy2, double idz2, double factor, int rows, int kc,
+                  double* partials, DevState* st, double cells) {
+    const int nstr = (g.I + kSwOwn - 1) / kSwOwn, nrb = (g.J + rows - 1) / rows;
+    const int nb = sweep3_blocks(g, rows, kc);
+    switch (rows) {
+    case 4:
+        hipLaunchKernelGGL(k3_sweep<4>, dim3(nb), dim3(256), 0, s, g, src, dst, rhs, idx2, idy2,
+                           idz2, factor, nstr, nrb, kc, partials, st);
+        break;
+    case 12:
+        hipLaunchKernelGGL(k3_sweep<12>, dim3(nb), dim3(256), 0, s, g, src, dst, rhs, idx2, idy2,
+                           idz2, factor, nstr, nrb, kc, partials, st);
+        break;
+    default:
+        hipLaunchKernelGGL(k3_sweep<8>, dim3(nb), dim3(256), 0, s, g, src, dst, rhs, idx2, idy2,
+                           idz2, factor, nstr, nrb, kc, partials, st);
+        break;
+    }
+    hipLaunchKernelGGL(k3_finish, dim3(1), dim3(1024), 0, s, partials, nb, 1, st, cells);
     return nb;
 }
 

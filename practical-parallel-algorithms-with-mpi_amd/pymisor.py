@@ -28,6 +28,7 @@ LEX_A4, LEX_SEQ = 0, 1
 COMM_ID_BYTES = 128
 # 3D field ids (misor3_*)
 P3, RHS3, U3, V3, W3, F3, G3, H3 = range(8)
+TUNE3_SWEEP, TUNE3_ROWS, TUNE3_KCHUNK = 1, 2, 3
 
 _dp = C.POINTER(C.c_double)
 
@@ -123,6 +124,8 @@ SIGNATURES = {
     "misor3_normalize_pressure": (C.c_int, [C.c_void_p]),
     "misor3_synchronize": (C.c_int, [C.c_void_p]),
     "misor3_enable_timing": (C.c_int, [C.c_void_p, C.c_int]),
+    "misor3_set_tuning": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
+    "misor3_get_tuning": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_int)]),
     "misor3_get_solve_time": (C.c_int, [C.c_void_p, _dp, C.POINTER(C.c_longlong)]),
 }
 
@@ -381,6 +384,14 @@ class Grid3:
 
     def enable_timing(self, on=True):
         _check(lib().misor3_enable_timing(self.h, 1 if on else 0))
+
+    def set_tuning(self, key, value):
+        _check(lib().misor3_set_tuning(self.h, key, value))
+
+    def get_tuning(self, key):
+        v = C.c_int(0)
+        _check(lib().misor3_get_tuning(self.h, key, C.byref(v)))
+        return v.value
 
     def solve_time(self):
         """(device ms, iterations) of the solves timed since enable_timing"""

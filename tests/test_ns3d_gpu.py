@@ -47,13 +47,23 @@ def random_state(shape, seed):
     return st
 
 
-def pair(prm, st, dt):
+# 3D solve variants (sweep, rows, kchunk): the fused k-march sweep with the
+# default and odd geometries (chunk boundaries inside the grid), and the
+# two colour-pass form
+SOLVE_TUNES = [(1, 8, 0), (1, 4, 4), (1, 12, 5), (1, 8, 3 + 4), (0, 8, 0)]
+
+
+def pair(prm, st, dt, tune=None):
     """oracle and GPU grid holding the same state"""
     ns = orc3.NS3(prm)
     for n in orc3.FIELDS:
         getattr(ns, n)[...] = st[n]
     ns.s.dt = dt
     g = M.Grid3(prm)
+    if tune is not None:
+        g.set_tuning(M.TUNE3_SWEEP, tune[0])
+        g.set_tuning(M.TUNE3_ROWS, tune[1])
+        g.set_tuning(M.TUNE3_KCHUNK, tune[2])
     for n in orc3.FIELDS:
         g.upload(GPU_FIELD[n], st[n])
     g.set_dt(dt)
@@ -125,26 +135,29 @@ def test_compute_timestep_at_rest(golden):
         assert g.compute_timestep() == ns.s.dt
 
 
+@pytest.mark.parametrize("tune", SOLVE_TUNES)
 @pytest.mark.parametrize("dims,itermax", [((5, 4, 3), 37), ((12, 9, 7), 11),
                                           ((64, 16, 8), 25), ((131, 37, 19), 9),
+                                          ((125, 13, 30), 4), ((249, 25, 17), 2),
                                           ((256, 128, 64), 3)])
-def test_solve_fixed_iterations_bitwise(golden, dims, itermax):
+def test_solve_fixed_iterations_bitwise(golden, dims, itermax, tune):
     prm = params(golden, "a6_dcavity.par", imax=dims[0], jmax=dims[1], kmax=dims[2],
                  eps=1e-150, itermax=itermax)
     shape = (dims[2] + 2, dims[1] + 2, dims[0] + 2)
     st = random_state(shape, sum(dims))
-    ns, g = pair(prm, st, 0.02)
+    ns, g = pair(prm, st, 0.02, tune)
     with g:
         it_ref, res_ref = ns.solve()
         it, res = g.solve()
         assert it == it_ref == itermax
-        assert np.array_equal(g.download(M.P3), ns.p)
+        assert_fields_equal(ns, g, "solve")  # p incl. every ghost, and nothing else touched
         assert res == pytest.approx(res_ref, rel=1e-12)
 
 
+@pytest.mark.parametrize("tune", SOLVE_TUNES)
 @pytest.mark.parametrize("dims,eps", [((24, 20, 16), 1e-3), ((40, 12, 10), 1e-4),
                                       ((33, 33, 33), 1e-4)])
-def test_solve_converges_like_oracle(golden, dims, eps):
+def test_solve_converges_like_oracle(golden, dims, eps, tune):
     """convergence-driven stop: same iteration count and bit-identical p"""
     prm = params(golden, "a6_dcavity.par", imax=dims[0], jmax=dims[1], kmax=dims[2],
                  eps=eps, itermax=5000)
@@ -152,7 +165,7 @@ def test_solve_converges_like_oracle(golden, dims, eps):
     st = random_state(shape, 11)
     st["p"] *= 1e-3
     st["rhs"] *= 1e-3
-    ns, g = pair(prm, st, 0.02)
+    ns, g = pair(prm, st, 0.02, tune)
     with g:
         it_ref, res_ref = ns.solve()
         it, res = g.solve()
@@ -165,6 +178,13 @@ def test_solve_converges_like_oracle(golden, dims, eps):
         it2, _ = g.solve()
         assert it2 == it2_ref
         assert np.array_equal(g.download(M.P3), ns.p)
+        # a third after p was replaced from the host (edges and corners included)
+        newp = np.random.default_rng(5).standard_normal(shape) * 1e-3
+        ns.p[...] = newp
+        g.upload(M.P3, newp)
+        it3_ref, _ = ns.solve()
+        assert g.solve()[0] == it3_ref
+        assert np.array_equal(g.download(M.P3), ns.p)
 
 
 def test_solve_itermax_zero_does_nothing(golden):
@@ -176,9 +196,13 @@ def test_solve_itermax_zero_does_nothing(golden):
         assert np.array_equal(g.download(M.P3), st["p"])
 
 
-def run_gpu(prm, steps):
+def run_gpu(prm, steps, tune=None):
     """assignment-6/src/main.c:45-60 through the C ABI (no normalizePressure)"""
     g = M.Grid3(prm)
+    if tune is not None:
+        g.set_tuning(M.TUNE3_SWEEP, tune[0])
+        g.set_tuning(M.TUNE3_ROWS, tune[1])
+        g.set_tuning(M.TUNE3_KCHUNK, tune[2])
     g.fill(M.U3, prm["u_init"])
     g.fill(M.V3, prm["v_init"])
     g.fill(M.W3, prm["w_init"])
@@ -196,14 +220,15 @@ def run_gpu(prm, steps):
     return g, np.array(iters), t
 
 
+@pytest.mark.parametrize("tune", [(1, 8, 0), (0, 8, 0), (1, 4, 4)])
 @pytest.mark.parametrize("fixture,par", [("ns3d_dcavity_short.npz", "a6_dcavity.par"),
                                          ("ns3d_canal_short.npz", "a6_canal.par")])
-def test_short_run_matches_reference_fixture(golden, fixture, par):
+def test_short_run_matches_reference_fixture(golden, fixture, par, tune):
     ref = np.load(os.path.join(golden, fixture))
     dims = [int(x) for x in ref["dims"]]
     prm = params(golden, par, imax=dims[0], jmax=dims[1], kmax=dims[2])
     steps = int(ref["steps"])
-    g, iters, t = run_gpu(prm, steps)
+    g, iters, t = run_gpu(prm, steps, tune)
     with g:
         assert np.array_equal(iters, ref["iters"])
         assert t == ref["t"]
@@ -222,3 +247,13 @@ def test_medium_run_matches_oracle(golden):
         assert t == t_ref
         for n in ("p", "u", "v", "w"):
             assert np.array_equal(g.download(GPU_FIELD[n]), getattr(ns, n)), n
+
+
+def test_tuning_keys(golden):
+    prm = params(golden, "a6_dcavity.par", imax=8, jmax=8, kmax=8)
+    with M.Grid3(prm) as g:
+        assert g.get_tuning(M.TUNE3_SWEEP) == 1 and g.get_tuning(M.TUNE3_ROWS) == 8
+        assert g.get_tuning(M.TUNE3_KCHUNK) >= 8
+        for key, bad in ((M.TUNE3_SWEEP, 2), (M.TUNE3_ROWS, 5), (M.TUNE3_KCHUNK, 2), (99, 0)):
+            with pytest.raises(M.MisorError):
+                g.set_tuning(key, bad)

@@ -87,6 +87,36 @@ def cpu_baseline(n=8192, sweeps=40):
                       % (n, n, sweeps, solve_s)}
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline_multicore(n=16384, sweeps=40):
+    """solveRB on all the host cores this job may use (no MPI on
+    the box, so pthreads over row bands, oracle/oracle_mt.c -- the restatement,
+    p bit-identical to the single-core solve); bounded sample"""
+    import numpy as np  # noqa: F401
+    import orc
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+    p, rhs = orc.poisson_init(n, n)
+    t1 = time.perf_counter()
+    it, _ = orc.solve_rb_mt(p, rhs, 1.0 / n, 1.0 / n, 1.9, 1e-300, sweeps, threads)
+    solve_s = time.perf_counter() - t1
+    assert it == sweeps
+    return {"value": round(n * n * sweeps / solve_s / 1e6, 1), "unit": "MLUP/s",
+            "cores": threads, "kind": "port", "cpu": cpu_model(),
+            "nproc": os.cpu_count(),
+            "sample": "solveRB %dx%d, %d sweeps, %.2f s solve, %d threads over row bands "
+                      "(oracle/oracle_mt.c)" % (n, n, sweeps, solve_s, threads)}
+
+
 def pmc_traffic(size, nranks, T):
     """HBM bytes per launch from the committed PMC summary, or None."""
     best = None
@@ -458,6 +488,10 @@ def main():
             out["cpu_baseline"] = cpu_baseline()
         except Exception as e:  # reported, never fatal for the GPU number
             out["cpu_baseline"] = {"value": None, "error": repr(e)}
+        try:
+            out["cpu_baseline_multicore"] = cpu_baseline_multicore()
+        except Exception as e:
+            out["cpu_baseline_multicore"] = {"value": None, "error": repr(e)}
     g.close()
     if dist is not None:
         dist.barrier()

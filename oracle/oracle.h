@@ -93,4 +93,9 @@ int orc_ns_run(orc_ns* s, int solver, int max_steps, int* iters, int cap,
 #ifdef __cplusplus
 }
 #endif
+/* multi-core solveRB (oracle_mt.c): the bench's multi-core CPU baseline; p
+ * bit-identical to orc_solve_rb, residual summed per thread band */
+int orc_solve_rb_mt(int imax, int jmax, double dx, double dy, double omega, double eps,
+                    int itermax, double* p, const double* rhs, double* res_out, int nthreads);
+
 #endif

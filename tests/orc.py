@@ -90,6 +90,19 @@ def solve_rb(p, rhs, dx, dy, omega, eps, itermax, variant="rb"):
     return it, res.value
 
 
+def solve_rb_mt(p, rhs, dx, dy, omega, eps, itermax, nthreads):
+    """multi-core solveRB (oracle_mt.c), in place on p"""
+    L = lib()
+    L.orc_solve_rb_mt.argtypes = [C.c_int, C.c_int, C.c_double, C.c_double, C.c_double,
+                                  C.c_double, C.c_int, _dp, _dp, _dp, C.c_int]
+    L.orc_solve_rb_mt.restype = C.c_int
+    jmax, imax = p.shape[0] - 2, p.shape[1] - 2
+    res = C.c_double(0.0)
+    it = L.orc_solve_rb_mt(imax, jmax, dx, dy, omega, eps, itermax, _ptr(p), _ptr(rhs),
+                           C.byref(res), nthreads)
+    return it, res.value
+
+
 def solve_lex(p, rhs, dx, dy, omega, eps, itermax, xorder=0):
     jmax, imax = p.shape[0] - 2, p.shape[1] - 2
     res = C.c_double(0.0)

@@ -165,3 +165,21 @@ def test_lex_ns_oracle_vs_reference_fixture(golden):
     assert steps == int(z["steps"])
     for k in ("p", "u", "v"):
         assert np.array_equal(getattr(ns, k), z[k]), k
+
+
+@pytest.mark.parametrize("ni,nj,threads", [(37, 23, 3), (64, 64, 8), (100, 100, 4), (9, 5, 8)])
+def test_multicore_solve_rb_matches_single_thread(ni, nj, threads):
+    """the bench's multi-core CPU baseline (oracle_mt.c) is the same solveRB:
+    p bit for bit, same iteration count; residual to rounding"""
+    p1, rhs = orc.poisson_init(ni, nj, 1.0, 1.0, 2)
+    p2 = p1.copy()
+    it1, r1 = orc.solve_rb(p1, rhs, 1.0 / ni, 1.0 / nj, 1.9, 1e-300, 25)
+    it2, r2 = orc.solve_rb_mt(p2, rhs, 1.0 / ni, 1.0 / nj, 1.9, 1e-300, 25, threads)
+    assert it1 == it2 == 25
+    assert np.array_equal(p1, p2)
+    assert r2 == pytest.approx(r1, rel=1e-12)
+    # to convergence: the poisson.par iteration count
+    if (ni, nj) == (100, 100):
+        p3, _ = orc.poisson_init(ni, nj, 1.0, 1.0, 2)
+        it3, _ = orc.solve_rb_mt(p3, rhs, 0.01, 0.01, 1.9, 1e-6, 1000000, threads)
+        assert it3 == 2388

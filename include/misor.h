@@ -226,19 +226,34 @@ typedef struct {
     int bcTop, bcBottom, bcLeft, bcRight, bcFront, bcBack; /* MISOR_NOSLIP ... */
     int problem;                        /* MISOR_PROBLEM_* */
     int device;                         /* HIP device; < 0: the current one */
+    /* decomposition: slabs of planes along k (misor3_decompose); nranks <= 1 =
+     * one GPU.  comm_id as misor_desc.comm_id (RCCL id from
+     * misor_comm_unique_id, or "LOCAL:<name>" for ranks as host threads) */
+    int nranks, rank;
+    const void* comm_id;
 } misor3_desc;
 
 /* field ids of misor3_upload / misor3_download / misor3_fill */
 enum { MISOR3_P = 0, MISOR3_RHS = 1, MISOR3_U = 2, MISOR3_V = 3, MISOR3_W = 4,
        MISOR3_F = 5, MISOR3_G = 6, MISOR3_H = 7 };
 
-/* initSolver (solver.c:60-143): device fields, all zero; dx = xlength/imax ... */
+/* the slab of `rank`: kloc planes from global plane koff+1 (sizeOfRank rule,
+ * assignment-6/src/comm.c:24-101, along k only); at least 2 planes per rank.
+ * The reference splits over a 3D process grid; see DESIGN.md 6b.  host-only */
+int misor3_decompose(int nranks, int rank, int kmax, int* kloc, int* koff);
+/* initSolver (solver.c:60-143): device fields, all zero; dx = xlength/imax ...
+ * Decomposed grids hold their slab: local arrays (imax+2)(jmax+2)(kloc+2) */
 int misor3_create(misor_grid3** out, const misor3_desc* d);
+int misor3_local_info(const misor_grid3* g, int* kloc, int* koff);
 void misor3_destroy(misor_grid3* g);
 /* whole field incl. ghosts, (imax+2)(jmax+2)(kmax+2) doubles */
 int misor3_upload(misor_grid3* g, int field, const double* host);
 int misor3_download(misor_grid3* g, int field, double* host);
 int misor3_fill(misor_grid3* g, int field, double value);
+/* commCollectResult's gather (assignment-6/src/comm.c:246-384) of a whole
+ * field, collective: rank 0 receives (imax+2)(jmax+2)(kmax+2) doubles, the
+ * other ranks pass NULL.  One rank: misor3_download */
+int misor3_gather(misor_grid3* g, int field, double* host_global);
 int misor3_set_dt(misor_grid3* g, double dt);
 /* computeTimestep (solver.c:340-362): dt = tau * min(dtBound, dx/umax, dy/vmax,
  * dz/wmax), dtBound = 0.5*re/(1/dx^2+1/dy^2+1/dz^2) (solver.c:136-139) */
@@ -249,7 +264,9 @@ int misor3_set_boundary_conditions(misor_grid3* g);       /* solver.c:364-577 */
 int misor3_set_special_boundary_condition(misor_grid3* g); /* solver.c:579-604 */
 int misor3_compute_fg(misor_grid3* g);                    /* solver.c:606-824 */
 int misor3_compute_rhs(misor_grid3* g);                   /* solver.c:145-173 */
-/* solve (solver.c:175-297): red-black SOR until res < eps^2 or itermax */
+/* solve (solver.c:175-297): red-black SOR until res < eps^2 or itermax;
+ * decomposed: halos and the residual sum cross the ranks, p and the
+ * iteration count are those of the single-domain solve */
 int misor3_solve(misor_grid3* g, int* iters, double* res);
 int misor3_adapt_uvw(misor_grid3* g);                     /* solver.c:826-853 */
 int misor3_normalize_pressure(misor_grid3* g);            /* solver.c:312-338 */

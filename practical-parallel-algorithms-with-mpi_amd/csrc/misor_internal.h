@@ -183,8 +183,10 @@ enum { kReduceSum = 0, kReduceMax = 1 };
 // 3D (assignment-6): dense reference layout (imax+2)(jmax+2)(kmax+2), i fastest
 // ---------------------------------------------------------------------------
 struct G3 {
-    int I, J, K;        // interior cells
+    int I, J, K;        // interior cells (K: this rank's planes)
     long long sx, sxy;  // strides of j and k: (I+2), (I+2)(J+2)
+    int Kg = 0, koff = 0;            // global planes; global k of local plane 0
+    int lo_phys = 1, hi_phys = 1;    // local planes 1 / K border the physical boundary
     __host__ __device__ long long ix(int i, int j, int k) const {
         return (long long)k * sxy + (long long)j * sx + i;
     }
@@ -205,7 +207,7 @@ int launch3_rb_iteration(hipStream_t s, const G3& g, double* p, const double* rh
 int sweep3_blocks(const G3& g, int rows, int kc);
 int launch3_sweep(hipStream_t s, const G3& g, const double* src, double* dst, const double* rhs,
                   double idx2, double idy2, double idz2, double factor, int rows, int kc,
-                  double* partials, DevState* st, double cells);
+                  double* partials, DevState* st, double cells, bool sum_only = false);
 void launch3_fg(hipStream_t s, const G3& g, const double* u, const double* v, const double* w,
                 double* f, double* gg, double* h, const Fg3& c);
 void launch3_adapt(hipStream_t s, const G3& g, const double* f, const double* gg,
@@ -219,5 +221,12 @@ void launch3_absmax(hipStream_t s, const double* u, const double* v, const doubl
                     long long n, double* partials, double* out);
 void launch3_normalize(hipStream_t s, const G3& g, double* p, double* partials, double* sum,
                        double cells);
+// normalizePressure in two halves around a cross-rank all-reduce of *sum
+void launch3_interior_sum(hipStream_t s, const G3& g, const double* p, double* partials,
+                          double* sum);
+void launch3_sub_mean(hipStream_t s, const G3& g, double* p, const double* sum, double cells);
+// the loop test of a decomposed solve: st->sum[0] holds the all-reduced sum
+// of r^2 of the iteration (written by launch3_sweep with sum_only)
+void launch3_decide(hipStream_t s, DevState* st, double cells);
 
 }  // namespace misor

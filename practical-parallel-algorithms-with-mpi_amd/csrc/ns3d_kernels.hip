@@ -122,7 +122,8 @@ __global__ __launch_bounds__(256) void k3_rb_pass(G3 g, double* __restrict__ p,
 // then it++ and the loop test (solver.c:199, 280-282, 291).  npass = 2 for
 // the two colour-pass form, 1 for the fused sweep (one partial per block).
 __global__ __launch_bounds__(1024) void k3_finish(const double* __restrict__ partials, int nb,
-                                                  int npass, DevState* st, double cells) {
+                                                  int npass, DevState* st, double cells,
+                                                  int sum_only) {
     __shared__ double sh[1024];
     __shared__ double tot[2];
     if (st->done) return;
@@ -142,7 +143,8 @@ __global__ __launch_bounds__(1024) void k3_finish(const double* __restrict__ par
         }
         __syncthreads();
     }
-    if (t == 0) {
+    if (t == 0 && sum_only) st->sum[0] = tot[0];  // decomposed: all-reduce, then decide
+    if (t == 0 && !sum_only) {
         double res = st->res + tot[0];
         if (npass > 1) res = res + tot[1];
         res = res / cells;
@@ -151,6 +153,16 @@ __global__ __launch_bounds__(1024) void k3_finish(const double* __restrict__ par
         st->it = it;
         st->done = !((res >= st->epssq) && (it < st->itermax));
     }
+}
+
+// decomposed solve: res = (res + all-reduced sum r^2) / (imax*jmax*kmax)
+__global__ void k3_decide(DevState* st, double cells) {
+    if (threadIdx.x != 0 || st->done) return;
+    const double res = (st->res + st->sum[0]) / cells;
+    const int it = st->it + 1;
+    st->res = res;
+    st->it = it;
+    st->done = !((res >= st->epssq) && (it < st->itermax));
 }
 
 // ------------------------------------------------- fused red-black sweep
@@ -267,7 +279,7 @@ __global__ __launch_bounds__(256) void k3_sweep(G3 g, const double* __restrict__
         }
     }
     // cells for the two parities of k: A = parity of the first step (k0-1)
-    const int qa = (k0 - 1) & 1;
+    const int qa = (k0 - 1 + g.koff) & 1;  // colours are global: i + j + (koff + k)
     SwCell redA[RR], redB[RR], blkA[BR], blkB[BR];
 #pragma unroll
     for (int m = 0; m < RR; ++m) {
@@ -285,7 +297,10 @@ __global__ __launch_bounds__(256) void k3_sweep(G3 g, const double* __restrict__
     }
 
     auto slot = [](int kk) { return (kk + kSwSlots) % kSwSlots; };
-    auto plane = [&](int kk) { return (long long)min(max(kk, 0), g.K + 1) * sxy; };
+    // planes -1 .. K+2 exist in memory (2-deep halo storage)
+    auto plane = [&](int kk) { return (long long)min(max(kk, -1), g.K + 2) * sxy; };
+    // red is computed on halo planes too where a neighbour rank owns them
+    const int kr_lo = g.lo_phys ? 1 : 0, kr_hi = g.hi_phys ? g.K : g.K + 1;
     auto load_plane = [&](int kk, double (&v)[LR][2]) {
         const double* sp = src + plane(kk);
 #pragma unroll
@@ -356,8 +371,8 @@ __global__ __launch_bounds__(256) void k3_sweep(G3 g, const double* __restrict__
                     if (f & 8) dk[o + 1] = v;
                     if (f & 16) dk[o - sx] = v;
                     if (f & 32) dk[o + sx] = v;
-                    if (kk == 1) dk[o - sxy] = v;
-                    if (kk == g.K) dk[o + sxy] = v;
+                    if (kk == 1 && g.lo_phys) dk[o - sxy] = v;
+                    if (kk == g.K && g.hi_phys) dk[o + sxy] = v;
                 }
             }
     };
@@ -369,7 +384,7 @@ __global__ __launch_bounds__(256) void k3_sweep(G3 g, const double* __restrict__
         load_rhs(k + 1, rc_n, bc_n, rr_n, rbk_n);
         __syncthreads();  // plane k+1 in LDS, plane k-2 final; the slot reused below is free
         if (k - 2 >= k0 && k - 2 <= kend) store_final(k - 2);
-        if (k >= 1 && k <= g.K) {
+        if (k >= kr_lo && k <= kr_hi) {
             double* Lc = L + slot(k) * PL;
             const double* Lm = L + slot(k - 1) * PL;
             const double* Lp = L + slot(k + 1) * PL;
@@ -491,8 +506,8 @@ __global__ void k3_fg_boundary(G3 g, const double* __restrict__ u, const double*
         gg[g.ix(a, g.J, b)] = v[g.ix(a, g.J, b)];
     } else {
         if (a > g.I || b > g.J) return;
-        h[g.ix(a, b, 0)] = w[g.ix(a, b, 0)];
-        h[g.ix(a, b, g.K)] = w[g.ix(a, b, g.K)];
+        if (g.lo_phys) h[g.ix(a, b, 0)] = w[g.ix(a, b, 0)];
+        if (g.hi_phys) h[g.ix(a, b, g.K)] = w[g.ix(a, b, g.K)];
     }
 }
 
@@ -546,7 +561,8 @@ __global__ void k3_special(G3 g, double* __restrict__ u, int problem) {
     const int a = 1 + blockIdx.x * blockDim.x + threadIdx.x;
     const int b = 1 + blockIdx.y;
     if (problem == MISOR_PROBLEM_DCAVITY) {  // i = 1..imax-1, k = 1..kmax-1
-        if (a < g.I && b < g.K) u[g.ix(a, g.J + 1, b)] = 2.0 - u[g.ix(a, g.J, b)];
+        if (a < g.I && b <= g.K && g.koff + b < g.Kg)
+            u[g.ix(a, g.J + 1, b)] = 2.0 - u[g.ix(a, g.J, b)];
     } else if (problem == MISOR_PROBLEM_CANAL) {  // U(0,j,k) = 2.0
         if (a <= g.J && b <= g.K) u[g.ix(0, a, b)] = 2.0;
     }
@@ -672,7 +688,7 @@ int launch3_rb_iteration(hipStream_t s, const G3& g, double* p, const double* rh
     for (int pass = 0; pass < 2; ++pass)
         hipLaunchKernelGGL(k3_rb_pass, grid, dim3(kBx, kBy), 0, s, g, p, rhs, pass, idx2, idy2,
                            idz2, factor, partials + (long long)pass * nb, st);
-    hipLaunchKernelGGL(k3_finish, dim3(1), dim3(1024), 0, s, partials, nb, 2, st, cells);
+    hipLaunchKernelGGL(k3_finish, dim3(1), dim3(1024), 0, s, partials, nb, 2, st, cells, 0);
     return nb;
 }
 
@@ -684,7 +700,7 @@ int sweep3_blocks(const G3& g, int rows, int kc) {
 
 int launch3_sweep(hipStream_t s, const G3& g, const double* src, double* dst, const double* rhs,
                   double idx2, double idy2, double idz2, double factor, int rows, int kc,
-                  double* partials, DevState* st, double cells) {
+                  double* partials, DevState* st, double cells, bool sum_only) {
     const int nstr = (g.I + kSwOwn - 1) / kSwOwn, nrb = (g.J + rows - 1) / rows;
     const int nb = sweep3_blocks(g, rows, kc);
     switch (rows) {
@@ -701,8 +717,13 @@ int launch3_sweep(hipStream_t s, const G3& g, const double* src, double* dst, co
                            idz2, factor, nstr, nrb, kc, partials, st);
         break;
     }
-    hipLaunchKernelGGL(k3_finish, dim3(1), dim3(1024), 0, s, partials, nb, 1, st, cells);
+    hipLaunchKernelGGL(k3_finish, dim3(1), dim3(1024), 0, s, partials, nb, 1, st, cells,
+                       sum_only ? 1 : 0);
     return nb;
+}
+
+void launch3_decide(hipStream_t s, DevState* st, double cells) {
+    hipLaunchKernelGGL(k3_decide, dim3(1), dim3(64), 0, s, st, cells);
 }
 
 void launch3_fg(hipStream_t s, const G3& g, const double* u, const double* v, const double* w,
@@ -742,6 +763,18 @@ void launch3_absmax(hipStream_t s, const double* u, const double* v, const doubl
     hipLaunchKernelGGL(k3_absmax3, dim3(absmax3_blocks()), dim3(256), 0, s, u, v, w, n,
                        partials);
     hipLaunchKernelGGL(k3_max_finish, dim3(1), dim3(256), 0, s, partials, absmax3_blocks(), out);
+}
+
+void launch3_interior_sum(hipStream_t s, const G3& g, const double* p, double* partials,
+                          double* sum) {
+    const dim3 grid = cells_grid(g, g.I);
+    hipLaunchKernelGGL(k3_sum_interior, grid, dim3(kBx, kBy), 0, s, g, p, partials);
+    hipLaunchKernelGGL(k3_sum_finish, dim3(1), dim3(1024), 0, s, partials,
+                       (int)(grid.x * grid.y * grid.z), sum);
+}
+
+void launch3_sub_mean(hipStream_t s, const G3& g, double* p, const double* sum, double cells) {
+    hipLaunchKernelGGL(k3_sub_mean, cells_grid(g, g.I), dim3(kBx, kBy), 0, s, g, p, sum, cells);
 }
 
 void launch3_normalize(hipStream_t s, const G3& g, double* p, double* partials, double* sum,

@@ -68,7 +68,8 @@ class Desc3(C.Structure):
                 ("itermax", C.c_int),
                 ("bcTop", C.c_int), ("bcBottom", C.c_int), ("bcLeft", C.c_int),
                 ("bcRight", C.c_int), ("bcFront", C.c_int), ("bcBack", C.c_int),
-                ("problem", C.c_int), ("device", C.c_int)]
+                ("problem", C.c_int), ("device", C.c_int), ("nranks", C.c_int),
+                ("rank", C.c_int), ("comm_id", C.c_void_p)]
 
 
 # every exported symbol of include/misor.h, with its ctypes signature
@@ -107,7 +108,11 @@ SIGNATURES = {
     "misor_enable_timing": (C.c_int, [C.c_void_p, C.c_int]),
     "misor_get_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
     "misor_reset_stats": (C.c_int, [C.c_void_p]),
+    "misor3_decompose": (C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int),
+                                   C.POINTER(C.c_int)]),
     "misor3_create": (C.c_int, [C.POINTER(C.c_void_p), C.POINTER(Desc3)]),
+    "misor3_local_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "misor3_gather": (C.c_int, [C.c_void_p, C.c_int, _dp]),
     "misor3_destroy": (None, [C.c_void_p]),
     "misor3_upload": (C.c_int, [C.c_void_p, C.c_int, _dp]),
     "misor3_download": (C.c_int, [C.c_void_p, C.c_int, _dp]),
@@ -314,11 +319,19 @@ class Grid:
 _PROBLEMS = {"dcavity": PROBLEM_DCAVITY, "canal": PROBLEM_CANAL}
 
 
-class Grid3:
-    """The 3D solver (assignment-6/src/solver.c) on one GPU: fields of shape
-    (kmax+2, jmax+2, imax+2), A(i,j,k) = a[k, j, i] (solver.c:19-34)."""
+def decompose3(nranks, rank, kmax):
+    """(kloc, koff) of rank's slab"""
+    a, b = C.c_int(0), C.c_int(0)
+    _check(lib().misor3_decompose(nranks, rank, kmax, C.byref(a), C.byref(b)))
+    return a.value, b.value
 
-    def __init__(self, prm: dict, device=-1):
+
+class Grid3:
+    """The 3D solver (assignment-6/src/solver.c): fields of shape
+    (kloc+2, jmax+2, imax+2), A(i,j,k) = a[k, j, i] (solver.c:19-34); kloc =
+    kmax on one GPU, the rank's slab when decomposed (nranks > 1)."""
+
+    def __init__(self, prm: dict, device=-1, nranks=1, rank=0, comm_id: bytes | None = None):
         d = Desc3()
         d.imax, d.jmax, d.kmax = int(prm["imax"]), int(prm["jmax"]), int(prm["kmax"])
         d.xlength, d.ylength, d.zlength = prm["xlength"], prm["ylength"], prm["zlength"]
@@ -329,10 +342,18 @@ class Grid3:
             setattr(d, k, int(prm[k]))
         d.problem = _PROBLEMS.get(prm.get("name") or "", PROBLEM_NONE)
         d.device = device
+        d.nranks, d.rank = nranks, rank
+        self._id = C.create_string_buffer(comm_id, COMM_ID_BYTES) if comm_id else None
+        d.comm_id = C.cast(self._id, C.c_void_p) if self._id is not None else None
         self.h = C.c_void_p()
         _check(lib().misor3_create(C.byref(self.h), C.byref(d)))
         self.desc = d
-        self.shape = (d.kmax + 2, d.jmax + 2, d.imax + 2)
+        a, b = C.c_int(0), C.c_int(0)
+        _check(lib().misor3_local_info(self.h, C.byref(a), C.byref(b)))
+        self.kloc, self.koff = a.value, b.value
+        self.rank, self.nranks = rank, nranks
+        self.shape = (self.kloc + 2, d.jmax + 2, d.imax + 2)
+        self.global_shape = (d.kmax + 2, d.jmax + 2, d.imax + 2)
 
     def close(self):
         if self.h:
@@ -363,6 +384,15 @@ class Grid3:
 
     def fill(self, field, value):
         _check(lib().misor3_fill(self.h, field, value))
+
+    def gather(self, field):
+        """the global field on rank 0, None elsewhere (collective)"""
+        if self.rank == 0:
+            out = np.empty(self.global_shape)
+            _check(lib().misor3_gather(self.h, field, _ptr(out)))
+            return out
+        _check(lib().misor3_gather(self.h, field, C.cast(None, _dp)))
+        return None
 
     def set_dt(self, dt):
         _check(lib().misor3_set_dt(self.h, dt))

@@ -89,3 +89,18 @@ def test_create3_rejects_bad_descriptors():
                bcTop=1, bcBottom=1, bcLeft=1, bcRight=1, bcFront=1, bcBack=1, name="dcavity")
     with pytest.raises(M.MisorError):
         M.Grid3(prm)
+
+
+@pytest.mark.parametrize("n,kmax", [(1, 2), (2, 128), (3, 29), (8, 128), (8, 16)])
+def test_decompose3_slabs(n, kmax):
+    """slabs along k, sizeOfRank rule; every plane owned once"""
+    off = 0
+    for r in range(n):
+        kl, ko = M.decompose3(n, r, kmax)
+        assert ko == off and kl == kmax // n + (kmax % n > r) and kl >= 2
+        off += kl
+    assert off == kmax
+    with pytest.raises(M.MisorError):
+        M.decompose3(9, 0, 17)  # fewer than 2 planes per rank
+    with pytest.raises(M.MisorError):
+        M.decompose3(2, 2, 64)

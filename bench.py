@@ -269,15 +269,20 @@ def cpu_baseline3d(n, iters=100):
 
 
 def run_ns3d(args, world, rank, local_rank, dist, torch):
-    """assignment-6's 3D NS (dcavity.par, --size^3 cells) on one GPU per rank:
-    the 3D path is not decomposed, so N ranks run N independent replicas
-    (replicas only).  A step is one time step of
-    assignment-6/src/main.c:45-60."""
+    """assignment-6's 3D NS (dcavity.par) weak scaling: --size^3 cells per GPU,
+    the global box size x size x (size*N) split into N slabs of planes (RCCL
+    halos and residual all-reduce).  A step is one time step of
+    assignment-6/src/main.c:45-60 over the whole box."""
     import pymisor as M
 
     n = args.size
-    prm = dict(DCAVITY3D, imax=n, jmax=n, kmax=n, itermax=args.itermax or 1000)
-    g = M.Grid3(prm, device=local_rank)
+    prm = dict(DCAVITY3D, imax=n, jmax=n, kmax=n * world, itermax=args.itermax or 1000)
+    comm_id = None
+    if world > 1:
+        obj = [M.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        comm_id = obj[0]
+    g = M.Grid3(prm, device=local_rank, nranks=world, rank=rank, comm_id=comm_id)
     for f, v in ((M.U3, prm["u_init"]), (M.V3, prm["v_init"]), (M.W3, prm["w_init"]),
                  (M.P3, prm["p_init"])):
         g.fill(f, v)
@@ -310,15 +315,11 @@ def run_ns3d(args, world, rank, local_rank, dist, torch):
     elapsed = time.perf_counter() - t0
     solve_ms, solve_iters = g.solve_time()
     if dist is not None:
-        tt = torch.tensor([elapsed, float(iters)], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = tt.tolist()[0]
-        it_all = torch.tensor([float(iters)], dtype=torch.float64, device="cuda")
-        dist.all_reduce(it_all, op=dist.ReduceOp.SUM)
-        iters_all = it_all.item()
-    else:
-        iters_all = iters
-    cells = float(n) ** 3
+    cells = float(n) ** 3  # per GPU
+    iters_all = iters * world  # every rank runs the same iterations over its slab
     out = {
         "metric": "3D dcavity NS (assignment-6): pressure-solve MLUP/s within full time steps",
         "value": round(cells * iters_all / elapsed / 1e6, 1),
@@ -333,8 +334,10 @@ def run_ns3d(args, world, rank, local_rank, dist, torch):
         "dtype": "f64",
         "data": "synthetic (dcavity initial state u = v = w = p = 0, generated on device)",
         "config": {"workload": "3D NS lid-driven cavity (assignment-6 dcavity.par), %d^3 "
-                               "cells per GPU (replicas), 1 time step = 1 step" % n,
-                   "imax": n, "jmax": n, "kmax": n, "itermax": prm["itermax"]},
+                               "cells per GPU, %dx%dx%d global in %d slabs along k, "
+                               "1 time step = 1 step" % (n, n, n, n * world, world),
+                   "imax": n, "jmax": n, "kmax": n * world, "itermax": prm["itermax"],
+                   "decomposition": "%d slabs" % world},
         "pressure_iterations": iters,
     }
     if solve_ms > 0:

@@ -5,7 +5,9 @@
  * %.2fs" line, same <problem>.vtk output (ASCII, as the reference's
  * VtkOptions default; MISOR_VTK_FORMAT=binary selects the BINARY variant).
  * MISOR_ITERLOG=<file> additionally writes one line per time step:
- * "nt t dt iterations".  One GPU: the 3D path is not decomposed.
+ * "nt t dt iterations".  MISOR_RANKS=N (or a launcher's WORLD_SIZE/RANK,
+ * host/ranks.h) runs it decomposed into N slabs of planes like the
+ * reference's mpirun -np N; rank 0 prints and writes the collected result.
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -13,29 +15,23 @@
 
 #include "parameter.h"
 #include "progress.h"
+#include "ranks.h"
 #include "solver_ns3d.h"
 #include "util.h"
 #include "vtk_writer.h"
 
-int main(int argc, char** argv)
+static int rank_main(const RankCtx* rk, void* arg)
 {
+    Parameter p = *(Parameter*)arg;
+    const int root = rk->rank == 0;
     double timeStart, timeStop;
-    Parameter p;
     Solver s;
-
-    initParameter(&p);
-    if (argc != 2) {
-        printf("Usage: %s <configFile>\n", argv[0]);
-        exit(EXIT_SUCCESS);
-    }
-    readParameter(&p, argv[1]);
-    printParameter3D(&p);
     initSolver(&s, &p);
 #ifndef VERBOSE
-    initProgress(s.te);
+    if (root) initProgress(s.te);
 #endif
     const char* logname = getenv("MISOR_ITERLOG");
-    FILE* ilog = logname ? fopen(logname, "w") : NULL;
+    FILE* ilog = (root && logname) ? fopen(logname, "w") : NULL;
 
     double tau = s.tau;
     double te = s.te;
@@ -43,7 +39,7 @@ int main(int argc, char** argv)
     int nt = 0;
 
     timeStart = getTimeStamp();
-    while (t <= te) {
+    while (t <= te) { /* dt is all-reduced: every rank takes the same steps */
         if (tau > 0.0) computeTimestep(&s);
         setBoundaryConditions(&s);
         setSpecialBoundaryCondition(&s);
@@ -55,37 +51,57 @@ int main(int argc, char** argv)
         t += s.dt;
         nt++;
 #ifdef VERBOSE
-        printf("TIME %f , TIMESTEP %f\n", t, s.dt);
+        if (root) printf("TIME %f , TIMESTEP %f\n", t, s.dt);
 #else
-        printProgress(t);
+        if (root) printProgress(t);
 #endif
     }
     timeStop = getTimeStamp();
+    if (root) {
 #ifndef VERBOSE
-    stopProgress();
+        stopProgress();
 #endif
-    printf("Solution took %.2fs\n", timeStop - timeStart);
+        printf("Solution took %.2fs\n", timeStop - timeStart);
+    }
     if (ilog) fclose(ilog);
 
-    size_t bytesize = (size_t)s.grid.imax * s.grid.jmax * s.grid.kmax * sizeof(double);
-    double* pg = allocate(64, bytesize);
-    double* ug = allocate(64, bytesize);
-    double* vg = allocate(64, bytesize);
-    double* wg = allocate(64, bytesize);
+    double *pg = NULL, *ug = NULL, *vg = NULL, *wg = NULL;
+    if (root) {
+        size_t bytesize = (size_t)s.grid.imax * s.grid.jmax * s.grid.kmax * sizeof(double);
+        pg = allocate(64, bytesize);
+        ug = allocate(64, bytesize);
+        vg = allocate(64, bytesize);
+        wg = allocate(64, bytesize);
+    }
     collectResult(&s, pg, ug, vg, wg);
-
-    const char* fmt = getenv("MISOR_VTK_FORMAT");
-    VtkOptions opts = { .grid = s.grid };
-    if (fmt && strcmp(fmt, "binary") == 0) opts.fmt = BINARY;
-    vtkOpen(&opts, s.problem);
-    vtkScalar(&opts, "pressure", pg);
-    vtkVector(&opts, "velocity", (VtkVector){ ug, vg, wg });
-    vtkClose(&opts);
-
-    free(pg);
-    free(ug);
-    free(vg);
-    free(wg);
+    if (root) {
+        const char* fmt = getenv("MISOR_VTK_FORMAT");
+        VtkOptions opts = { .grid = s.grid };
+        if (fmt && strcmp(fmt, "binary") == 0) opts.fmt = BINARY;
+        vtkOpen(&opts, s.problem);
+        vtkScalar(&opts, "pressure", pg);
+        vtkVector(&opts, "velocity", (VtkVector){ ug, vg, wg });
+        vtkClose(&opts);
+        free(pg);
+        free(ug);
+        free(vg);
+        free(wg);
+    }
     freeSolver(&s);
-    return EXIT_SUCCESS;
+    return 0;
+}
+
+int main(int argc, char** argv)
+{
+    Parameter p;
+    initParameter(&p);
+    if (argc != 2) {
+        printf("Usage: %s <configFile>\n", argv[0]);
+        exit(EXIT_SUCCESS);
+    }
+    readParameter(&p, argv[1]);
+    const char* r = getenv("RANK");
+    if (!r || atoi(r) == 0) printParameter3D(&p);
+    fflush(stdout);
+    return runRanks(rank_main, &p) ? EXIT_FAILURE : EXIT_SUCCESS;
 }

@@ -10,6 +10,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "ranks.h"
 #include "util.h"
 
 static int problemId(const char* name)
@@ -76,7 +77,14 @@ void initSolver(Solver* s, Parameter* params)
     d.bcFront = s->bcFront;
     d.bcBack = s->bcBack;
     d.problem = problemId(s->problem);
-    d.device = -1;
+    /* decomposed runs (host/ranks.h): slabs of planes, one rank per GPU */
+    const RankCtx* rk = currentRank();
+    d.device = rk->size > 1 ? rk->device : -1;
+    d.nranks = rk->size;
+    d.rank = rk->rank;
+    d.comm_id = rk->comm_id;
+    s->rank = rk->rank;
+    s->size = rk->size;
     misorCheck(misor3_create(&s->dev, &d), "initSolver");
     misorCheck(misor3_fill(s->dev, MISOR3_U, params->u_init), "initSolver");
     misorCheck(misor3_fill(s->dev, MISOR3_V, params->v_init), "initSolver");
@@ -95,7 +103,8 @@ void solve(Solver* s)
 {
     misorCheck(misor3_solve(s->dev, &s->lastIterations, &s->lastRes), "solve");
 #ifdef VERBOSE
-    printf("Solver took %d iterations to reach %f\n", s->lastIterations, sqrt(s->lastRes));
+    if (s->rank == 0)
+        printf("Solver took %d iterations to reach %f\n", s->lastIterations, sqrt(s->lastRes));
 #endif
 }
 
@@ -126,15 +135,20 @@ void adaptUV(Solver* s) { misorCheck(misor3_adapt_uvw(s->dev), "adaptUV"); }
 void collectResult(Solver* s, double* pg, double* ug, double* vg, double* wg)
 {
     const int imax = s->grid.imax, jmax = s->grid.jmax, kmax = s->grid.kmax;
+    const int root = s->rank == 0;
     const size_t n = (size_t)(imax + 2) * (jmax + 2) * (kmax + 2);
-    double* p = allocate(64, n * sizeof(double));
-    double* u = allocate(64, n * sizeof(double));
-    double* v = allocate(64, n * sizeof(double));
-    double* w = allocate(64, n * sizeof(double));
-    misorCheck(misor3_download(s->dev, MISOR3_P, p), "collectResult");
-    misorCheck(misor3_download(s->dev, MISOR3_U, u), "collectResult");
-    misorCheck(misor3_download(s->dev, MISOR3_V, v), "collectResult");
-    misorCheck(misor3_download(s->dev, MISOR3_W, w), "collectResult");
+    double *p = NULL, *u = NULL, *v = NULL, *w = NULL;
+    if (root) {
+        p = allocate(64, n * sizeof(double));
+        u = allocate(64, n * sizeof(double));
+        v = allocate(64, n * sizeof(double));
+        w = allocate(64, n * sizeof(double));
+    }
+    misorCheck(misor3_gather(s->dev, MISOR3_P, p), "collectResult");
+    misorCheck(misor3_gather(s->dev, MISOR3_U, u), "collectResult");
+    misorCheck(misor3_gather(s->dev, MISOR3_V, v), "collectResult");
+    misorCheck(misor3_gather(s->dev, MISOR3_W, w), "collectResult");
+    if (!root) return;
 #define L(a, i, j, k) (a)[((size_t)(k) * (jmax + 2) + (size_t)(j)) * (imax + 2) + (size_t)(i)]
     size_t q = 0;
     for (int k = 1; k <= kmax; k++)

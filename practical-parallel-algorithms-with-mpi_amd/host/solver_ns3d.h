@@ -31,6 +31,7 @@ typedef struct {
     misor_grid3* dev;   /* device-resident state (added) */
     int lastIterations; /* iterations of the last pressure solve (added) */
     double lastRes;     /* its final residual (added) */
+    int rank, size;     /* this rank of a decomposed run (added; 0 of 1 on one GPU) */
 } Solver;
 
 extern void initSolver(Solver*, Parameter*);
@@ -42,8 +43,9 @@ extern void setBoundaryConditions(Solver*);
 extern void setSpecialBoundaryCondition(Solver*);
 extern void computeFG(Solver*);
 extern void adaptUV(Solver*);
-/* commCollectResult's single-domain branch (assignment-6/src/comm.c:386-426):
- * interior p and cell-centred u, v, w, imax*jmax*kmax each, i fastest */
+/* commCollectResult (assignment-6/src/comm.c:246-426): interior p and
+ * cell-centred u, v, w of the whole domain, imax*jmax*kmax each, i fastest,
+ * on rank 0 (collective; the other ranks pass NULLs) */
 extern void collectResult(Solver*, double* pg, double* ug, double* vg, double* wg);
 extern void freeSolver(Solver*);
 #endif

@@ -97,3 +97,18 @@ def test_exe_ns3d_binary_vtk(golden, tmp_path):
     assert np.array_equal(vel[:, 0], ug) and np.array_equal(vel[:, 1], vg)
     assert np.array_equal(vel[:, 2], wg)
     assert raw[off + 24 * npts:] == b"\n"
+
+
+@pytest.mark.parametrize("ranks", [2, 3, 4])
+def test_exe_ns3d_decomposed(golden, tmp_path, ranks):
+    """MISOR_RANKS=N: N slabs (threads, in-process transport), result collected on
+    rank 0 -- the same iteration log and the same .vtk bytes as the oracle's run"""
+    par = write_par(golden, tmp_path, "a6_dcavity.par", imax=24, jmax=20, kmax=16, te=0.3)
+    prm = orc3.read_par3(str(par))
+    ns = orc3.NS3(prm)
+    n, iters, _ = ns.run()
+    out = run_exe(par, tmp_path, MISOR_RANKS=str(ranks))
+    assert out.count("Parameters for dcavity") == 1 and out.count("Solution took") == 1
+    log = np.loadtxt(tmp_path / "iters.log", ndmin=2)
+    assert len(log) == n and np.array_equal(log[:, 3].astype(int), iters)
+    assert (tmp_path / "dcavity.vtk").read_text() == vtk_ascii(prm, *ns.collect())

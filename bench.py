@@ -56,35 +56,36 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(n=8192, sweeps=40):
-    """Reference solveRB on 1 core, bounded sample; returns the JSON object."""
-    import ctypes as C
-
+def cpu_baseline(n=8192, sweeps=40, reps=3):
+    """Reference solveRB on 1 core, bounded sample, best of `reps` (median
+    reported beside it); returns the JSON object."""
     import numpy as np
     import orc
 
     kind = "reference" if orc.have_ref() else "port"
-    p = np.zeros((n + 2, n + 2))
-    rhs = np.zeros((n + 2, n + 2))
-    if kind == "reference":
-        R = orc.ref()
-        # refa4_run does init + solve; time init separately by a 0-sweep call
-        t0 = time.perf_counter()
-        R.refa4_run(n, n, 1.0, 1.0, 0, 1e-300, 1.9, 2, 1, None, None, None)
-        t1 = time.perf_counter()
-        it = R.refa4_run(n, n, 1.0, 1.0, sweeps, 1e-300, 1.9, 2, 1, None, None, None)
-        t2 = time.perf_counter()
-        solve_s = (t2 - t1) - (t1 - t0)
-    else:
-        p, rhs = orc.poisson_init(n, n)
-        t1 = time.perf_counter()
-        it, _ = orc.solve_rb(p, rhs, 1.0 / n, 1.0 / n, 1.9, 1e-300, sweeps)
-        solve_s = time.perf_counter() - t1
-    assert it == sweeps
-    mlups = n * n * sweeps / solve_s / 1e6
-    return {"value": round(mlups, 2), "unit": "MLUP/s", "cores": 1, "kind": kind,
-            "sample": "solveRB %dx%d, %d sweeps, %.2f s solve (init excluded), 1 host core"
-                      % (n, n, sweeps, solve_s)}
+    times = []
+    for _ in range(reps):
+        if kind == "reference":
+            R = orc.ref()
+            # refa4_run does init + solve; time init separately by a 0-sweep call
+            t0 = time.perf_counter()
+            R.refa4_run(n, n, 1.0, 1.0, 0, 1e-300, 1.9, 2, 1, None, None, None)
+            t1 = time.perf_counter()
+            it = R.refa4_run(n, n, 1.0, 1.0, sweeps, 1e-300, 1.9, 2, 1, None, None, None)
+            t2 = time.perf_counter()
+            times.append((t2 - t1) - (t1 - t0))
+        else:
+            p, rhs = orc.poisson_init(n, n)
+            t1 = time.perf_counter()
+            it, _ = orc.solve_rb(p, rhs, 1.0 / n, 1.0 / n, 1.9, 1e-300, sweeps)
+            times.append(time.perf_counter() - t1)
+        assert it == sweeps
+    best, med = min(times), float(np.median(times))
+    lup = float(n) * n * sweeps
+    return {"value": round(lup / best / 1e6, 2), "unit": "MLUP/s", "cores": 1, "kind": kind,
+            "median": round(lup / med / 1e6, 2), "cpu": cpu_model(),
+            "sample": "solveRB %dx%d, %d sweeps, best of %d (%.2f s solve, init excluded), "
+                      "1 host core" % (n, n, sweeps, reps, best)}
 
 
 def cpu_model():
@@ -97,24 +98,28 @@ def cpu_model():
     return None
 
 
-def cpu_baseline_multicore(n=16384, sweeps=40):
+def cpu_baseline_multicore(n=8192, sweeps=40, reps=3):
     """solveRB on all the host cores this job may use (no MPI on
     the box, so pthreads over row bands, oracle/oracle_mt.c -- the restatement,
-    p bit-identical to the single-core solve); bounded sample"""
-    import numpy as np  # noqa: F401
+    p bit-identical to the single-core solve); bounded sample, best of `reps`"""
+    import numpy as np
     import orc
 
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
-    p, rhs = orc.poisson_init(n, n)
-    t1 = time.perf_counter()
-    it, _ = orc.solve_rb_mt(p, rhs, 1.0 / n, 1.0 / n, 1.9, 1e-300, sweeps, threads)
-    solve_s = time.perf_counter() - t1
-    assert it == sweeps
-    return {"value": round(n * n * sweeps / solve_s / 1e6, 1), "unit": "MLUP/s",
-            "cores": threads, "kind": "port", "cpu": cpu_model(),
+    times = []
+    for _ in range(reps):
+        p, rhs = orc.poisson_init(n, n)
+        t1 = time.perf_counter()
+        it, _ = orc.solve_rb_mt(p, rhs, 1.0 / n, 1.0 / n, 1.9, 1e-300, sweeps, threads)
+        times.append(time.perf_counter() - t1)
+        assert it == sweeps
+    best, med = min(times), float(np.median(times))
+    lup = float(n) * n * sweeps
+    return {"value": round(lup / best / 1e6, 1), "unit": "MLUP/s", "cores": threads,
+            "kind": "port", "median": round(lup / med / 1e6, 1), "cpu": cpu_model(),
             "nproc": os.cpu_count(),
-            "sample": "solveRB %dx%d, %d sweeps, %.2f s solve, %d threads over row bands "
-                      "(oracle/oracle_mt.c)" % (n, n, sweeps, solve_s, threads)}
+            "sample": "solveRB %dx%d, %d sweeps, best of %d (%.2f s solve), %d threads over "
+                      "row bands (oracle/oracle_mt.c)" % (n, n, sweeps, reps, best, threads)}
 
 
 def pmc_traffic(size, nranks, T):

@@ -110,52 +110,84 @@ void launch_special_bc(const NsLaunch& L, double* u) {
 }
 
 // ---- computeFG, :360-436 (+ its F/G boundary lines :426-435 on wall ranks)
+//
+// Column march: a thread owns column i and walks up a band of kFgBand rows,
+// keeping rows j-1, j, j+1 of u and v (each at i-1, i, i+1) in registers, so
+// each row of u and v is loaded once per band (its x-neighbours hit in L1)
+// instead of once per stencil use; consecutive lanes are consecutive columns
+// (coalesced).  Per-cell arithmetic is the reference's, term by term.
+constexpr int kFgBand = 32;
+
+struct Uv3 {  // u and v at i-1, i, i+1 of one row
+    double um, uc, up, vm, vc, vp;
+};
+
+__device__ __forceinline__ Uv3 load_uv3(const CLay& u, const CLay& v, int i, int j) {
+    Uv3 r;
+    r.um = u(i - 1, j);
+    r.uc = u(i, j);
+    r.up = u(i + 1, j);
+    r.vm = v(i - 1, j);
+    r.vc = v(i, j);
+    r.vp = v(i + 1, j);
+    return r;
+}
+
 __global__ __launch_bounds__(kTx* kTy) void fg_kernel(CLay u, CLay v, Lay f, Lay g, int ni,
                                                       int nj, double dt, double inverseRe,
                                                       double inverseDx, double inverseDy,
                                                       double gamma, double gx, double gy,
                                                       int wl, int wr, int wb, int wt) {
     const int i = 1 + blockIdx.x * kTx + threadIdx.x;
-    const int j = 1 + blockIdx.y * kTy + threadIdx.y;
-    if (i > ni || j > nj) return;
+    const int j0 = 1 + (blockIdx.y * kTy + threadIdx.y) * kFgBand;
+    if (i > ni || j0 > nj) return;
+    const int j1 = min(nj, j0 + kFgBand - 1);
+    Uv3 S = load_uv3(u, v, i, j0 - 1), C = load_uv3(u, v, i, j0), N = load_uv3(u, v, i, j0 + 1);
+    for (int j = j0; j <= j1; ++j) {
+        Uv3 NN;
+        if (j + 2 <= nj + 1) NN = load_uv3(u, v, i, j + 2);  // next row, one step ahead
+        const double uc = C.uc, ue = C.up, uw = C.um;
+        const double un = N.uc, us = S.uc, unw = N.um;
+        const double vc = C.vc, ve = C.vp, vw = C.vm;
+        const double vn = N.vc, vs = S.vc, vse = S.vp;
 
-    const double uc = u(i, j), ue = u(i + 1, j), uw = u(i - 1, j);
-    const double un = u(i, j + 1), us = u(i, j - 1), unw = u(i - 1, j + 1);
-    const double vc = v(i, j), ve = v(i + 1, j), vw = v(i - 1, j);
-    const double vn = v(i, j + 1), vs = v(i, j - 1), vse = v(i + 1, j - 1);
+        const double du2dx = inverseDx * 0.25 * ((uc + ue) * (uc + ue) - (uc + uw) * (uc + uw)) +
+                             gamma * inverseDx * 0.25 *
+                                 (fabs(uc + ue) * (uc - ue) + fabs(uc + uw) * (uc - uw));
+        const double duvdy = inverseDy * 0.25 * ((vc + ve) * (uc + un) - (vs + vse) * (uc + us)) +
+                             gamma * inverseDy * 0.25 *
+                                 (fabs(vc + ve) * (uc - un) + fabs(vs + vse) * (uc - us));
+        const double du2dx2 = inverseDx * inverseDx * (ue - 2.0 * uc + uw);
+        const double du2dy2 = inverseDy * inverseDy * (un - 2.0 * uc + us);
+        double fv = uc + dt * (inverseRe * (du2dx2 + du2dy2) - du2dx - duvdy + gx);
 
-    const double du2dx = inverseDx * 0.25 * ((uc + ue) * (uc + ue) - (uc + uw) * (uc + uw)) +
-                         gamma * inverseDx * 0.25 *
-                             (fabs(uc + ue) * (uc - ue) + fabs(uc + uw) * (uc - uw));
-    const double duvdy = inverseDy * 0.25 * ((vc + ve) * (uc + un) - (vs + vse) * (uc + us)) +
-                         gamma * inverseDy * 0.25 *
-                             (fabs(vc + ve) * (uc - un) + fabs(vs + vse) * (uc - us));
-    const double du2dx2 = inverseDx * inverseDx * (ue - 2.0 * uc + uw);
-    const double du2dy2 = inverseDy * inverseDy * (un - 2.0 * uc + us);
-    double fv = uc + dt * (inverseRe * (du2dx2 + du2dy2) - du2dx - duvdy + gx);
+        const double duvdx = inverseDx * 0.25 * ((uc + un) * (vc + ve) - (uw + unw) * (vc + vw)) +
+                             gamma * inverseDx * 0.25 *
+                                 (fabs(uc + un) * (vc - ve) + fabs(uw + unw) * (vc - vw));
+        const double dv2dy = inverseDy * 0.25 * ((vc + vn) * (vc + vn) - (vc + vs) * (vc + vs)) +
+                             gamma * inverseDy * 0.25 *
+                                 (fabs(vc + vn) * (vc - vn) + fabs(vc + vs) * (vc - vs));
+        const double dv2dx2 = inverseDx * inverseDx * (ve - 2.0 * vc + vw);
+        const double dv2dy2 = inverseDy * inverseDy * (vn - 2.0 * vc + vs);
+        double gv = vc + dt * (inverseRe * (dv2dx2 + dv2dy2) - duvdx - dv2dy + gy);
 
-    const double duvdx = inverseDx * 0.25 * ((uc + un) * (vc + ve) - (uw + unw) * (vc + vw)) +
-                         gamma * inverseDx * 0.25 *
-                             (fabs(uc + un) * (vc - ve) + fabs(uw + unw) * (vc - vw));
-    const double dv2dy = inverseDy * 0.25 * ((vc + vn) * (vc + vn) - (vc + vs) * (vc + vs)) +
-                         gamma * inverseDy * 0.25 *
-                             (fabs(vc + vn) * (vc - vn) + fabs(vc + vs) * (vc - vs));
-    const double dv2dx2 = inverseDx * inverseDx * (ve - 2.0 * vc + vw);
-    const double dv2dy2 = inverseDy * inverseDy * (vn - 2.0 * vc + vs);
-    double gv = vc + dt * (inverseRe * (dv2dx2 + dv2dy2) - duvdx - dv2dy + gy);
-
-    // boundary of F / G (:426-435) overrides the interior value at i = imax / j = jmax
-    if (wr && i == ni) fv = uc;
-    if (wt && j == nj) gv = vc;
-    f(i, j) = fv;
-    g(i, j) = gv;
-    if (wl && i == 1) f(0, j) = uw;
-    if (wb && j == 1) g(i, 0) = vs;
+        // boundary of F / G (:426-435) overrides the interior value at i = imax / j = jmax
+        if (wr && i == ni) fv = uc;
+        if (wt && j == nj) gv = vc;
+        f(i, j) = fv;
+        g(i, j) = gv;
+        if (wl && i == 1) f(0, j) = uw;
+        if (wb && j == 1) g(i, 0) = vs;
+        S = C;
+        C = N;
+        N = NN;
+    }
 }
 
 void launch_compute_fg(const NsLaunch& L, const double* u, const double* v, double* f,
                        double* g) {
-    dim3 grid((L.ni + kTx - 1) / kTx, (L.nj + kTy - 1) / kTy);
+    const int bands = (L.nj + kFgBand - 1) / kFgBand;
+    dim3 grid((L.ni + kTx - 1) / kTx, (bands + kTy - 1) / kTy);
     const NsParams& P = L.prm;
     hipLaunchKernelGGL(fg_kernel, grid, dim3(kTx, kTy), 0, L.s, CLay{u, L.pitch},
                        CLay{v, L.pitch}, Lay{f, L.pitch}, Lay{g, L.pitch}, L.ni, L.nj, P.dt,
@@ -243,13 +275,15 @@ __global__ __launch_bounds__(kRedThreads) void absmax2_kernel(CLay u, CLay v, Re
                                                               double* partials) {
     __shared__ double su[kRedThreads / 64], sv[kRedThreads / 64];
     double mu = 2.2250738585072014e-308, mv = 2.2250738585072014e-308;  // DBL_MIN
-    const long long n = (long long)R.w * R.h;
-    for (long long k = (long long)blockIdx.x * kRedThreads + threadIdx.x; k < n;
-         k += (long long)gridDim.x * kRedThreads) {
-        const int i = R.ilo + (int)(k % R.w), j = R.jlo + (int)(k / R.w);
-        const double a = fabs(u(i, j)), b = fabs(v(i, j));
-        mu = (mu > a) ? mu : a;
-        mv = (mv > b) ? mv : b;
+    // rows over blocks, columns over threads (coalesced; max is order-free)
+    for (int jj = blockIdx.x; jj < R.h; jj += gridDim.x) {
+        const int j = R.jlo + jj;
+        for (int ii = threadIdx.x; ii < R.w; ii += kRedThreads) {
+            const int i = R.ilo + ii;
+            const double a = fabs(u(i, j)), b = fabs(v(i, j));
+            mu = (mu > a) ? mu : a;
+            mv = (mv > b) ? mv : b;
+        }
     }
     mu = wmax(mu);
     mv = wmax(mv);

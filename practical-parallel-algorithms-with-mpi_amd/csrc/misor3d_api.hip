@@ -61,6 +61,8 @@ int fail3(int code, const char* fmt, ...) {
     } while (0)
 
 constexpr int kHalo = 2;          // halo planes per side in storage
+constexpr int kSlack = 2;         // spare doubles before / after every buffer: the sweep's
+                                  // 16-byte column-pair loads reach one past a row end
 constexpr int kBufs = 9;          // the 8 fields + the ping-pong partner of P
 constexpr int kAlt = 8;
 constexpr char kLocalPrefix3[] = "LOCAL:";
@@ -78,7 +80,8 @@ struct misor_grid3 {
     G3 g{};                    // this rank's slab: g.K planes, g.koff, physical flags
     long long n = 0;           // cells of the reference's local array (planes 0 .. K+1)
     long long nalloc = 0;      // cells allocated per field (planes -1 .. K+2)
-    double* mem[kBufs] = {};   // allocations
+    double* alloc[kBufs] = {}; // allocations: nalloc + 2*kSlack doubles
+    double* mem[kBufs] = {};   // plane -1 of each buffer (alloc + kSlack)
     double* fld[kBufs] = {};   // plane-0 origins: MISOR3_P .. MISOR3_H, kAlt = P's partner
     bool alt_stale = true;     // the partner's edge/corner ghosts may differ from P's
     int sweep = 1;             // MISOR3_TUNE_SWEEP
@@ -210,7 +213,7 @@ void misor3_destroy(misor_grid3* g) {
     if (!g) return;
     (void)hipSetDevice(g->device);
     if (g->stream) (void)hipStreamSynchronize(g->stream);
-    for (auto& f : g->mem)
+    for (auto& f : g->alloc)
         if (f) (void)hipFree(f);
     (void)hipFree(g->partials);
     (void)hipFree(g->out);
@@ -293,11 +296,12 @@ int misor3_create(misor_grid3** out, const misor3_desc* d) {
         g->dt_bound = 0.5 * d->re * 1.0 / inv;  // solver.c:136-139
     }
     for (int b = 0; b < kBufs; ++b) {
-        if (hipMalloc(&g->mem[b], sizeof(double) * (size_t)g->nalloc) != hipSuccess)
+        const size_t bytes = sizeof(double) * (size_t)(g->nalloc + 2 * kSlack);
+        if (hipMalloc(&g->alloc[b], bytes) != hipSuccess)
             CF(MISOR_ENOMEM, "hipMalloc of %lld doubles failed", g->nalloc);
-        if (hipMemsetAsync(g->mem[b], 0, sizeof(double) * (size_t)g->nalloc, g->stream) !=
-            hipSuccess)
+        if (hipMemsetAsync(g->alloc[b], 0, bytes, g->stream) != hipSuccess)
             CF(MISOR_EHIP, "hipMemset failed");
+        g->mem[b] = g->alloc[b] + kSlack;
         g->fld[b] = g->mem[b] + (long long)(kHalo - 1) * g->g.sxy;
     }
     g->partials_cap = 2LL * ns3_partials(g->g);
@@ -683,6 +687,7 @@ int misor3_solve(misor_grid3* g, int* iters, double* res) {
     if (fused && (g->st_host->it & 1)) {
         std::swap(g->fld[MISOR3_P], g->fld[kAlt]);
         std::swap(g->mem[MISOR3_P], g->mem[kAlt]);
+        std::swap(g->alloc[MISOR3_P], g->alloc[kAlt]);
     }
     if (g->timing) {
         float ms = 0.f;

@@ -180,18 +180,25 @@ __global__ void k3_decide(DevState* st, double cells) {
 //   stored split by parity (even columns, then odd ones), so the cells of one
 //   colour -- and each of their x-neighbours -- are 64 consecutive doubles:
 //   every LDS access of a wave is contiguous.
-// * Software pipeline: step k issues the loads of plane k+3 and of the rhs
-//   of step k+1, and writes plane k+2 (issued one step earlier) to LDS at
-//   its end; the k loop is unrolled by two so the register sets alternate
-//   with compile-time indices.  Loads are unconditional (addresses clamped
-//   into the array), so the compiler waits for each with a counted vmcnt.
-// * Everything per-thread that does not change along k (cell columns, LDS
-//   positions, in-plane offsets, validity and boundary flags, for the two
-//   parities of k) is computed once; a step adds scalar plane offsets.
-// * New values go straight from registers to dst; the Neumann face copy is
-//   fused as in k3_rb_pass.  Per-cell arithmetic is the reference's, term by
-//   term; the residual of the owned cells is summed per workgroup in a fixed
-//   order.
+// * Loads: lane l reads the column pair (2l, 2l+1) of a row with one 16-byte
+//   load (the fields carry one spare double at each end of the allocation,
+//   so the pair of the first strip's column -1 stays inside it).  p rows go
+//   to LDS, split by parity.  rhs rows are read once for both colours: the
+//   pair of row t of plane k arrives during step k-1; step k uses its red
+//   element and keeps the black one for step k+1.  Red and black cells of a
+//   row are handled by the same lane, so nothing is exchanged.
+// * Software pipeline: step k issues the loads of plane k+3 and the rhs pairs
+//   of plane k+1, and writes plane k+2 (issued one step earlier) to LDS at its
+//   end; the k loop is unrolled by two so the register sets alternate with
+//   compile-time indices.  Loads are unconditional (addresses clamped into the
+//   array), so the compiler waits for each with a counted vmcnt.
+// * Everything per-thread that does not change along k (LDS positions,
+//   in-plane offsets, validity and boundary flags, for the two parities of k)
+//   is computed once; a step adds scalar plane offsets.
+// * Finished planes go from LDS to dst in whole rows (one write per 128-B
+//   line) with the Neumann face mirrors of k3_rb_pass.  Per-cell arithmetic
+//   is the reference's, term by term; the residual of the owned cells is
+//   summed per workgroup in a fixed order.
 constexpr int kSwCols = 128;           // loaded columns per strip
 constexpr int kSwOwn = kSwCols - 4;    // owned columns per strip
 constexpr int kSwSlots = 5;
@@ -203,28 +210,34 @@ namespace {
 struct SwCell {
     int lds;    // row offset + position of the cell in the split row
     int nb;     // row offset + position of its left x-neighbour (right = nb + 1)
-    int go;     // j*sx + i (clamped into the plane when the cell is not valid)
-    int flags;  // 1 valid, 2 owned, 4 i==1, 8 i==I, 16 j==1, 32 j==J
+    int sel;    // which element of the lane's column pair the cell is (0 / 1)
+    int flags;  // 1 red valid, 2 red owned, 4 black valid (owned)
 };
 
-// red (colour offset 1: i+j+k odd) or black (0) cell of LDS row t for planes
-// of parity q
-__device__ __forceinline__ SwCell sw_cell(const G3& g, int c_ld, int j_ld, int t, int lane,
-                                          int q, int colour, bool need_own_cols, int R) {
+// the red cell (i+j+k odd) of LDS row t for planes of parity q, and whether
+// this lane's black cell of the same row is owned
+__device__ __forceinline__ SwCell sw_cell(const G3& g, int c_ld, int j_ld, int t, int lane, int q,
+                                          int R) {
     const int j = j_ld + t;
-    const int sel = ((c_ld + j + q) & 1) ^ colour;  // parity of the cell's LDS column
+    const int sel = ((c_ld + j + q) & 1) ^ 1;  // LDS column parity of the red cell
     const int x = 2 * lane + sel, i = c_ld + x;
+    const int xb = 2 * lane + (sel ^ 1), ib = c_ld + xb;  // the black cell of the pair
     SwCell c;
     c.lds = t * kSwRow + sel * kSwOdd + lane;
     c.nb = t * kSwRow + (1 - sel) * kSwOdd + lane + sel - 1;
-    const bool inside = i >= 1 && i <= g.I && j >= 1 && j <= g.J;
-    const bool owned = inside && t >= 2 && t <= R + 1 && x >= 2 && x <= kSwCols - 3;
-    const bool valid = need_own_cols ? owned : (inside && x >= 1 && x <= kSwCols - 2);
-    c.go = valid ? j * (int)g.sx + i : 0;
-    c.flags = (valid ? 1 : 0) | (owned ? 2 : 0) | (i == 1 ? 4 : 0) | (i == g.I ? 8 : 0) |
-              (j == 1 ? 16 : 0) | (j == g.J ? 32 : 0);
+    c.sel = sel;
+    const bool row_in = j >= 1 && j <= g.J && t <= R + 2;
+    const bool red_valid = row_in && i >= 1 && i <= g.I && x >= 1 && x <= kSwCols - 2;
+    const bool red_owned = red_valid && t >= 2 && t <= R + 1 && x >= 2 && x <= kSwCols - 3;
+    const bool blk_owned = row_in && t >= 2 && t <= R + 1 && ib >= 1 && ib <= g.I && xb >= 2 &&
+                           xb <= kSwCols - 3;
+    c.flags = (red_valid ? 1 : 0) | (red_owned ? 2 : 0) | (blk_owned ? 4 : 0);
     return c;
 }
+
+struct alignas(8) D2 {
+    double v[2];
+};
 }  // namespace
 
 template <int R>
@@ -238,8 +251,7 @@ __global__ __launch_bounds__(256) void k3_sweep(G3 g, const double* __restrict__
     constexpr int NR = R + 4;  // rows per plane in LDS
     static_assert(R % 4 == 0, "R must be a multiple of 4");
     constexpr int LR = NR / 4;           // rows each wave loads
-    constexpr int RR = (R + 2 + 3) / 4;  // red rows per wave (LDS rows 1..R+2)
-    constexpr int BR = R / 4;            // black rows per wave (LDS rows 2..R+1)
+    constexpr int RR = (R + 2 + 3) / 4;  // update rows per wave (LDS rows 1..R+2)
     constexpr int PL = NR * kSwRow;      // doubles per LDS plane
     __shared__ double L[kSwSlots * PL];
     __shared__ double sh[4];
@@ -264,36 +276,31 @@ __global__ __launch_bounds__(256) void k3_sweep(G3 g, const double* __restrict__
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const long long sxy = g.sxy;
     const int sx = (int)g.sx;
+    // the pair of lane l starts at column c_ld + 2l: >= -1 and, clamped, <=
+    // I+1, so it reaches at most one double before / after a row -- inside the
+    // allocation, which has a spare double at each end; lanes past the last
+    // column re-read the last pair (their LDS columns are never used)
+    const int pc = min(c_ld + 2 * lane, g.I + 1);
 
-    // loads: in-plane offsets (clamped) and LDS positions (parity split)
-    int lo[LR][2], ls[LR][2];
+    // p loads: in-plane offsets (rows clamped) and LDS positions (parity split)
+    int lo[LR], ls[LR];
 #pragma unroll
     for (int m = 0; m < LR; ++m) {
         const int t = w + 4 * m;
-        const int j = min(max(j_ld + t, 0), g.J + 1);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int x = lane + 64 * h;
-            lo[m][h] = j * sx + min(max(c_ld + x, 0), g.I + 1);
-            ls[m][h] = t * kSwRow + (x & 1) * kSwOdd + (x >> 1);
-        }
+        lo[m] = min(max(j_ld + t, 0), g.J + 1) * sx + pc;
+        ls[m] = t * kSwRow + lane;  // even column 2l at lane, odd 2l+1 at kSwOdd + lane
     }
-    // cells for the two parities of k: A = parity of the first step (k0-1)
+    // update rows t = 1 + w + 4m: rhs pair offsets and the cells for the two
+    // parities of k (A = parity of the first step, k0-1)
     const int qa = (k0 - 1 + g.koff) & 1;  // colours are global: i + j + (koff + k)
-    SwCell redA[RR], redB[RR], blkA[BR], blkB[BR];
+    int ro[RR];
+    SwCell cA[RR], cB[RR];
 #pragma unroll
     for (int m = 0; m < RR; ++m) {
         const int t = 1 + w + 4 * m;
-        redA[m] = sw_cell(g, c_ld, j_ld, t, lane, qa, 1, false, R);
-        redB[m] = sw_cell(g, c_ld, j_ld, t, lane, qa ^ 1, 1, false, R);
-        if (t > R + 2) redA[m].flags = redB[m].flags = 0;
-    }
-#pragma unroll
-    for (int m = 0; m < BR; ++m) {
-        const int t = 2 + w + 4 * m;
-        // the black cells of step k are in plane k-1: parity q ^ 1
-        blkA[m] = sw_cell(g, c_ld, j_ld, t, lane, qa ^ 1, 0, true, R);
-        blkB[m] = sw_cell(g, c_ld, j_ld, t, lane, qa, 0, true, R);
+        ro[m] = min(max(j_ld + t, 0), g.J + 1) * sx + pc;
+        cA[m] = sw_cell(g, c_ld, j_ld, t, lane, qa, R);
+        cB[m] = sw_cell(g, c_ld, j_ld, t, lane, qa ^ 1, R);
     }
 
     auto slot = [](int kk) { return (kk + kSwSlots) % kSwSlots; };
@@ -301,44 +308,28 @@ __global__ __launch_bounds__(256) void k3_sweep(G3 g, const double* __restrict__
     auto plane = [&](int kk) { return (long long)min(max(kk, -1), g.K + 2) * sxy; };
     // red is computed on halo planes too where a neighbour rank owns them
     const int kr_lo = g.lo_phys ? 1 : 0, kr_hi = g.hi_phys ? g.K : g.K + 1;
-    auto load_plane = [&](int kk, double (&v)[LR][2]) {
+    auto load_plane = [&](int kk, D2 (&v)[LR]) {
         const double* sp = src + plane(kk);
 #pragma unroll
-        for (int m = 0; m < LR; ++m)
-#pragma unroll
-            for (int h = 0; h < 2; ++h) v[m][h] = sp[lo[m][h]];
+        for (int m = 0; m < LR; ++m) v[m] = *reinterpret_cast<const D2*>(sp + lo[m]);
     };
-    auto store_plane = [&](int kk, const double (&v)[LR][2]) {
+    auto store_plane = [&](int kk, const D2 (&v)[LR]) {
         double* Ls = L + slot(kk) * PL;
 #pragma unroll
-        for (int m = 0; m < LR; ++m)
-#pragma unroll
-            for (int h = 0; h < 2; ++h) Ls[ls[m][h]] = v[m][h];
+        for (int m = 0; m < LR; ++m) {
+            Ls[ls[m]] = v[m].v[0];
+            Ls[ls[m] + kSwOdd] = v[m].v[1];
+        }
     };
-    // the rhs of step k: red cells of plane k, black cells of plane k-1
-    auto load_rhs = [&](int k, const SwCell (&rc)[RR], const SwCell (&bc)[BR], double (&rr)[RR],
-                        double (&rbk)[BR]) {
-        const double* rp = rhs + plane(k);
-        const double* bp = rhs + plane(k - 1);
+    auto load_rhs = [&](int kk, D2 (&v)[RR]) {
+        const double* rp = rhs + plane(kk);
 #pragma unroll
-        for (int m = 0; m < RR; ++m) rr[m] = rp[rc[m].go];
-#pragma unroll
-        for (int m = 0; m < BR; ++m) rbk[m] = bp[bc[m].go];
-    };
-    double acc = 0.0;
-    // one update: the reference's arithmetic on LDS neighbours; returns the new value
-    auto update = [&](const double* Lc, const double* Lm, const double* Lp, const SwCell& c,
-                      double rh, double& r) {
-        const double cc = Lc[c.lds];
-        const double tx = (Lc[c.nb + 1] - 2.0 * cc) + Lc[c.nb];
-        const double ty = (Lc[c.lds + kSwRow] - 2.0 * cc) + Lc[c.lds - kSwRow];
-        const double tz = (Lp[c.lds] - 2.0 * cc) + Lm[c.lds];
-        r = rh - ((tx * idx2 + ty * idy2) + tz * idz2);
-        return cc - (factor * r);
+        for (int m = 0; m < RR; ++m) v[m] = *reinterpret_cast<const D2*>(rp + ro[m]);
     };
     // owned cells of a finished plane (both colours) from LDS to dst in whole
     // rows -- full 128-B lines, one write per line -- with the Neumann face
     // mirrors of the boundary cells (solver.c:237-278)
+    constexpr int BR = R / 4;
     int so[BR][2], sl[BR][2], sf[BR][2];
 #pragma unroll
     for (int m = 0; m < BR; ++m) {
@@ -376,12 +367,24 @@ __global__ __launch_bounds__(256) void k3_sweep(G3 g, const double* __restrict__
                 }
             }
     };
-    auto step = [&](const int k, double (&pl_in)[LR][2], const double (&pl_out)[LR][2],
-                    const SwCell (&rc)[RR], const SwCell (&bc)[BR], const double (&rr)[RR],
-                    const double (&rbk)[BR], const SwCell (&rc_n)[RR], const SwCell (&bc_n)[BR],
-                    double (&rr_n)[RR], double (&rbk_n)[BR]) {
+    double acc = 0.0;
+    // one update: the reference's arithmetic on LDS neighbours; returns the new value
+    auto update = [&](const double* Lc, const double* Lm, const double* Lp, int o, int nbo,
+                      double rh, double& r) {
+        const double cc = Lc[o];
+        const double tx = (Lc[nbo + 1] - 2.0 * cc) + Lc[nbo];
+        const double ty = (Lc[o + kSwRow] - 2.0 * cc) + Lc[o - kSwRow];
+        const double tz = (Lp[o] - 2.0 * cc) + Lm[o];
+        r = rh - ((tx * idx2 + ty * idy2) + tz * idz2);
+        return cc - (factor * r);
+    };
+    // step k: red of plane k (cells c: parity of k), black of plane k-1 (the
+    // same lanes' other pair element, cells cp: parity of k-1)
+    auto step = [&](const int k, D2 (&pl_in)[LR], const D2 (&pl_out)[LR], const SwCell (&c)[RR],
+                    const SwCell (&cp)[RR], const D2 (&rk)[RR], const D2 (&rkm)[RR],
+                    D2 (&rk_n)[RR]) {
         load_plane(k + 3, pl_in);
-        load_rhs(k + 1, rc_n, bc_n, rr_n, rbk_n);
+        load_rhs(k + 1, rk_n);
         __syncthreads();  // plane k+1 in LDS, plane k-2 final; the slot reused below is free
         if (k - 2 >= k0 && k - 2 <= kend) store_final(k - 2);
         if (k >= kr_lo && k <= kr_hi) {
@@ -391,11 +394,12 @@ __global__ __launch_bounds__(256) void k3_sweep(G3 g, const double* __restrict__
             const bool own_k = k >= k0 && k <= kend;
 #pragma unroll
             for (int m = 0; m < RR; ++m) {
-                if (rc[m].flags & 1) {
+                if (c[m].flags & 1) {
                     double r;
-                    const double np = update(Lc, Lm, Lp, rc[m], rr[m], r);
-                    Lc[rc[m].lds] = np;
-                    if (own_k && (rc[m].flags & 2)) acc += r * r;
+                    const double rh = c[m].sel ? rk[m].v[1] : rk[m].v[0];
+                    const double np = update(Lc, Lm, Lp, c[m].lds, c[m].nb, rh, r);
+                    Lc[c[m].lds] = np;
+                    if (own_k && (c[m].flags & 2)) acc += r * r;
                 }
             }
         }
@@ -406,11 +410,16 @@ __global__ __launch_bounds__(256) void k3_sweep(G3 g, const double* __restrict__
             const double* Lm = L + slot(kb1 - 1) * PL;
             const double* Lp = L + slot(k) * PL;
 #pragma unroll
-            for (int m = 0; m < BR; ++m) {
-                if (bc[m].flags & 1) {
+            for (int m = 0; m < RR; ++m) {
+                if (cp[m].flags & 4) {
+                    // the black cell is the pair element the red cell of plane k-1 is not
+                    const int sb = cp[m].sel ^ 1;
+                    const int o = cp[m].lds + (sb - cp[m].sel) * kSwOdd;
+                    const int nbo = cp[m].nb + (cp[m].sel - sb) * kSwOdd + (sb - cp[m].sel);
+                    const double rh = sb ? rkm[m].v[1] : rkm[m].v[0];
                     double r;
-                    const double np = update(Lc, Lm, Lp, bc[m], rbk[m], r);
-                    Lc[bc[m].lds] = np;
+                    const double np = update(Lc, Lm, Lp, o, nbo, rh, r);
+                    Lc[o] = np;
                     acc += r * r;
                 }
             }
@@ -420,21 +429,32 @@ __global__ __launch_bounds__(256) void k3_sweep(G3 g, const double* __restrict__
 
     // preload planes k0-2 .. k0 into LDS, plane k0+1 into registers
     {
-        double v[LR][2];
+        D2 v[LR];
         for (int kk = k0 - 2; kk <= k0; ++kk) {
             load_plane(kk, v);
             store_plane(kk, v);
         }
     }
-    double pl[2][LR][2];
-    double rrs[2][RR], rbs[2][BR];
+    D2 pl[2][LR];
+    D2 rs[3][RR];  // rhs pairs of three consecutive planes, rotating
     load_plane(k0 + 1, pl[0]);
-    load_rhs(k0 - 1, redA, blkA, rrs[0], rbs[0]);
-    // pl[0] holds plane k0+1 (written at the end of step k0-1), pl[1] receives k0+2
-    for (int k = k0 - 1; k <= kend + 1; k += 2) {
-        step(k, pl[1], pl[0], redA, blkA, rrs[0], rbs[0], redB, blkB, rrs[1], rbs[1]);
-        if (k + 1 <= kend + 1)
-            step(k + 1, pl[0], pl[1], redB, blkB, rrs[1], rbs[1], redA, blkA, rrs[0], rbs[0]);
+    load_rhs(k0 - 2, rs[2]);
+    load_rhs(k0 - 1, rs[0]);
+    // step k uses the pairs of planes k (red) and k-1 (black) and loads k+1;
+    // with k = k0-1+3n+u the three sets rotate with period 3, the planes with
+    // period 2: unroll by 6
+    for (int k = k0 - 1; k <= kend + 1; k += 6) {
+        step(k, pl[1], pl[0], cA, cB, rs[0], rs[2], rs[1]);
+        if (k + 1 > kend + 1) break;
+        step(k + 1, pl[0], pl[1], cB, cA, rs[1], rs[0], rs[2]);
+        if (k + 2 > kend + 1) break;
+        step(k + 2, pl[1], pl[0], cA, cB, rs[2], rs[1], rs[0]);
+        if (k + 3 > kend + 1) break;
+        step(k + 3, pl[0], pl[1], cB, cA, rs[0], rs[2], rs[1]);
+        if (k + 4 > kend + 1) break;
+        step(k + 4, pl[1], pl[0], cA, cB, rs[1], rs[0], rs[2]);
+        if (k + 5 > kend + 1) break;
+        step(k + 5, pl[0], pl[1], cB, cA, rs[2], rs[1], rs[0]);
     }
     __syncthreads();  // black of plane kend done
     store_final(kend);

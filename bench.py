@@ -15,7 +15,7 @@ region; the timed region is K iterations, barrier + device sync on both
 sides, max over ranks.  Rank 0 prints ONE JSON line.
 
 A launch (a "pass") of the default temporally blocked kernel performs T
-complete iterations (sor_tb.hip; T = iters_per_pass, default 3): it reads p
+complete iterations (sor_tb.hip; T = iters_per_pass, default 6): it reads p
 and rhs once and writes p once per T iterations.
 
 roofline: algorithmic bytes per launch = 24 B per lattice update (read p,

@@ -49,7 +49,9 @@ int fail(int code, const char* fmt, ...) {
                         __FILE__, __LINE__);                                              \
     } while (0)
 
-enum { kP0 = 0, kP1 = 1, kRhs = 2, kU = 3, kV = 4, kF = 5, kG = 6, kNumFields = 7 };
+// kP2: third pressure buffer of decomposed runs (the pipelined pass loop of
+// misor_solve_rb_n writes pass k's result while pass k-1's source is kept)
+enum { kP0 = 0, kP1 = 1, kRhs = 2, kU = 3, kV = 4, kF = 5, kG = 6, kP2 = 7, kNumFields = 8 };
 
 // MPI_Dims_create(n, 2): the most balanced factorisation, larger factor first
 void dims_create(int n, int dims[2]) {
@@ -106,12 +108,14 @@ struct misor_grid {
     misor_local loc{};
     long long pitch = 0, rows = 0, elems = 0;
     double* fld[kNumFields] = {};
-    int cur = 0;  // which p buffer holds the current pressure
+    int np = 2;   // pressure buffers: 2 (ping-pong), 3 on decomposed runs
+    int cur = 0;  // which one (0 .. np-1, see pbuf) holds the current pressure
+    int rhs_halo = 0;  // depth of rhs's exchanged halo still valid (0: rhs changed)
 
     // sweep
     SweepParams sp{};
     int nbx = 0, nby = 0, nparts = 0, partials_cap = 0;
-    double* partials = nullptr;
+    double* partials = nullptr;  // two slots of partials_cap doubles (by pass parity)
     DevState* st = nullptr;
     DevState* st_host = nullptr;  // pinned
     int last_iters = 0;
@@ -141,7 +145,9 @@ struct misor_grid {
     std::shared_ptr<LocalGroup> local;                   // in-process transport
     bool overlap = true;            // exchange on cstream while the interior sweeps
     hipStream_t cstream = nullptr;  // communication stream
-    hipEvent_t ev_s = nullptr, ev_x = nullptr, ev_d = nullptr;
+    hipStream_t estream = nullptr;  // edge blocks of a pipelined pass
+    hipEvent_t ev_s = nullptr, ev_x = nullptr, ev_d = nullptr, ev_e = nullptr;
+    hipEvent_t ev_i[2] = {}, ev_dk[2] = {};  // interior blocks / decide of pass k, by k & 1
     double* sendbuf = nullptr;
     double* recvbuf = nullptr;
     double* gbuf = nullptr;  // misor_gather: this rank's owned block, packed
@@ -152,6 +158,12 @@ struct misor_grid {
     std::vector<hipEvent_t> ev;
     misor_stats stats{};
 };
+
+// pressure buffer x (mod np)
+static double* pbuf(misor_grid* g, long long x) {
+    const int b = (int)(x % g->np);
+    return g->fld[b == 2 ? kP2 : kP0 + b];
+}
 
 extern "C" {
 
@@ -222,6 +234,13 @@ void misor_destroy(misor_grid* g) {
     (void)hipFree(g->gbuf);
     if (g->cstream) (void)hipStreamSynchronize(g->cstream);
     if (g->cstream) (void)hipStreamDestroy(g->cstream);
+    if (g->estream) (void)hipStreamSynchronize(g->estream);
+    if (g->estream) (void)hipStreamDestroy(g->estream);
+    if (g->ev_e) (void)hipEventDestroy(g->ev_e);
+    for (int b = 0; b < 2; ++b) {
+        if (g->ev_i[b]) (void)hipEventDestroy(g->ev_i[b]);
+        if (g->ev_dk[b]) (void)hipEventDestroy(g->ev_dk[b]);
+    }
     if (g->ev_s) (void)hipEventDestroy(g->ev_s);
     if (g->ev_x) (void)hipEventDestroy(g->ev_x);
     if (g->ev_d) (void)hipEventDestroy(g->ev_d);
@@ -350,7 +369,7 @@ static int ensure_partials(misor_grid* g, int n) {
     if (g->partials) (void)hipFree(g->partials);
     g->partials = nullptr;
     g->partials_cap = 0;
-    if (hipMalloc(&g->partials, sizeof(double) * n) != hipSuccess)
+    if (hipMalloc(&g->partials, sizeof(double) * 2 * (size_t)n) != hipSuccess)
         return fail(MISOR_ENOMEM, "partials allocation failed");
     g->partials_cap = n;
     return MISOR_OK;
@@ -388,15 +407,16 @@ static int effective_tsteps(const misor_grid* g) {
 }
 
 static int pick_tb_rows(int ni, int nj, int T, int waves) {
-    // long marches amortise the 4T rows each block streams beyond its own
-    // (H + 4T loads for H rows), but keep >= ~2 workgroups per CU
+    // Long marches amortise the 4T rows a block streams beyond its own (H + 4T
+    // loads for H rows); short ones give a launch more workgroups, so the last,
+    // partial round of workgroups (the tail) costs less.  Measured at T = 6
+    // (tools/scale_proxy.py, profiles/r01_scale_proxy.txt): H = 160 is best from
+    // 32768^2 down to 16384^2; below ~3000 workgroups (8192 x 16384, one rank of
+    // the 8-GPU split) H = 96 is ~4% faster.
     const int strips = (ni + tb_out_width(T) - 1) / tb_out_width(T);
-    const int nbx = (strips + waves - 1) / waves;
-    const int target_blocks = 1024;
-    const int want_nby = (target_blocks + nbx - 1) / nbx;
-    int h = (nj + want_nby - 1) / want_nby;
-    if (h < 32 * T) h = 32 * T;
-    if (h > kDefaultTbRows) h = kDefaultTbRows;
+    const long long nbx = (strips + waves - 1) / waves;
+    int h = kDefaultTbRows;
+    if (nbx * ((nj + h - 1) / h) < 3000) h = kSmallTbRows;
     return h;
 }
 
@@ -439,6 +459,7 @@ int misor_create(misor_grid** out, const misor_desc* d) {
     // a comm id with nranks == 1 still runs the decomposed code path (one rank, no
     // neighbours): lets the RCCL / overlap machinery be exercised on one GPU
     g->dist = nranks > 1 || d->comm_id != nullptr;
+    g->np = g->dist ? 3 : 2;
     if (d->device >= 0) {
         g->device = d->device;
         if (hipSetDevice(g->device) != hipSuccess) {
@@ -462,6 +483,7 @@ int misor_create(misor_grid** out, const misor_desc* d) {
     g->rows = layout_rows(L.nj);
     g->elems = g->pitch * g->rows;
     for (int k = 0; k < kNumFields; ++k) {
+        if (k == kP2 && g->np < 3) continue;
         if (hipMalloc(&g->fld[k], (size_t)g->elems * sizeof(double)) != hipSuccess)
             CREATE_FAIL(MISOR_ENOMEM, "hipMalloc of %lld doubles failed", g->elems);
         if (hipMemsetAsync(g->fld[k], 0, (size_t)g->elems * sizeof(double), g->stream) !=
@@ -536,11 +558,18 @@ int misor_create(misor_grid** out, const misor_desc* d) {
         const int minb = std::min(d->imax / L.dims[0], d->jmax / L.dims[1]);
         g->max_depth = std::max(2, std::min(2 * kMaxT, minb));
         for (int dd = 1; dd <= g->max_depth; ++dd) build_plan(g, dd);
-        if (hipStreamCreateWithFlags(&g->cstream, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&g->ev_s, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&g->ev_x, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&g->ev_d, hipEventDisableTiming) != hipSuccess)
-            CREATE_FAIL(MISOR_EHIP, "comm stream/event creation failed");
+        // communication and edge blocks at high priority: their workgroups are
+        // dispatched ahead of queued interior blocks as slots free up
+        int prio_lo = 0, prio_hi = 0;
+        (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+        bool ok = hipStreamCreateWithPriority(&g->cstream, hipStreamNonBlocking, prio_hi) ==
+                      hipSuccess &&
+                  hipStreamCreateWithPriority(&g->estream, hipStreamNonBlocking, prio_hi) ==
+                      hipSuccess;
+        for (hipEvent_t* e : {&g->ev_s, &g->ev_x, &g->ev_d, &g->ev_e, &g->ev_i[0], &g->ev_i[1],
+                              &g->ev_dk[0], &g->ev_dk[1]})
+            ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
+        if (!ok) CREATE_FAIL(MISOR_EHIP, "comm stream/event creation failed");
         // blocks whose footprint (rows j0-2..j1+1, columns c0-2..c_end+1) stays clear
         // of the halo on neighbour sides AND of the 2-deep send region can sweep
         // while the exchange is in flight
@@ -619,7 +648,7 @@ int misor_synchronize(misor_grid* g) {
 
 static double* field_ptr(misor_grid* g, int field) {
     switch (field) {
-    case MISOR_P: return g->fld[g->cur];
+    case MISOR_P: return pbuf(g, g->cur);
     case MISOR_RHS: return g->fld[kRhs];
     case MISOR_U: return g->fld[kU];
     case MISOR_V: return g->fld[kV];
@@ -638,10 +667,11 @@ int misor_upload(misor_grid* g, int field, const double* host) {
     HIPCHK(hipSetDevice(g->device));
     const size_t w = (size_t)(g->loc.ni + 2) * sizeof(double);
     const size_t h = (size_t)(g->loc.nj + 2);
-    if (field == MISOR_P) {  // both ping-pong buffers: corners and ghosts must agree
+    if (field == MISOR_RHS) g->rhs_halo = 0;
+    if (field == MISOR_P) {  // every pressure buffer: corners and ghosts must agree
         g->cur = 0;
-        for (int b = 0; b < 2; ++b)
-            HIPCHK(hipMemcpy2DAsync(origin(g, g->fld[kP0 + b]), g->pitch * sizeof(double), host,
+        for (int b = 0; b < g->np; ++b)
+            HIPCHK(hipMemcpy2DAsync(origin(g, pbuf(g, b)), g->pitch * sizeof(double), host,
                                     w, w, h, hipMemcpyHostToDevice, g->stream));
     } else {
         HIPCHK(hipMemcpy2DAsync(origin(g, field_ptr(g, field)), g->pitch * sizeof(double), host,
@@ -773,10 +803,10 @@ int misor_fill(misor_grid* g, int field, double value) {
     if (!g || !field_ptr(g, field)) return fail(MISOR_EINVAL, "bad fill");
     HIPCHK(hipSetDevice(g->device));
     // whole padded array: ghosts included, pads too (pads never feed results)
+    if (field == MISOR_RHS) g->rhs_halo = 0;
     if (field == MISOR_P) {
         g->cur = 0;
-        launch_fill(g->stream, g->fld[kP0], g->elems, value);
-        launch_fill(g->stream, g->fld[kP1], g->elems, value);
+        for (int b = 0; b < g->np; ++b) launch_fill(g->stream, pbuf(g, b), g->elems, value);
     } else {
         launch_fill(g->stream, field_ptr(g, field), g->elems, value);
     }
@@ -808,8 +838,9 @@ int misor_poisson_init(misor_grid* g, double xlength, double ylength, int proble
     HIPCHK(hipMemcpyAsync(tab + 2 * (ni + 2), sy.data(), (nj + 2) * sizeof(double),
                           hipMemcpyHostToDevice, g->stream));
     g->cur = 0;
-    for (int b = 0; b < 2; ++b)
-        launch_poisson_init(g->stream, g->fld[kP0 + b], g->fld[kRhs], tab, tab + 2 * (ni + 2),
+    g->rhs_halo = 0;
+    for (int b = 0; b < g->np; ++b)
+        launch_poisson_init(g->stream, pbuf(g, b), g->fld[kRhs], tab, tab + 2 * (ni + 2),
                             tab + (ni + 2), ni, nj, g->pitch, problem);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(g->stream));
@@ -850,7 +881,7 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
                           g->stream));
     const double cells = (double)g->desc.imax * (double)g->desc.jmax;
     if (!g->dist && g->small_solve && small_solve_fits(g->loc.ni, g->loc.nj)) {
-        double* p = g->fld[g->cur];
+        double* p = pbuf(g, g->cur);
         if (g->timing) {
             int rc = ensure_events(g, 2);
             if (rc) return rc;
@@ -883,23 +914,44 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
     const int depth = 2 * T;  // halo of src each pass needs
     const int nparts = T == 1 ? g->nparts : g->tb_nparts;
     double* const rhs = g->fld[kRhs];
-    auto pass = [&](hipStream_t s, int part, const double* src, double* dst, int Tp, int force) {
+    auto pass = [&](hipStream_t s, int part, const double* src, double* dst, int Tp, int force,
+                    double* partials) {
         if (T == 1) {
             SweepParams sp = g->sp;
             sp.part = part;
-            launch_sweep(s, sp, src, dst, rhs, g->partials, g->st);
+            launch_sweep(s, sp, src, dst, rhs, partials, g->st);
         } else {
             SweepParams tp = g->tp;
             tp.part = part;
             if (Tp != T) tb_geometry(g, Tp, tp);  // narrower cone: wider strips
-            launch_tb(s, Tp, tp, src, dst, rhs, g->partials, g->st, force);
+            launch_tb(s, Tp, tp, src, dst, rhs, partials, g->st, force);
         }
     };
     const int cur0 = g->cur;
     long long launched = 0;  // passes enqueued
-    if (g->dist) {  // the halo-ring updates read rhs outside the block
-        int rc = exchange(g, rhs, T == 1 ? 1 : depth);
+    const int rhs_depth = T == 1 ? 1 : depth;
+    if (g->dist && g->rhs_halo < rhs_depth) {  // the halo-ring updates read rhs outside the block
+        int rc = exchange(g, rhs, rhs_depth);
         if (rc) return rc;
+        g->rhs_halo = rhs_depth;
+    }
+    // Pipelined decomposed passes (T >= 2, overlap on; three pressure buffers):
+    // pass k reads src_k = pbuf(k), writes pbuf(k+1), which is the source of
+    // pass k-2 -- so pass k waits for the loop test of pass k-2 only (a pass that
+    // overshoots convergence is recomputed from its source), and the all-reduce
+    // + loop test of pass k-1 run while pass k sweeps.  Within a pass the
+    // interior blocks (main stream) and the edge blocks (estream: those whose
+    // cone reads src's halo; they alone write dst's send region) run
+    // concurrently; the exchange of dst's halo for pass k+1 starts on cstream as
+    // soon as the edge blocks are done, and so overlaps the interior blocks.
+    const bool pipelined = g->dist && g->overlap && T > 1;
+    if (pipelined) {
+        HIPCHK(hipEventRecord(g->ev_s, g->stream));  // state upload, rhs halo, prior work
+        HIPCHK(hipStreamWaitEvent(g->cstream, g->ev_s, 0));
+        HIPCHK(hipStreamWaitEvent(g->estream, g->ev_s, 0));
+        int rc = exchange(g, pbuf(g, cur0), depth, g->cstream);
+        if (rc) return rc;
+        HIPCHK(hipEventRecord(g->ev_x, g->cstream));
     }
     const long long max_passes = (itermax + T - 1) / T;
     // iterations pass k performs: T, except that the last pass of the cap does
@@ -923,20 +975,53 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
             int rc = ensure_events(g, 2 * (size_t)batch);
             if (rc) return rc;
         }
-        for (int b = 0; b < batch && g->dist && g->overlap; ++b) {
+        for (int b = 0; b < batch && pipelined; ++b) {
+            const long long k = launched + b;
+            const int Tk = t_of(k);
+            const double* src = pbuf(g, cur0 + k);
+            double* dst = pbuf(g, cur0 + k + 1);
+            double* part = g->partials + (k & 1) * (long long)g->partials_cap;
+            // interior blocks: after pass k-1 (this stream, plus the edge blocks:
+            // waited on at the end of the previous iteration) and decide k-2
+            if (k >= 2) HIPCHK(hipStreamWaitEvent(g->stream, g->ev_dk[k & 1], 0));
+            if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b], g->stream));
+            pass(g->stream, 1, src, dst, Tk, 0, part);
+            HIPCHK(hipEventRecord(g->ev_i[k & 1], g->stream));
+            // edge blocks: after the interior blocks of pass k-1, the edge blocks
+            // of k-1 (this stream) and the exchange of src's halo (which follows
+            // decide k-2 on cstream)
+            if (k >= 1) HIPCHK(hipStreamWaitEvent(g->estream, g->ev_i[(k - 1) & 1], 0));
+            HIPCHK(hipStreamWaitEvent(g->estream, g->ev_x, 0));
+            pass(g->estream, 2, src, dst, Tk, 0, part);
+            HIPCHK(hipEventRecord(g->ev_e, g->estream));
+            // cstream: dst's halo for pass k+1, then the residual of pass k
+            HIPCHK(hipStreamWaitEvent(g->cstream, g->ev_e, 0));
+            int rc = exchange(g, dst, depth, g->cstream);
+            if (rc) return rc;
+            HIPCHK(hipEventRecord(g->ev_x, g->cstream));
+            HIPCHK(hipStreamWaitEvent(g->cstream, g->ev_i[k & 1], 0));
+            launch_finish(g->cstream, part, nparts_of(Tk), Tk, g->st, cells, 0);
+            rc = allreduce(g, g->st->sum, Tk, 0, g->cstream);
+            if (rc) return rc;
+            launch_decide(g->cstream, g->st, Tk, cells);
+            HIPCHK(hipEventRecord(g->ev_dk[k & 1], g->cstream));
+            // pass k+1's interior blocks read what the edge blocks of pass k wrote
+            HIPCHK(hipStreamWaitEvent(g->stream, g->ev_e, 0));
+            if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b + 1], g->stream));
+            if (b == batch - 1)  // the host reads the loop state after the last decide
+                HIPCHK(hipStreamWaitEvent(g->stream, g->ev_dk[k & 1], 0));
+        }
+        for (int b = 0; b < batch && g->dist && g->overlap && !pipelined; ++b) {
             // Overlapped pass k.  comm stream: [wait pass k-1] all-reduce and
             // decide of k-1, exchange of src_k.  compute stream: interior blocks
             // of pass k (no halo reads) meanwhile, then [wait exchange] boundary
-            // blocks, partial sums.  With T = 1 an interior pass launched after
-            // convergence (decide k-1 still in flight) only writes the buffer
-            // that is not the result.  With T >= 2 the source of pass k-1 must
-            // survive (a pass that overshoots convergence is recomputed from
-            // it), so the interior blocks wait for decide k-1; the exchange still
-            // overlaps them.
+            // blocks, partial sums.  (T = 1 only: T >= 2 takes the pipelined
+            // loop above.)  An interior pass launched after convergence (decide
+            // k-1 still in flight) only writes a buffer that is not the result.
             const long long k = launched + b;
             const int Tk = t_of(k);
-            const double* src = g->fld[kP0 + ((cur0 + k) & 1)];
-            double* dst = g->fld[kP0 + ((cur0 + k + 1) & 1)];
+            const double* src = pbuf(g, cur0 + k);
+            double* dst = pbuf(g, cur0 + k + 1);
             HIPCHK(hipEventRecord(g->ev_s, g->stream));
             HIPCHK(hipStreamWaitEvent(g->cstream, g->ev_s, 0));
             if (b > 0) {  // pass k-1 of this batch (the previous batch closed its own)
@@ -952,9 +1037,9 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
             if (rc) return rc;
             HIPCHK(hipEventRecord(g->ev_x, g->cstream));
             if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b], g->stream));
-            pass(g->stream, 1, src, dst, Tk, 0);
+            pass(g->stream, 1, src, dst, Tk, 0, g->partials);
             HIPCHK(hipStreamWaitEvent(g->stream, g->ev_x, 0));
-            pass(g->stream, 2, src, dst, Tk, 0);
+            pass(g->stream, 2, src, dst, Tk, 0, g->partials);
             if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b + 1], g->stream));
             launch_finish(g->stream, g->partials, nparts_of(Tk), Tk, g->st, cells, 0);
             if (b == batch - 1) {  // close the batch: all-reduce + decide of the last one
@@ -970,14 +1055,14 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
         for (int b = 0; b < batch && !(g->dist && g->overlap); ++b) {
             const long long k = launched + b;
             const int Tk = t_of(k);
-            const double* src = g->fld[kP0 + ((cur0 + k) & 1)];
-            double* dst = g->fld[kP0 + ((cur0 + k + 1) & 1)];
+            const double* src = pbuf(g, cur0 + k);
+            double* dst = pbuf(g, cur0 + k + 1);
             if (g->dist) {  // 2T-deep halo of src: one exchange per pass
                 int rc = exchange(g, const_cast<double*>(src), depth);
                 if (rc) return rc;
             }
             if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b], g->stream));
-            pass(g->stream, 0, src, dst, Tk, 0);
+            pass(g->stream, 0, src, dst, Tk, 0, g->partials);
             if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b + 1], g->stream));
             if (g->dist) {
                 launch_finish(g->stream, g->partials, nparts_of(Tk), Tk, g->st, cells, 0);
@@ -1015,16 +1100,16 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
     const int it = g->st_host->it;
     const long long passes = std::min((long long)(it + T - 1) / T, max_passes);
     const int over = (int)(covered(passes) - it);
-    g->cur = (int)((cur0 + passes) & 1);
+    g->cur = (int)((cur0 + passes) % g->np);
     if (over > 0) {
         // the last pass ran past the iteration that ended the loop: redo it
         // with T - over iterations from its source (untouched since)
-        const double* src = g->fld[kP0 + ((cur0 + passes - 1) & 1)];
-        pass(g->stream, 0, src, g->fld[g->cur], t_of(passes - 1) - over, 1);
+        const double* src = pbuf(g, cur0 + passes - 1);
+        pass(g->stream, 0, src, pbuf(g, g->cur), t_of(passes - 1) - over, 1, g->partials);
         HIPCHK(hipGetLastError());
     }
     if (g->dist) {  // leave the halo of the final field consistent (adaptUV reads it)
-        int rc = exchange(g, g->fld[g->cur], 2);
+        int rc = exchange(g, pbuf(g, g->cur), 2);
         if (rc) return rc;
     }
     HIPCHK(hipStreamSynchronize(g->stream));
@@ -1052,7 +1137,7 @@ int misor_solve_lex(misor_grid* g, int xorder, int* iters, double* res) {
     HIPCHK(hipMemcpyAsync(g->st, g->st_host, sizeof(DevState), hipMemcpyHostToDevice,
                           g->stream));
     const double cells = (double)g->desc.imax * (double)g->desc.jmax;
-    launch_solve_lex(g->stream, g->fld[g->cur], g->fld[kRhs], g->loc.ni, g->loc.nj, g->pitch,
+    launch_solve_lex(g->stream, pbuf(g, g->cur), g->fld[kRhs], g->loc.ni, g->loc.nj, g->pitch,
                      g->sp.idx2, g->sp.idy2, g->sp.coef, cells, xorder != 0, g->st);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(g->st_host, g->st, sizeof(DevState), hipMemcpyDeviceToHost,
@@ -1184,13 +1269,14 @@ int misor_compute_rhs(misor_grid* g) {
     if (!rc) rc = exchange(g, g->fld[kG], 1);
     if (rc) return rc;
     launch_compute_rhs(g->nl, g->fld[kF], g->fld[kG], g->fld[kRhs]);
+    g->rhs_halo = 0;
     HIPCHK(hipGetLastError());
     return MISOR_OK;
 }
 
 int misor_normalize_pressure(misor_grid* g) {
     NEED_NS(g);
-    double* p = g->fld[g->cur];
+    double* p = pbuf(g, g->cur);
     launch_sum(g->nl, p, g->red_partials);
     launch_finish_reduce(g->stream, g->red_partials, reduce_blocks(g->loc.ni, g->loc.nj),
                          kReduceSum, 1, g->red_out);
@@ -1207,7 +1293,7 @@ int misor_normalize_pressure(misor_grid* g) {
 
 int misor_adapt_uv(misor_grid* g) {
     NEED_NS(g);
-    launch_adapt_uv(g->nl, g->fld[kF], g->fld[kG], g->fld[g->cur], g->fld[kU], g->fld[kV]);
+    launch_adapt_uv(g->nl, g->fld[kF], g->fld[kG], pbuf(g, g->cur), g->fld[kU], g->fld[kV]);
     HIPCHK(hipGetLastError());
     return MISOR_OK;
 }

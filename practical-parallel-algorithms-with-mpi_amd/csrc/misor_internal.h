@@ -66,7 +66,8 @@ constexpr TbVariant kTbVariants[] = {{4, 2, 0, 0}, {8, 2, 0, 0}, {4, 3, 0, 0}, {
 constexpr int kNumTbVariants = 8;
 constexpr int kDefaultTsteps = 6;      // iterations per pass (tools/tune_sweep.py --tb)
 constexpr int kDefaultTbVariant = 2;   // 4 strips, 3 rows in flight, rhs ring in registers
-constexpr int kDefaultTbRows = 192;    // cap of the automatic rows per block
+constexpr int kDefaultTbRows = 160;    // automatic rows per block (misor_api.hip pick_tb_rows)
+constexpr int kSmallTbRows = 96;       // ... for launches of fewer than ~3000 workgroups
 int tb_waves(int variant);
 int tb_out_width(int T);
 int tb_partials(int ni, int nj, int T, int rows_per_block, int waves, int* nbx, int* nby);

@@ -190,3 +190,58 @@ def test_rccl_single_rank_path(golden):
         it, res = g.solve_rb()
         assert it == 3 and np.array_equal(g.download(M.P), p)
         assert abs(res - res_ref) <= 1e-12 * res_ref
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("T", [2, 6])
+def test_consecutive_solves_rotate_buffers(world, T):
+    """three solves in a row (7, 13, 25 iterations): the pipelined pass loop
+    rotates three pressure buffers, so each solve starts from a different one;
+    p after each solve is bit-identical to the single-domain oracle"""
+    ni, nj = 410, 230
+    rng = np.random.default_rng(7 * world + T)
+    p = rng.standard_normal((nj + 2, ni + 2))
+    rhs = rng.standard_normal((nj + 2, ni + 2)) * 10
+    dx, dy = 1.0 / ni, 1.3 / nj
+    counts = (7, 13, 25)
+    wants = []
+    w = p.copy()
+    for k in counts:
+        orc.solve_rb(w, rhs, dx, dy, 1.8, 1e-300, k)
+        wants.append(w.copy())
+
+    def rank_fn(r, cid, dims):
+        with M.Grid(ni, nj, dx, dy, 1.8, 1e-300, 100, device=0, nranks=world, rank=r,
+                    comm_id=cid) as g:
+            g.set_tuning(M.TUNE_TSTEPS, T)
+            g.upload(M.P, local_window(p, g.loc))
+            g.upload(M.RHS, local_window(rhs, g.loc))
+            got = []
+            for k in counts:
+                it, _ = g.solve_rb(itermax=k)
+                assert it == k
+                got.append(g.download(M.P))
+            return g.loc, got
+
+    outs = run_ranks(world, rank_fn)
+    for s in range(len(counts)):
+        got = assemble([(o[0], o[1][s]) for o in outs], p.shape)
+        assert np.array_equal(got, wants[s]), (s, np.argwhere(got != wants[s])[:5])
+
+
+def test_rccl_single_rank_pipelined_fixed_sweeps():
+    """the pipelined pass loop on real RCCL streams (one rank): interior and
+    edge launches, exchange and all-reduce on their own streams, 3 consecutive
+    solves of many passes each, bit-identical to the oracle"""
+    ni, nj = 1500, 1100
+    p, rhs = orc.poisson_init(ni, nj)
+    want = p.copy()
+    with M.Grid(ni, nj, 1.0 / ni, 1.0 / nj, 1.9, 1e-300, 100, device=0, nranks=1, rank=0,
+                comm_id=M.comm_unique_id()) as g:
+        g.poisson_init(1.0, 1.0, 2)
+        for k in (31, 24, 50):
+            it_ref, res_ref = orc.solve_rb(want, rhs, 1.0 / ni, 1.0 / nj, 1.9, 1e-300, k)
+            it, res = g.solve_rb(itermax=k)
+            assert it == k == it_ref
+            assert abs(res - res_ref) <= 1e-12 * res_ref
+            assert np.array_equal(g.download(M.P), want)

@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""Compute-side strong-scaling proxy on ONE GPU.
+
+For N = 1, 2, 4, 8 the 32768^2 bench grid is split as bench.py splits it
+(misor_decompose); this script times ONE rank's block (rank 0's ni x nj) as a
+single-rank solve on this GPU, for several temporally-blocked row heights, and
+prints the compute-only efficiency t(1) / (N * t(N)).  Communication is not
+modelled (the box has one GPU); what this isolates is the loss from smaller
+grids: fewer workgroups per launch, wave quantisation, the last partial round.
+
+    python tools/scale_proxy.py [--size 32768] [--rows 0,128,192] [--sweeps 24]
+"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "practical-parallel-algorithms-with-mpi_amd"))
+import pymisor as M  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--size", type=int, default=32768)
+    ap.add_argument("--ranks", default="1,2,4,8")
+    ap.add_argument("--rows", default="0,96,128,160,192")
+    ap.add_argument("--sweeps", type=int, default=24)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--base-ms", type=float, default=0.0,
+                    help="N=1 ms per iteration to compute eff against (default: first row)")
+    ap.add_argument("--tsteps", default="6", help="iterations per pass to try")
+    ap.add_argument("--variants", default="-1", help="TB variants to try (-1: default)")
+    args = ap.parse_args()
+    n = args.size
+    combos = [(int(t), int(v), int(r)) for t in args.tsteps.split(",")
+              for v in args.variants.split(",") for r in args.rows.split(",")]
+    base = args.base_ms or None
+    print("%-2s %-12s %2s %2s %5s %10s %10s %10s %6s" % (
+        "N", "local", "T", "v", "rows", "ms/iter", "wall/iter", "MLUP/s/GPU", "eff"), flush=True)
+    for N in [int(x) for x in args.ranks.split(",")]:
+        L = M.decompose(N, 0, n, n)
+        ni, nj = L.ni, L.nj
+        g = M.Grid(ni, nj, 1.0 / n, 1.0 / n, 1.9, 1e-300, args.sweeps, device=0)
+        g.poisson_init(1.0, 1.0, 2)
+        g.enable_timing(True)
+        g.solve_rb(itermax=args.sweeps)  # warm-up
+        v0 = g.get_tuning(M.TUNE_TB_VARIANT)
+        res = {c: ([], []) for c in combos}
+        for _ in range(args.rounds):
+            for c in combos:
+                T, v, r = c
+                g.set_tuning(M.TUNE_TSTEPS, T)
+                g.set_tuning(M.TUNE_TB_VARIANT, v0 if v < 0 else v)
+                g.set_tuning(M.TUNE_TB_ROWS, r)
+                g.reset_stats()
+                g.synchronize()
+                t0 = time.perf_counter()
+                g.solve_rb(itermax=args.sweeps)
+                g.synchronize()
+                wall = time.perf_counter() - t0
+                st = g.stats()
+                assert st["iters_per_pass"] == T
+                res[c][0].append(st["sweep_ms"] / st["timed_sweeps"])
+                res[c][1].append(wall * 1e3 / st["timed_sweeps"])
+        for c in combos:
+            T, v, r = c
+            ms = float(np.median(res[c][0]))
+            wall = float(np.median(res[c][1]))
+            mlups = ni * nj / (ms * 1e-3) / 1e6
+            if base is None:
+                base = ms * N
+            eff = base / (N * ms)
+            print("%-2d %-12s %2d %2d %5d %10.4f %10.4f %10.0f %6.3f" % (
+                N, "%dx%d" % (ni, nj), T, v, r, ms, wall, mlups, eff), flush=True)
+        g.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -408,15 +408,16 @@ static int effective_tsteps(const misor_grid* g) {
 
 static int pick_tb_rows(int ni, int nj, int T, int waves) {
     // Long marches amortise the 4T rows a block streams beyond its own (H + 4T
-    // loads for H rows); short ones give a launch more workgroups, so the last,
-    // partial round of workgroups (the tail) costs less.  Measured at T = 6
-    // (tools/scale_proxy.py, profiles/r01_scale_proxy.txt): H = 160 is best from
-    // 32768^2 down to 16384^2; below ~3000 workgroups (8192 x 16384, one rank of
-    // the 8-GPU split) H = 96 is ~4% faster.
+    // loads for H rows); short ones give a launch more workgroups.  Measured at
+    // T = 6, 7 once the physical-side blocks stopped running the lane-masked
+    // path for whole block rows (tools/scale_proxy.py, profiles/
+    // r01_shape_sweep*.txt): H = 192 is within noise of the best from 32768^2
+    // down to 8192 x 16384 (one rank of the 8-GPU split); smaller grids halve H
+    // until the launch has ~1024 workgroups (4 per CU) to spread.
     const int strips = (ni + tb_out_width(T) - 1) / tb_out_width(T);
     const long long nbx = (strips + waves - 1) / waves;
     int h = kDefaultTbRows;
-    if (nbx * ((nj + h - 1) / h) < 3000) h = kSmallTbRows;
+    while (h / 2 >= kMinTbRows && nbx * ((nj + h - 1) / h) < 1024) h /= 2;
     return h;
 }
 

@@ -64,10 +64,10 @@ struct TbVariant {
 constexpr TbVariant kTbVariants[] = {{4, 2, 0, 0}, {8, 2, 0, 0}, {4, 3, 0, 0}, {4, 2, 1, 0},
                                      {4, 2, 1, 4}, {4, 3, 1, 0}, {8, 2, 1, 0}, {6, 2, 1, 0}};
 constexpr int kNumTbVariants = 8;
-constexpr int kDefaultTsteps = 6;      // iterations per pass (tools/tune_sweep.py --tb)
+constexpr int kDefaultTsteps = 7;      // iterations per pass (tools/scale_proxy.py, r01_shape_sweep)
 constexpr int kDefaultTbVariant = 2;   // 4 strips, 3 rows in flight, rhs ring in registers
-constexpr int kDefaultTbRows = 160;    // automatic rows per block (misor_api.hip pick_tb_rows)
-constexpr int kSmallTbRows = 96;       // ... for launches of fewer than ~3000 workgroups
+constexpr int kDefaultTbRows = 192;    // automatic rows per block (misor_api.hip pick_tb_rows)
+constexpr int kMinTbRows = 48;         // ... halved down to this while a launch has < 1024 WGs
 int tb_waves(int variant);
 int tb_out_width(int T);
 int tb_partials(int ni, int nj, int T, int rows_per_block, int waves, int* nbx, int* nby);

@@ -125,7 +125,11 @@ struct Lane {
 //          stored value); only the residual (select on the row's ownership)
 //          and the store are row-tested.  The 4T+1 warm-up and 2T drain steps.
 //  kSteady interior, every row touched is owned: no tests at all.
-enum { kEdge = 0, kWarm = 1, kSteady = 2 };
+//  kRowEdge columns interior (every lane's two columns updated, ownership
+//          uniform per lane), rows general: the first/last block row at a
+//          physical bottom/top side.  Row tests and ghost-row copies are
+//          wave-uniform; no lane masks, the residual as in kWarm.
+enum { kEdge = 0, kWarm = 1, kSteady = 2, kRowEdge = 3 };
 
 // One iteration stage.  In = row rin of the previous stage's output (stage 1:
 // of the field in memory).  Returns row rin-2 of this stage's output.
@@ -137,15 +141,16 @@ enum { kEdge = 0, kWarm = 1, kSteady = 2 };
 template <int Q, int MODE>
 __device__ __forceinline__ d2 stage(const Lane& c, bool fixrows, d2 In, int rin, d2& A, d2& M1,
                                     d2& M2, d2 Ra, d2 Rb, double& acc) {
-    constexpr bool EDGE = MODE == kEdge;
-    if (EDGE && fixrows) {
+    constexpr bool EDGE = MODE == kEdge;                // lane masks
+    constexpr bool ROWS = EDGE || MODE == kRowEdge;     // row tests, ghost rows
+    if (ROWS && fixrows) {
         if (c.gb && rin == 1) {  // row 0 := row 1 (A holds row 0)
-            if (c.up_a) A.x = In.x;
-            if (c.up_b) A.y = In.y;
+            if (!EDGE || c.up_a) A.x = In.x;
+            if (!EDGE || c.up_b) A.y = In.y;
         }
         if (c.gt && rin == c.nj + 1) {  // row nj+1 := row nj (A holds row nj)
-            if (c.up_a) In.x = A.x;
-            if (c.up_b) In.y = A.y;
+            if (!EDGE || c.up_a) In.x = A.x;
+            if (!EDGE || c.up_b) In.y = A.y;
         }
     }
     const int rr = rin - 1;  // red row
@@ -156,7 +161,7 @@ __device__ __forceinline__ d2 stage(const Lane& c, bool fixrows, d2 In, int rin,
     auto tally = [&](double r, bool own_row, bool own_col) {
         if (MODE == kSteady) {
             acc = __builtin_fma(r, r, acc);
-        } else if (MODE == kWarm) {
+        } else if (MODE == kWarm || MODE == kRowEdge) {
             const double rm = own_row ? r : 0.0;  // uniform select: no branch, NaN-safe
             acc = __builtin_fma(rm, rm, acc);
         } else if (own_row && own_col) {
@@ -166,7 +171,7 @@ __device__ __forceinline__ d2 stage(const Lane& c, bool fixrows, d2 In, int rin,
 
     // red pass on row rr
     d2 Mr = A;
-    if (!EDGE || (rr >= c.lo_j && rr <= c.hi_j)) {
+    if (!ROWS || (rr >= c.lo_j && rr <= c.hi_j)) {
         const bool own = (rr >= c.j0) && (rr < c.j1);
         if (q == 0) {
             const double Lf = from_left(A.y);
@@ -187,7 +192,7 @@ __device__ __forceinline__ d2 stage(const Lane& c, bool fixrows, d2 In, int rin,
 
     // black pass on row rb (+ the ghost column copy of this finished row)
     d2 F = M1;
-    if (!EDGE || (rb >= c.lo_j && rb <= c.hi_j)) {
+    if (!ROWS || (rb >= c.lo_j && rb <= c.hi_j)) {
         const bool own = (rb >= c.j0) && (rb < c.j1);
         if (q == 0) {
             const double Ln = from_left(M1.y);
@@ -284,6 +289,15 @@ __device__ __forceinline__ void tb_step(March<T, D, LR>& m, const Lane& c, const
                 if (c.st_a) stv<NT>(io.dp + (long long)jw * pitch, v);
             } else if (MODE == kWarm) {
                 if (jw >= c.j0 && jw < c.j1 && c.st_a) stv<NT>(io.dp + (long long)jw * pitch, v);
+            } else if (MODE == kRowEdge) {
+                // every column of the lane updated and stored alike (st_a == st_b);
+                // ghost rows 0 / nj+1 of the stored field are copies of rows 1 / nj
+                if (jw >= c.j0 && jw < c.j1 && c.st_a) {
+                    double* drow = io.dp + (long long)jw * pitch;
+                    stv<NT>(drow, v);
+                    if (c.gb && jw == 1) stv<NT>(drow - pitch, v);
+                    if (c.gt && jw == c.nj) stv<NT>(drow + pitch, v);
+                }
             } else if (jw >= c.j0 && jw < c.j1) {
                 double* drow = io.dp + (long long)jw * pitch;
                 auto put = [&](double* p, d2 o) {
@@ -340,6 +354,27 @@ __device__ __forceinline__ void march_interior_q(March<T, D, LR>& m, const Lane&
         tb_step<T, D, LR, NT, 1 - Q0, kWarm>(m, c, io, r0 + 1);
     }
     if (r0 <= rend) tb_step<T, D, LR, NT, Q0, kWarm>(m, c, io, r0);
+}
+
+// Blocks with a physical side in their cone (kEdge / kRowEdge): every step
+// general, but still in colour pairs so the colour is a compile-time constant.
+template <int T, int D, bool LR, bool NT, int Q0, int MODE>
+__device__ __forceinline__ void march_edge_q(March<T, D, LR>& m, const Lane& c, const Io& io,
+                                             int r0, int rend) {
+    for (; r0 + 1 <= rend; r0 += 2) {
+        tb_step<T, D, LR, NT, Q0, MODE>(m, c, io, r0);
+        tb_step<T, D, LR, NT, 1 - Q0, MODE>(m, c, io, r0 + 1);
+    }
+    if (r0 <= rend) tb_step<T, D, LR, NT, Q0, MODE>(m, c, io, r0);
+}
+
+template <int T, int D, bool LR, bool NT, int MODE>
+__device__ __forceinline__ void march_edge(March<T, D, LR>& m, const Lane& c, const Io& io,
+                                           int rs, int rend) {
+    if (((c.parity + rs) & 1) == 0)
+        march_edge_q<T, D, LR, NT, 0, MODE>(m, c, io, rs, rend);
+    else
+        march_edge_q<T, D, LR, NT, 1, MODE>(m, c, io, rs, rend);
 }
 
 template <int T, int D, bool LR, bool NT>
@@ -450,17 +485,23 @@ __global__ __launch_bounds__(kLanes* WAVES, MINW) void rb_tb_kernel(
             for (int k = 0; k < 2 * T; ++k) m.R[k] = d2{0.0, 0.0};
         }
 
-        // every cell of the cone an updated cell (no masks, no ghost rows or
-        // columns) and every output column owned (on a neighbour side the strip
-        // may run into the halo: those columns are neither stored nor counted)
-        const bool interior = c_ld >= prm.upd_lo_i && c_ld + kStripCells - 1 <= prm.upd_hi_i &&
-                              c_out + OW - 1 <= ni && rs >= prm.upd_lo_j &&
-                              rend <= prm.upd_hi_j;
-        if (!interior) {
-            for (int r0 = rs; r0 <= rend; ++r0) tb_step<T, D, LR, NT, -1, kEdge>(m, c, io, r0);
+        // columns interior: every column of the cone an updated cell (no lane
+        // masks, no ghost columns) and ownership uniform per lane -- the strip
+        // is whole, or it runs past column ni into a neighbour's halo (or the
+        // padding beyond it) with ni even, so ni | ni+1 falls between lanes;
+        // those lanes are neither stored nor counted.  Rows interior: no
+        // ghost rows in the cone.
+        const bool cols_in = c_ld >= prm.upd_lo_i && c_ld + kStripCells - 1 <= prm.upd_hi_i &&
+                             (c_out + OW - 1 <= ni || (ni & 1) == 0);
+        const bool rows_in = rs >= prm.upd_lo_j && rend <= prm.upd_hi_j;
+        if (!cols_in) {
+            march_edge<T, D, LR, NT, kEdge>(m, c, io, rs, rend);
         } else {
-            march_interior<T, D, LR, NT>(m, c, io, rs, rend);
-            if (!own_lane) {
+            if (rows_in)
+                march_interior<T, D, LR, NT>(m, c, io, rs, rend);
+            else
+                march_edge<T, D, LR, NT, kRowEdge>(m, c, io, rs, rend);
+            if (!c.own_a) {
 #pragma unroll
                 for (int t = 0; t < T; ++t) m.acc[t] = 0.0;
             }

@@ -7,7 +7,7 @@ tag=$1; shift
 out=gpurun_out/prof_$tag
 mkdir -p $out
 timeout -k 10 300 python bench.py "$@" > $out/bench.json 2> $out/bench.err
-B="python bench.py --steps 24 --warmup 6 --no-cpu-baseline $*"
+B="python bench.py --steps 28 --warmup 7 --no-cpu-baseline $*"
 timeout -s KILL 180 rocprofv3 --kernel-trace --stats -d $out -o trace --output-format csv -- $B > $out/trace.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $out -o fetch --output-format csv -- $B > $out/fetch.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $out -o write --output-format csv -- $B > $out/write.log 2>&1

@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--base-ms", type=float, default=0.0,
                     help="N=1 ms per iteration to compute eff against (default: first row)")
     ap.add_argument("--tsteps", default="6", help="iterations per pass to try")
+    ap.add_argument("--shapes", default="",
+                    help="explicit local blocks NIxNJ[:N],... instead of the decomposition of --ranks")
     ap.add_argument("--variants", default="-1", help="TB variants to try (-1: default)")
     args = ap.parse_args()
     n = args.size
@@ -40,9 +42,18 @@ def main():
     base = args.base_ms or None
     print("%-2s %-12s %2s %2s %5s %10s %10s %10s %6s" % (
         "N", "local", "T", "v", "rows", "ms/iter", "wall/iter", "MLUP/s/GPU", "eff"), flush=True)
-    for N in [int(x) for x in args.ranks.split(",")]:
-        L = M.decompose(N, 0, n, n)
-        ni, nj = L.ni, L.nj
+    if args.shapes:
+        cases = []
+        for sh in args.shapes.split(","):
+            dims, _, nr = sh.partition(":")
+            a, b = dims.split("x")
+            cases.append((int(nr or (n * n) // (int(a) * int(b))), int(a), int(b)))
+    else:
+        cases = []
+        for N in [int(x) for x in args.ranks.split(",")]:
+            L = M.decompose(N, 0, n, n)
+            cases.append((N, L.ni, L.nj))
+    for N, ni, nj in cases:
         g = M.Grid(ni, nj, 1.0 / n, 1.0 / n, 1.9, 1e-300, args.sweeps, device=0)
         g.poisson_init(1.0, 1.0, 2)
         g.enable_timing(True)

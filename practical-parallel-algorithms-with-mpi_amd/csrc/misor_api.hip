@@ -406,27 +406,28 @@ static int effective_tsteps(const misor_grid* g) {
     return T;
 }
 
-static int pick_tb_rows(int ni, int nj, int T, int waves) {
-    // Long marches amortise the 4T rows a block streams beyond its own (H + 4T
-    // loads for H rows); short ones give a launch more workgroups.  Measured at
-    // T = 6, 7 once the physical-side blocks stopped running the lane-masked
-    // path for whole block rows (tools/scale_proxy.py, profiles/
-    // r01_shape_sweep*.txt): H = 192 is within noise of the best from 32768^2
-    // down to 8192 x 16384 (one rank of the 8-GPU split); smaller grids halve H
-    // until the launch has ~1024 workgroups (4 per CU) to spread.
-    const int strips = (ni + tb_out_width(T) - 1) / tb_out_width(T);
-    const long long nbx = (strips + waves - 1) / waves;
+static int pick_tb_nby(int ni, int nj, int T, int waves) {
+    // Block rows for a pass of T iterations.  A block streams H + 4T rows for
+    // its H, so tall blocks waste less; short ones give a launch more
+    // workgroups.  Measured at T = 6, 7 once the physical-side blocks stopped
+    // running the lane-masked path for whole block rows (tools/scale_proxy.py,
+    // profiles/r01_shape_sweep*.txt): H ~ 192 is within noise of the best from
+    // 32768^2 down to 8192 x 16384 (one rank of the 8-GPU split).  Taller
+    // blocks lose even where they fill the last round of resident workgroups
+    // exactly (r01_geom_sweep.txt: 8192 x 16384 at H = 225, 2.99 rounds of 512
+    // workgroups, is 7% slower than H = 191, 3.5 rounds).  Smaller grids halve
+    // H until the launch has ~1024 workgroups (4 per CU) to spread.  Heights
+    // inside a launch differ by at most one row.
+    const long long nbx = tb_nbx(ni, T, waves);
     int h = kDefaultTbRows;
     while (h / 2 >= kMinTbRows && nbx * ((nj + h - 1) / h) < 1024) h /= 2;
-    return h;
+    return (nj + h - 1) / h;
 }
 
 // geometry of the temporally blocked pass with T iterations into `tp`
 static void tb_geometry(const misor_grid* g, int T, SweepParams& tp) {
-    const int waves = tb_waves(tp.variant);
-    int nby = 0, nbx = 0;
-    tp.nblocks = tb_partials(g->loc.ni, g->loc.nj, T, tp.rows_per_block, waves, &nbx, &nby);
-    tp.nbx = nbx;
+    tp.nbx = tb_nbx(g->loc.ni, T, tb_waves(tp.variant));
+    tp.nblocks = tp.nbx * tp.nby;
 }
 
 static int configure_tb(misor_grid* g, int T, int variant, int rows) {
@@ -435,7 +436,10 @@ static int configure_tb(misor_grid* g, int T, int variant, int rows) {
     g->tsteps = T;
     SweepParams& tp = g->tp;
     tp.variant = variant;
-    tp.rows_per_block = rows > 0 ? rows : pick_tb_rows(g->loc.ni, g->loc.nj, T, tb_waves(variant));
+    const int Tg = effective_tsteps(g);
+    tp.nby = rows > 0 ? (g->loc.nj + rows - 1) / rows
+                      : pick_tb_nby(g->loc.ni, g->loc.nj, Tg, tb_waves(variant));
+    tp.rows_per_block = (g->loc.nj + tp.nby - 1) / tp.nby;
     tp.xcd_remap = g->sp.xcd_remap;
     const int Te = effective_tsteps(g);
     tb_geometry(g, Te, tp);

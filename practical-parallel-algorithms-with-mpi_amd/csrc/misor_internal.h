@@ -70,7 +70,7 @@ constexpr int kDefaultTbRows = 192;    // automatic rows per block (misor_api.hi
 constexpr int kMinTbRows = 48;         // ... halved down to this while a launch has < 1024 WGs
 int tb_waves(int variant);
 int tb_out_width(int T);
-int tb_partials(int ni, int nj, int T, int rows_per_block, int waves, int* nbx, int* nby);
+int tb_nbx(int ni, int T, int waves);           // block columns of a pass of T iterations
 
 // Solver state that lives on the device between launches.  Written only by
 // the finish kernel (one workgroup) and read by the next sweep launch.
@@ -88,7 +88,9 @@ struct DevState {
 struct SweepParams {
     long long pitch;
     int ni, nj;          // local interior size
-    int rows_per_block;  // H
+    int rows_per_block;  // H (temporally blocked: the tallest block, ceil(nj / nby))
+    int nby;             // temporally blocked: block rows; block row by owns rows
+                         // [1 + by*nj/nby, 1 + (by+1)*nj/nby) -- heights differ by <= 1
     int parity;          // (ioff + joff) & 1 : global colour of local cell (0,0)
     int ghost_left, ghost_right, ghost_bottom, ghost_top;  // physical boundary -> Neumann copy
     int red_lo_i, red_hi_i, red_lo_j, red_hi_j;  // cells whose red value is computed

@@ -317,15 +317,33 @@ __global__ __launch_bounds__(1024) void rb_finish_kernel(const double* __restric
     __shared__ double tot[kMaxT];
     if (st->done) return;
     const int t = threadIdx.x;
-    // all T groups in one strided pass (T independent loads in flight per thread)
-    double s[kMaxT];
+    // all T groups in one strided pass, four strides per trip with separate
+    // accumulators (4T independent loads in flight per thread: the partials of
+    // a 32768^2 pass are ~14k per group, and a 1-deep loop paid one memory
+    // latency per stride), combined in a fixed order
+    double s[kMaxT], s1[kMaxT], s2[kMaxT], s3[kMaxT];
 #pragma unroll
-    for (int g = 0; g < kMaxT; ++g) s[g] = 0.0;
-    for (int k = t; k < n; k += 1024) {
+    for (int g = 0; g < kMaxT; ++g) s[g] = s1[g] = s2[g] = s3[g] = 0.0;
+    int k = t;
+    for (; k + 3 * 1024 < n; k += 4 * 1024) {
+#pragma unroll
+        for (int g = 0; g < kMaxT; ++g) {
+            if (g < T) {
+                const double* q = partials + (long long)g * n + k;
+                s[g] += q[0];
+                s1[g] += q[1024];
+                s2[g] += q[2048];
+                s3[g] += q[3072];
+            }
+        }
+    }
+    for (; k < n; k += 1024) {
 #pragma unroll
         for (int g = 0; g < kMaxT; ++g)
             if (g < T) s[g] += partials[(long long)g * n + k];
     }
+#pragma unroll
+    for (int g = 0; g < kMaxT; ++g) s[g] = (s[g] + s1[g]) + (s2[g] + s3[g]);
 #pragma unroll
     for (int g = 0; g < kMaxT; ++g)
         if (g < T) sh[g][t] = s[g];

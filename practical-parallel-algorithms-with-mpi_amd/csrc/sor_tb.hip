@@ -89,6 +89,11 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
+// a - 2c as one FMA: 2c is exact in binary floating point, so the single
+// rounding of fma(-2, c, a) equals the rounding of the reference's a - 2.0*c
+// (bit-exact, one VALU instruction instead of a multiply and a subtract)
+__device__ __forceinline__ double m2c(double a, double c) { return __builtin_fma(-2.0, c, a); }
+
 typedef double d2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ d2 ldv(const double* p) { return *reinterpret_cast<const d2*>(p); }
@@ -176,15 +181,15 @@ __device__ __forceinline__ d2 stage(const Lane& c, bool fixrows, d2 In, int rin,
         if (q == 0) {
             const double Lf = from_left(A.y);
             const double cc = A.x;
-            const double r = Ra.x - (((A.y - 2.0 * cc) + Lf) * idx2 +
-                                     ((In.x - 2.0 * cc) + M1.x) * idy2);
+            const double r = Ra.x - ((m2c(A.y, cc) + Lf) * idx2 +
+                                     (m2c(In.x, cc) + M1.x) * idy2);
             if (!EDGE || c.up_a) Mr.x = cc - coef * r;
             tally(r, own, c.own_a);
         } else {
             const double Rf = from_right(A.x);
             const double cc = A.y;
-            const double r = Ra.y - (((Rf - 2.0 * cc) + A.x) * idx2 +
-                                     ((In.y - 2.0 * cc) + M1.y) * idy2);
+            const double r = Ra.y - ((m2c(Rf, cc) + A.x) * idx2 +
+                                     (m2c(In.y, cc) + M1.y) * idy2);
             if (!EDGE || c.up_b) Mr.y = cc - coef * r;
             tally(r, own, c.own_b);
         }
@@ -197,15 +202,15 @@ __device__ __forceinline__ d2 stage(const Lane& c, bool fixrows, d2 In, int rin,
         if (q == 0) {
             const double Ln = from_left(M1.y);
             const double cc = M1.x;
-            const double r = Rb.x - (((M1.y - 2.0 * cc) + Ln) * idx2 +
-                                     ((Mr.x - 2.0 * cc) + M2.x) * idy2);
+            const double r = Rb.x - ((m2c(M1.y, cc) + Ln) * idx2 +
+                                     (m2c(Mr.x, cc) + M2.x) * idy2);
             if (!EDGE || c.up_a) F.x = cc - coef * r;
             tally(r, own, c.own_a);
         } else {
             const double Rn = from_right(M1.x);
             const double cc = M1.y;
-            const double r = Rb.y - (((Rn - 2.0 * cc) + M1.x) * idx2 +
-                                     ((Mr.y - 2.0 * cc) + M2.y) * idy2);
+            const double r = Rb.y - ((m2c(Rn, cc) + M1.x) * idx2 +
+                                     (m2c(Mr.y, cc) + M2.y) * idy2);
             if (!EDGE || c.up_b) F.y = cc - coef * r;
             tally(r, own, c.own_b);
         }
@@ -405,8 +410,8 @@ __global__ __launch_bounds__(kLanes* WAVES, MINW) void rb_tb_kernel(
     }
     const int bx = L % prm.nbx, by = L / prm.nbx;
     const int ni = prm.ni, nj = prm.nj;
-    const int j0 = 1 + by * prm.rows_per_block;
-    const int j1 = min(j0 + prm.rows_per_block, nj + 1);
+    const int j0 = 1 + (int)(((long long)by * nj) / prm.nby);
+    const int j1 = 1 + (int)(((long long)(by + 1) * nj) / prm.nby);
     if (prm.part != 0) {  // overlapped decomposed pass: blocks clear of the halo first
         const int lo = 1 + bx * WAVES * OW - 2 * T;
         const int hi = 1 + (bx * WAVES + WAVES - 1) * OW - 2 * T + kStripCells - 1;
@@ -528,12 +533,10 @@ int tb_out_width(int T) { return kStripCells - 4 * T; }
 
 int tb_waves(int variant) { return kTbVariants[variant].waves; }
 
-int tb_partials(int ni, int nj, int T, int rows_per_block, int waves, int* nbx, int* nby) {
+int tb_nbx(int ni, int T, int waves) {
     const int ow = tb_out_width(T);
     const int strips = (ni + ow - 1) / ow;
-    *nbx = (strips + waves - 1) / waves;
-    *nby = (nj + rows_per_block - 1) / rows_per_block;
-    return (*nbx) * (*nby);
+    return (strips + waves - 1) / waves;
 }
 
 void launch_tb(hipStream_t s, int T, const SweepParams& prm, const double* src, double* dst,

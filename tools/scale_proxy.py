@@ -32,10 +32,13 @@ def main():
     ap.add_argument("--base-ms", type=float, default=0.0,
                     help="N=1 ms per iteration to compute eff against (default: first row)")
     ap.add_argument("--tsteps", default="6", help="iterations per pass to try")
+    ap.add_argument("--lib", default="", help="load this libmisor.so instead (A/B runs)")
     ap.add_argument("--shapes", default="",
                     help="explicit local blocks NIxNJ[:N],... instead of the decomposition of --ranks")
     ap.add_argument("--variants", default="-1", help="TB variants to try (-1: default)")
     args = ap.parse_args()
+    if args.lib:
+        M.LIBPATH = os.path.abspath(args.lib)
     n = args.size
     combos = [(int(t), int(v), int(r)) for t in args.tsteps.split(",")
               for v in args.variants.split(",") for r in args.rows.split(",")]
@@ -60,12 +63,14 @@ def main():
         g.solve_rb(itermax=args.sweeps)  # warm-up
         v0 = g.get_tuning(M.TUNE_TB_VARIANT)
         res = {c: ([], []) for c in combos}
+        hrow = {}
         for _ in range(args.rounds):
             for c in combos:
                 T, v, r = c
                 g.set_tuning(M.TUNE_TSTEPS, T)
                 g.set_tuning(M.TUNE_TB_VARIANT, v0 if v < 0 else v)
                 g.set_tuning(M.TUNE_TB_ROWS, r)
+                hrow[c] = g.get_tuning(M.TUNE_TB_ROWS)
                 g.reset_stats()
                 g.synchronize()
                 t0 = time.perf_counter()
@@ -85,7 +90,7 @@ def main():
                 base = ms * N
             eff = base / (N * ms)
             print("%-2d %-12s %2d %2d %5d %10.4f %10.4f %10.0f %6.3f" % (
-                N, "%dx%d" % (ni, nj), T, v, r, ms, wall, mlups, eff), flush=True)
+                N, "%dx%d" % (ni, nj), T, v, hrow[c], ms, wall, mlups, eff), flush=True)
         g.close()
 
 

@@ -122,9 +122,9 @@ def cpu_baseline_multicore(n=8192, sweeps=40, reps=3):
                       "row bands (oracle/oracle_mt.c)" % (n, n, sweeps, reps, best, threads)}
 
 
-def pmc_traffic(size, nranks, T):
-    """HBM bytes per launch from the committed PMC summary, or None."""
-    best = None
+def pmc_summary(size, nranks, T):
+    """The committed PMC summary (tools/pmc_summary.py) for this size / ranks / T, or {}."""
+    best = {}
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
         try:
             d = json.load(open(path))
@@ -132,7 +132,7 @@ def pmc_traffic(size, nranks, T):
             continue
         if (d.get("size") == size and d.get("nranks", 1) == nranks
                 and d.get("iters_per_pass", 1) == T and "bytes_per_launch" in d):
-            best = d["bytes_per_launch"]
+            best = d
     return best
 
 
@@ -469,6 +469,7 @@ def main():
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9  # GB/s per GPU, algorithmic
     hbm_achieved = BYTES_PER_LUP * local_cells / (kern_ms * 1e-3) / 1e9
     dims = "%dx%d" % tuple(g.loc.dims)
+    pmc = pmc_summary(n, world, T)
     out = {
         "metric": "red-black SOR MLUP/s + % HBM roofline at 1/2/4/8 MI355X, 32768^2 grid",
         "value": round(mlups, 1),
@@ -489,13 +490,19 @@ def main():
                    "decomposition": dims, "baseline_config": 4},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / PEAK_GBS, 4),
-                     "traffic": pmc_traffic(n, world, T),
+                     "traffic": pmc.get("bytes_per_launch"),
                      "kernel": "rb_tb_kernel" if T > 1 else "rb_sweep_kernel",
                      "iters_per_launch": round(iters_launch, 3), "kernel_ms": round(kern_ms, 4),
                      "bytes_per_launch": bytes_launch,
                      "hbm_achieved": round(hbm_achieved, 1),
                      "hbm_frac": round(hbm_achieved / PEAK_GBS, 4)},
     }
+    if pmc.get("sq"):
+        # what actually bounds the temporally blocked kernel: VALU issue
+        # (SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES per wave, 2 waves per SIMD)
+        out["roofline"]["valu"] = {"insts_per_launch": pmc["sq"].get("valu_insts"),
+                                   "valu_busy_per_wave": pmc["sq"].get("active_inst_valu"),
+                                   "source": "profiles PMC summary, same size and T"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline()

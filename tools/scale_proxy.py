@@ -36,12 +36,14 @@ def main():
     ap.add_argument("--shapes", default="",
                     help="explicit local blocks NIxNJ[:N],... instead of the decomposition of --ranks")
     ap.add_argument("--variants", default="-1", help="TB variants to try (-1: default)")
+    ap.add_argument("--remap", default="1", help="XCD-aware block remap settings to try")
     args = ap.parse_args()
     if args.lib:
         M.LIBPATH = os.path.abspath(args.lib)
     n = args.size
-    combos = [(int(t), int(v), int(r)) for t in args.tsteps.split(",")
-              for v in args.variants.split(",") for r in args.rows.split(",")]
+    combos = [(int(t), int(v), int(r), int(x)) for t in args.tsteps.split(",")
+              for v in args.variants.split(",") for r in args.rows.split(",")
+              for x in args.remap.split(",")]
     base = args.base_ms or None
     print("%-2s %-12s %2s %2s %5s %10s %10s %10s %6s" % (
         "N", "local", "T", "v", "rows", "ms/iter", "wall/iter", "MLUP/s/GPU", "eff"), flush=True)
@@ -66,7 +68,8 @@ def main():
         hrow = {}
         for _ in range(args.rounds):
             for c in combos:
-                T, v, r = c
+                T, v, r, x = c
+                g.set_tuning(M.TUNE_XCD_REMAP, x)
                 g.set_tuning(M.TUNE_TSTEPS, T)
                 g.set_tuning(M.TUNE_TB_VARIANT, v0 if v < 0 else v)
                 g.set_tuning(M.TUNE_TB_ROWS, r)
@@ -82,15 +85,15 @@ def main():
                 res[c][0].append(st["sweep_ms"] / st["timed_sweeps"])
                 res[c][1].append(wall * 1e3 / st["timed_sweeps"])
         for c in combos:
-            T, v, r = c
+            T, v, r, x = c
             ms = float(np.median(res[c][0]))
             wall = float(np.median(res[c][1]))
             mlups = ni * nj / (ms * 1e-3) / 1e6
             if base is None:
                 base = ms * N
             eff = base / (N * ms)
-            print("%-2d %-12s %2d %2d %5d %10.4f %10.4f %10.0f %6.3f" % (
-                N, "%dx%d" % (ni, nj), T, v, hrow[c], ms, wall, mlups, eff), flush=True)
+            print("%-2d %-12s %2d %2d %5d %10.4f %10.4f %10.0f %6.3f  remap=%d" % (
+                N, "%dx%d" % (ni, nj), T, v, hrow[c], ms, wall, mlups, eff, x), flush=True)
         g.close()
 
 

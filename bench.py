@@ -372,7 +372,7 @@ def run_ns3d(args, world, rank, local_rank, dist, torch):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=70)
+    ap.add_argument("--steps", type=int, default=140)
     ap.add_argument("--warmup", type=int, default=7)
     ap.add_argument("--size", type=int, default=32768)
     ap.add_argument("--no-cpu-baseline", action="store_true")

@@ -310,34 +310,39 @@ __global__ __launch_bounds__(kLanes* WAVES) void rb_sweep_kernel(
 // A temporally blocked pass leaves T groups of partials (one per iteration);
 // they are decided in iteration order and the first failing test stops the
 // count, exactly as the reference loop would have stopped.
-__global__ __launch_bounds__(1024) void rb_finish_kernel(const double* __restrict__ partials,
-                                                         int n, int T, DevState* st,
-                                                         double cells, int decide) {
-    __shared__ double sh[kMaxT][1024];
+// 256 threads: while a temporally blocked pass keeps every SIMD's registers
+// full, a workgroup can only start where one of the sweep's workgroups has
+// just left -- which frees one wave per SIMD, so a 1024-thread finish (4 waves
+// per SIMD) could wait for a whole CU to drain; on the decomposed pipeline this
+// kernel runs on the comm stream beside the next pass's sweep.
+constexpr int kFinishThreads = 256;
+__global__ __launch_bounds__(kFinishThreads) void rb_finish_kernel(
+    const double* __restrict__ partials, int n, int T, DevState* st, double cells, int decide) {
+    constexpr int NT = kFinishThreads;
+    __shared__ double sh[kMaxT][NT];
     __shared__ double tot[kMaxT];
     if (st->done) return;
     const int t = threadIdx.x;
     // all T groups in one strided pass, four strides per trip with separate
-    // accumulators (4T independent loads in flight per thread: the partials of
-    // a 32768^2 pass are ~14k per group, and a 1-deep loop paid one memory
-    // latency per stride), combined in a fixed order
+    // accumulators (4T independent loads in flight per thread), combined in a
+    // fixed order
     double s[kMaxT], s1[kMaxT], s2[kMaxT], s3[kMaxT];
 #pragma unroll
     for (int g = 0; g < kMaxT; ++g) s[g] = s1[g] = s2[g] = s3[g] = 0.0;
     int k = t;
-    for (; k + 3 * 1024 < n; k += 4 * 1024) {
+    for (; k + 3 * NT < n; k += 4 * NT) {
 #pragma unroll
         for (int g = 0; g < kMaxT; ++g) {
             if (g < T) {
                 const double* q = partials + (long long)g * n + k;
                 s[g] += q[0];
-                s1[g] += q[1024];
-                s2[g] += q[2048];
-                s3[g] += q[3072];
+                s1[g] += q[NT];
+                s2[g] += q[2 * NT];
+                s3[g] += q[3 * NT];
             }
         }
     }
-    for (; k < n; k += 1024) {
+    for (; k < n; k += NT) {
 #pragma unroll
         for (int g = 0; g < kMaxT; ++g)
             if (g < T) s[g] += partials[(long long)g * n + k];
@@ -349,7 +354,7 @@ __global__ __launch_bounds__(1024) void rb_finish_kernel(const double* __restric
         if (g < T) sh[g][t] = s[g];
     __syncthreads();
 #pragma unroll
-    for (int w = 512; w >= 64; w >>= 1) {
+    for (int w = NT / 2; w >= 64; w >>= 1) {
         if (t < w) {
 #pragma unroll
             for (int g = 0; g < kMaxT; ++g)
@@ -419,20 +424,30 @@ void launch_sweep(hipStream_t s, const SweepParams& prm, const double* src, doub
 
 void launch_finish(hipStream_t s, const double* partials, int nparts, int T, DevState* st,
                    double cells, int decide) {
-    hipLaunchKernelGGL(rb_finish_kernel, dim3(1), dim3(1024), 0, s, partials, nparts, T, st,
+    hipLaunchKernelGGL(rb_finish_kernel, dim3(1), dim3(kFinishThreads), 0, s, partials, nparts, T, st,
                        cells, decide);
 }
 
 // decomposed runs: st->sum[0..T-1] hold the all-reduced sums r^2 of every rank
+// one thread; the state is read once and written once (it runs on the comm
+// stream beside a full sweep, where every dependent memory round trip is slow)
 __global__ void rb_decide_kernel(DevState* st, int T, double cells) {
-    for (int s_ = 0; s_ < T; ++s_) {
-        if (st->done) return;
-        const double res = st->sum[s_] / cells;
-        const int it = st->it + 1;
-        st->res = res;
-        st->it = it;
-        st->done = !((res >= st->epssq) && (it < st->itermax));
+    if (st->done) return;
+    double sum[kMaxT];
+#pragma unroll
+    for (int g = 0; g < kMaxT; ++g) sum[g] = g < T ? st->sum[g] : 0.0;
+    const double epssq = st->epssq;
+    const int itermax = st->itermax;
+    int it = st->it, done = 0;
+    double res = st->res;
+    for (int g = 0; g < T && !done; ++g) {
+        res = sum[g] / cells;
+        ++it;
+        done = !((res >= epssq) && (it < itermax));
     }
+    st->res = res;
+    st->it = it;
+    st->done = done;
 }
 
 void launch_decide(hipStream_t s, DevState* st, int T, double cells) {

@@ -37,10 +37,24 @@ def main():
                     help="explicit local blocks NIxNJ[:N],... instead of the decomposition of --ranks")
     ap.add_argument("--variants", default="-1", help="TB variants to try (-1: default)")
     ap.add_argument("--remap", default="1", help="XCD-aware block remap settings to try")
+    ap.add_argument("--no-timing", action="store_true", help="no per-pass HIP events (wall only)")
+    ap.add_argument("--torch-pg", action="store_true",
+                    help="also hold a one-rank torch.distributed NCCL process group (as bench.py "
+                         "does at N > 1)")
+    ap.add_argument("--comm", action="store_true",
+                    help="one-rank RCCL communicator: the decomposed, pipelined pass loop "
+                         "(comm stream, all-reduce, split launches) without neighbours")
     args = ap.parse_args()
     if args.lib:
         M.LIBPATH = os.path.abspath(args.lib)
     n = args.size
+    if args.torch_pg:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", init_method="tcp://127.0.0.1:29533", rank=0,
+                                world_size=1, device_id=torch.device("cuda", 0))
+        dist.barrier()
     combos = [(int(t), int(v), int(r), int(x)) for t in args.tsteps.split(",")
               for v in args.variants.split(",") for r in args.rows.split(",")
               for x in args.remap.split(",")]
@@ -59,9 +73,10 @@ def main():
             L = M.decompose(N, 0, n, n)
             cases.append((N, L.ni, L.nj))
     for N, ni, nj in cases:
-        g = M.Grid(ni, nj, 1.0 / n, 1.0 / n, 1.9, 1e-300, args.sweeps, device=0)
+        g = M.Grid(ni, nj, 1.0 / n, 1.0 / n, 1.9, 1e-300, args.sweeps, device=0,
+                   comm_id=M.comm_unique_id() if args.comm else None)
         g.poisson_init(1.0, 1.0, 2)
-        g.enable_timing(True)
+        g.enable_timing(not args.no_timing)
         g.solve_rb(itermax=args.sweeps)  # warm-up
         v0 = g.get_tuning(M.TUNE_TB_VARIANT)
         res = {c: ([], []) for c in combos}
@@ -82,12 +97,14 @@ def main():
                 wall = time.perf_counter() - t0
                 st = g.stats()
                 assert st["iters_per_pass"] == T
-                res[c][0].append(st["sweep_ms"] / st["timed_sweeps"])
-                res[c][1].append(wall * 1e3 / st["timed_sweeps"])
+                res[c][0].append(st["sweep_ms"] / max(st["timed_sweeps"], 1))
+                res[c][1].append(wall * 1e3 / args.sweeps)
         for c in combos:
             T, v, r, x = c
             ms = float(np.median(res[c][0]))
             wall = float(np.median(res[c][1]))
+            if ms <= 0:  # --no-timing: wall clock only
+                ms = wall
             mlups = ni * nj / (ms * 1e-3) / 1e6
             if base is None:
                 base = ms * N

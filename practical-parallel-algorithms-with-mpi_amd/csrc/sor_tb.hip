@@ -553,7 +553,9 @@ void launch_tb(hipStream_t s, int T, const SweepParams& prm, const double* src, 
     case 4: TB(TT, 4, 2, true, (TT <= 4 ? 4 : 1)); break; \
     case 5: TB(TT, 4, 3, true, 1); break;     \
     case 6: TB(TT, 8, 2, true, 1); break;     \
-    default: TB(TT, 6, 2, true, 1); break;    \
+    case 7: TB(TT, 6, 2, true, 1); break;     \
+    case 8: TB(TT, 2, 3, false, 1); break;    \
+    default: TB(TT, 1, 3, false, 1); break;   \
     }
     // must match kTbVariants (misor_internal.h)
     switch (T) {

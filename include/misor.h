@@ -195,8 +195,8 @@ enum {
                                     * iteration sweep kernel, T >= 2 = temporally blocked
                                     * kernel (T iterations per read of p and rhs); the
                                     * iteration count and every bit of p are unchanged */
-    MISOR_TUNE_TB_VARIANT = 7,     /* temporally blocked kernel: 0..9 strips x rows in flight
-                                    * x rhs ring in registers / LDS */
+    MISOR_TUNE_TB_VARIANT = 7,     /* temporally blocked kernel: 0..13 strips x rows in flight
+                                    * x rhs ring in registers / LDS / re-read from L2 */
     MISOR_TUNE_TB_ROWS = 8         /* temporally blocked kernel: rows per block; <= 0: auto */
 };
 int misor_set_tuning(misor_grid* g, int key, int value);

@@ -440,6 +440,13 @@ static int configure_tb(misor_grid* g, int T, int variant, int rows) {
     tp.nby = rows > 0 ? (g->loc.nj + rows - 1) / rows
                       : pick_tb_nby(g->loc.ni, g->loc.nj, Tg, tb_waves(variant));
     tp.rows_per_block = (g->loc.nj + tp.nby - 1) / tp.nby;
+    if (kTbVariants[variant].lds_ring >= 2 &&
+        (long long)(tp.rows_per_block + 4 * kMaxT + 4) * tp.pitch * 8 >= (1LL << 31)) {
+        // the rhs re-read variants address a block's rows with 32-bit buffer offsets
+        tp.variant = kDefaultTbVariant;
+        configure_tb(g, T, kDefaultTbVariant, rows);
+        return fail(MISOR_EINVAL, "tb variant %d: a block of rows exceeds 2 GiB", variant);
+    }
     tp.xcd_remap = g->sp.xcd_remap;
     const int Te = effective_tsteps(g);
     tb_geometry(g, Te, tp);

@@ -57,14 +57,17 @@ constexpr int kDefaultSweepVariant = 7;  // 8 strips, 2 rows ahead, nt stores (t
 int sweep_waves(int variant);
 
 // temporally blocked sweep (sor_tb.hip): strips per workgroup, rows in flight,
-// rhs ring in registers (0) or in LDS (1), minimum waves per SIMD (0: none)
+// rhs ring in registers (0), in LDS (1) or re-read from L2 by stages 1..K
+// (LR = K + 1 >= 2, the later stages keep the register ring),
+// minimum waves per SIMD (0: none)
 struct TbVariant {
     int waves, ahead, lds_ring, min_waves;
 };
 constexpr TbVariant kTbVariants[] = {{4, 2, 0, 0}, {8, 2, 0, 0}, {4, 3, 0, 0}, {4, 2, 1, 0},
                                      {4, 2, 1, 4}, {4, 3, 1, 0}, {8, 2, 1, 0}, {6, 2, 1, 0},
-                                     {2, 3, 0, 0}, {1, 3, 0, 0}};
-constexpr int kNumTbVariants = 10;
+                                     {2, 3, 0, 0}, {1, 3, 0, 0}, {4, 3, 8, 0}, {4, 3, 2, 0},
+                                     {4, 3, 3, 0}, {4, 3, 4, 0}};
+constexpr int kNumTbVariants = 14;
 constexpr int kDefaultTsteps = 7;      // iterations per pass (tools/scale_proxy.py, r01_shape_sweep)
 constexpr int kDefaultTbVariant = 2;   // 4 strips, 3 rows in flight, rhs ring in registers
 constexpr int kDefaultTbRows = 192;    // automatic rows per block (misor_api.hip pick_tb_rows)

@@ -229,10 +229,13 @@ __device__ __forceinline__ d2 stage(const Lane& c, bool fixrows, d2 In, int rin,
 }
 
 // the registers of one wave's march
-template <int T, int D, bool LR>
+template <int T, int D, int LR>
 struct March {
     d2 A[T], M1[T], M2[T];
-    d2 R[LR ? 1 : 2 * T];  // register rhs ring: R[k] = rhs(r0 - 1 - k)
+    // LR 0: register rhs ring, R[k] = rhs(r0 - 1 - k).  LR 2 (re-read): R[2t] =
+    // rhs(r0 - 2t - 1) for stage t >= 1, loaded during the previous step, and
+    // R[2t + 1] = rhs(r0 - 2t - 2), stage t's red row of the previous step
+    d2 R[LR == 1 ? 1 : 2 * T];
     d2 Pq[D], Rq[D];       // rows in flight: p(r0 .. r0+D-1), rhs(r0-1 .. r0+D-2)
     double acc[T];
 };
@@ -247,7 +250,17 @@ struct Io {
     // only what it wrote: no barrier), component-major so each wave access is
     // one contiguous 512-byte ds_*_b64.  Row x lives in slot x mod 2T.
     double* ring;
+    // re-read rhs (LR == 2): buffer descriptor whose base is row rlo of this
+    // wave's strip (wave-uniform), lane byte offset, row stride in bytes
+    __amdgpu_buffer_rsrc_t rrs;
+    int lane_off, rlo, row_bytes;
 };
+
+// LR >= 2: stages 1 .. K re-read their rhs rows (K = LR - 1, at most T - 1)
+template <int T, int LR>
+__device__ __forceinline__ constexpr int rr_stages() {
+    return LR - 1 < T - 1 ? LR - 1 : T - 1;
+}
 
 // slot of row x in a ring of 2T rows (x >= -kYOff - 2T - 1; scalar arithmetic)
 template <int T>
@@ -257,37 +270,55 @@ __device__ __forceinline__ int ring_slot(int x) {
 
 // one step of the march: stream in old row r0, push it through the T stages,
 // store the row the last stage finished (r0 - 2T) if this block owns it
-template <int T, int D, bool LR, bool NT, int Q, int MODE>
+template <int T, int D, int LR, bool NT, int Q, int MODE>
 __device__ __forceinline__ void tb_step(March<T, D, LR>& m, const Lane& c, const Io& io, int r0) {
     const long long pitch = io.pitch;
     const d2 nP = ldv(io.sp + (long long)(r0 + D) * pitch);
     const d2 nR = ldv(io.rp + (long long)(r0 - 1 + D) * pitch);
-    if (LR) {  // rhs(r0 - 1) joins the LDS ring
+    if (LR == 1) {  // rhs(r0 - 1) joins the LDS ring
         double* w = io.ring + ring_slot<T>(r0 - 1) * 128;
         w[0] = m.Rq[0].x;
         w[64] = m.Rq[0].y;
-    } else {
+    } else if (LR == 0) {
 #pragma unroll
         for (int k = 2 * T - 1; k > 0; --k) m.R[k] = m.R[k - 1];
         m.R[0] = m.Rq[0];
     }
 
     d2 v = m.Pq[0];
+    d2 Rk = d2{0.0, 0.0};  // LR >= 2: stage K's black rhs row, the ring's next newest
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         const d2 prevM2 = m.M2[t];
         d2 Ra, Rb;
-        if (LR) {  // only component q of rows r0-2t-1 (red) and r0-2t-2 (black) is used
+        if (LR == 1) {  // only component q of rows r0-2t-1 (red) and r0-2t-2 (black) is used
             const int q = Q >= 0 ? Q : ((c.parity + r0) & 1);
             const double ra = io.ring[ring_slot<T>(r0 - 2 * t - 1) * 128 + q * 64];
             const double rb = io.ring[ring_slot<T>(r0 - 2 * t - 2) * 128 + q * 64];
             Ra = d2{ra, ra};
             Rb = d2{rb, rb};
-        } else {
+        } else if (LR == 0) {
             Ra = m.R[2 * t];
             Rb = m.R[2 * t + 1];
+        } else {
+            Ra = t == 0 ? m.Rq[0] : m.R[2 * t];
+            Rb = m.R[2 * t + 1];
         }
+        constexpr int K = LR >= 2 ? rr_stages<T, LR>() : 0;
         v = stage<Q, MODE>(c, t > 0, v, r0 - 2 * t, m.A[t], m.M1[t], m.M2[t], Ra, Rb, m.acc[t]);
+        if (LR >= 2 && t <= K) {
+            // Rb is dead: its register takes next step's red row (loaded from L2:
+            // this wave streamed it 2t + D steps ago); rows below the stream
+            // start were zeros in the ring and only feed cells outside the cone
+            if (t == K) Rk = Rb;
+            m.R[2 * t + 1] = Ra;
+            if (t > 0) {
+                const int row = max(r0 - 2 * t, io.rlo);
+                m.R[2 * t] = __builtin_bit_cast(
+                    d2, __builtin_amdgcn_raw_buffer_load_b128(
+                            io.rrs, io.lane_off, (row - io.rlo) * io.row_bytes, 0));
+            }
+        }
         if (t == T - 1) {
             const int jw = r0 - 2 * T;  // row finished by the last stage
             if (MODE == kSteady) {
@@ -328,6 +359,14 @@ __device__ __forceinline__ void tb_step(March<T, D, LR>& m, const Lane& c, const
             }
         }
     }
+    if (LR >= 2) {
+        // stages K+1 .. T-1 keep the register ring, R[k] = rhs(r0 - 1 - k) for
+        // k >= 2K + 2 (shifted after every stage has read it)
+        constexpr int K = rr_stages<T, LR>();
+#pragma unroll
+        for (int k = 2 * T - 1; k > 2 * K + 2; --k) m.R[k] = m.R[k - 1];
+        if (K < T - 1) m.R[2 * K + 2] = Rk;
+    }
 #pragma unroll
     for (int k = 0; k + 1 < D; ++k) {
         m.Pq[k] = m.Pq[k + 1];
@@ -341,7 +380,7 @@ __device__ __forceinline__ void tb_step(March<T, D, LR>& m, const Lane& c, const
 // the colour a constant (Q0 = colour of row r0).  Steps r0 in
 // [j0+2T+1, j1-1] touch only owned rows and store unconditionally (kSteady);
 // the 4T+1 warm-up steps before and the 2T drain steps after are kWarm.
-template <int T, int D, bool LR, bool NT, int Q0>
+template <int T, int D, int LR, bool NT, int Q0>
 __device__ __forceinline__ void march_interior_q(March<T, D, LR>& m, const Lane& c,
                                                  const Io& io, int r0, int rend) {
     const int sbeg = c.j0 + 2 * T + 1, send = c.j1 - 1;
@@ -363,7 +402,7 @@ __device__ __forceinline__ void march_interior_q(March<T, D, LR>& m, const Lane&
 
 // Blocks with a physical side in their cone (kEdge / kRowEdge): every step
 // general, but still in colour pairs so the colour is a compile-time constant.
-template <int T, int D, bool LR, bool NT, int Q0, int MODE>
+template <int T, int D, int LR, bool NT, int Q0, int MODE>
 __device__ __forceinline__ void march_edge_q(March<T, D, LR>& m, const Lane& c, const Io& io,
                                              int r0, int rend) {
     for (; r0 + 1 <= rend; r0 += 2) {
@@ -373,7 +412,7 @@ __device__ __forceinline__ void march_edge_q(March<T, D, LR>& m, const Lane& c, 
     if (r0 <= rend) tb_step<T, D, LR, NT, Q0, MODE>(m, c, io, r0);
 }
 
-template <int T, int D, bool LR, bool NT, int MODE>
+template <int T, int D, int LR, bool NT, int MODE>
 __device__ __forceinline__ void march_edge(March<T, D, LR>& m, const Lane& c, const Io& io,
                                            int rs, int rend) {
     if (((c.parity + rs) & 1) == 0)
@@ -382,7 +421,7 @@ __device__ __forceinline__ void march_edge(March<T, D, LR>& m, const Lane& c, co
         march_edge_q<T, D, LR, NT, 1, MODE>(m, c, io, rs, rend);
 }
 
-template <int T, int D, bool LR, bool NT>
+template <int T, int D, int LR, bool NT>
 __device__ __forceinline__ void march_interior(March<T, D, LR>& m, const Lane& c, const Io& io,
                                                int rs, int rend) {
     if (((c.parity + rs) & 1) == 0)
@@ -393,14 +432,14 @@ __device__ __forceinline__ void march_interior(March<T, D, LR>& m, const Lane& c
 
 }  // namespace
 
-template <int T, int WAVES, int D, bool LR, int MINW, bool NT>
+template <int T, int WAVES, int D, int LR, int MINW, bool NT>
 __global__ __launch_bounds__(kLanes* WAVES, MINW) void rb_tb_kernel(
     SweepParams prm, const double* __restrict__ src, double* __restrict__ dst,
     const double* __restrict__ rhs, double* __restrict__ partials,
     const DevState* __restrict__ st, int force) {
     constexpr int OW = kStripCells - 4 * T;
     __shared__ double wsum[T][WAVES];
-    __shared__ double ring[LR ? WAVES : 1][LR ? 2 * T * kStripCells : 1];
+    __shared__ double ring[LR == 1 ? WAVES : 1][LR == 1 ? 2 * T * kStripCells : 1];
     if (!force && st->done) return;
 
     int L = blockIdx.x;
@@ -471,8 +510,8 @@ __global__ __launch_bounds__(kLanes* WAVES, MINW) void rb_tb_kernel(
 
     if (c_out <= ni) {  // wave-uniform
         const long long base = (long long)kYOff * pitch + kXOff + c.ia;
-        const Io io{src + base, rhs + base, dst + base, pitch,
-                    LR ? &ring[LR ? wave : 0][LR ? lane : 0] : nullptr};
+        Io io{src + base, rhs + base, dst + base, pitch,
+              LR == 1 ? &ring[LR == 1 ? wave : 0][LR == 1 ? lane : 0] : nullptr};
         const int rs = j0 - 2 * T;  // first streamed row
         const int rend = j1 - 1 + 2 * T;
 #pragma unroll
@@ -482,7 +521,21 @@ __global__ __launch_bounds__(kLanes* WAVES, MINW) void rb_tb_kernel(
         }
 #pragma unroll
         for (int t = 0; t < T; ++t) m.A[t] = m.M1[t] = m.M2[t] = d2{0.0, 0.0};
-        if (LR) {
+        if (LR >= 2) {
+            // wave-uniform descriptor over rows rs-1 .. rend of the strip's
+            // 128 columns (the base is made scalar explicitly)
+            io.rlo = rs - 1;
+            io.row_bytes = (int)(pitch * 8);
+            io.lane_off = lane * 16;
+            const long long off = ((long long)(kYOff + rs - 1) * pitch + kXOff + c_ld) * 8;
+            const unsigned long long a = (unsigned long long)(const char*)rhs + off;
+            const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+            const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+            const int nrec = (rend - rs + 2) * io.row_bytes;
+            io.rrs = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(((unsigned long long)hi << 32) | lo), (short)0, nrec, 0x00020000);
+        }
+        if (LR == 1) {
 #pragma unroll
             for (int k = 0; k < 4 * T; ++k) io.ring[k * 64] = 0.0;
         } else {
@@ -555,7 +608,11 @@ void launch_tb(hipStream_t s, int T, const SweepParams& prm, const double* src, 
     case 6: TB(TT, 8, 2, true, 1); break;     \
     case 7: TB(TT, 6, 2, true, 1); break;     \
     case 8: TB(TT, 2, 3, false, 1); break;    \
-    default: TB(TT, 1, 3, false, 1); break;   \
+    case 9: TB(TT, 1, 3, false, 1); break;    \
+    case 10: TB(TT, 4, 3, 8, 1); break;       \
+    case 11: TB(TT, 4, 3, 2, 1); break;       \
+    case 12: TB(TT, 4, 3, 3, 1); break;       \
+    default: TB(TT, 4, 3, 4, 1); break;       \
     }
     // must match kTbVariants (misor_internal.h)
     switch (T) {

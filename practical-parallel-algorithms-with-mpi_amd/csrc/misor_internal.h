@@ -66,8 +66,8 @@ struct TbVariant {
 constexpr TbVariant kTbVariants[] = {{4, 2, 0, 0}, {8, 2, 0, 0}, {4, 3, 0, 0}, {4, 2, 1, 0},
                                      {4, 2, 1, 4}, {4, 3, 1, 0}, {8, 2, 1, 0}, {6, 2, 1, 0},
                                      {2, 3, 0, 0}, {1, 3, 0, 0}, {4, 3, 8, 0}, {4, 3, 2, 0},
-                                     {4, 3, 3, 0}, {4, 3, 4, 0}};
-constexpr int kNumTbVariants = 14;
+                                     {4, 3, 3, 0}, {4, 3, 4, 0}, {4, 3, 0, 0}};
+constexpr int kNumTbVariants = 15;  // 14: as 2, branch-free steady stores
 constexpr int kDefaultTsteps = 7;      // iterations per pass (tools/scale_proxy.py, r01_shape_sweep)
 constexpr int kDefaultTbVariant = 2;   // 4 strips, 3 rows in flight, rhs ring in registers
 constexpr int kDefaultTbRows = 192;    // automatic rows per block (misor_api.hip pick_tb_rows)

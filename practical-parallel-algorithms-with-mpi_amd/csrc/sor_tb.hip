@@ -95,6 +95,7 @@ __device__ __forceinline__ double wave_sum(double v) {
 __device__ __forceinline__ double m2c(double a, double c) { return __builtin_fma(-2.0, c, a); }
 
 typedef double d2 __attribute__((ext_vector_type(2)));
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ d2 ldv(const double* p) { return *reinterpret_cast<const d2*>(p); }
 
@@ -254,6 +255,11 @@ struct Io {
     // wave's strip (wave-uniform), lane byte offset, row stride in bytes
     __amdgpu_buffer_rsrc_t rrs;
     int lane_off, rlo, row_bytes;
+    // steady-state stores (SST variants): the strip's 128 columns of row 0 of
+    // dst as a wave-uniform address, and this lane's byte offset in a row, out
+    // of range (the store is dropped) on lanes that do not store
+    unsigned long long dwave;
+    unsigned st_off;
 };
 
 // LR >= 2: stages 1 .. K re-read their rhs rows (K = LR - 1, at most T - 1)
@@ -270,8 +276,10 @@ __device__ __forceinline__ int ring_slot(int x) {
 
 // one step of the march: stream in old row r0, push it through the T stages,
 // store the row the last stage finished (r0 - 2T) if this block owns it
-template <int T, int D, int LR, bool NT, int Q, int MODE>
+template <int T, int D, int LR, int NT, int Q, int MODE>
 __device__ __forceinline__ void tb_step(March<T, D, LR>& m, const Lane& c, const Io& io, int r0) {
+    // NT bit 0: non-temporal stores; bit 1: branch-free steady-state stores
+    constexpr bool SST = (NT & 2) != 0;
     const long long pitch = io.pitch;
     const d2 nP = ldv(io.sp + (long long)(r0 + D) * pitch);
     const d2 nR = ldv(io.rp + (long long)(r0 - 1 + D) * pitch);
@@ -321,24 +329,32 @@ __device__ __forceinline__ void tb_step(March<T, D, LR>& m, const Lane& c, const
         }
         if (t == T - 1) {
             const int jw = r0 - 2 * T;  // row finished by the last stage
-            if (MODE == kSteady) {
-                if (c.st_a) stv<NT>(io.dp + (long long)jw * pitch, v);
+            if (MODE == kSteady && SST) {
+                // no branch around the store: the two steps of a colour pair stay one
+                // basic block, which the scheduler can interleave
+                const unsigned long long a = io.dwave + (unsigned long long)jw * (pitch * 8);
+                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                    (void*)a, (short)0, kStripCells * 8, 0x00020000);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), rs, io.st_off,
+                                                       0, (NT & 1) ? 2 : 0);
+            } else if (MODE == kSteady) {
+                if (c.st_a) stv<(NT & 1) != 0>(io.dp + (long long)jw * pitch, v);
             } else if (MODE == kWarm) {
-                if (jw >= c.j0 && jw < c.j1 && c.st_a) stv<NT>(io.dp + (long long)jw * pitch, v);
+                if (jw >= c.j0 && jw < c.j1 && c.st_a) stv<(NT & 1) != 0>(io.dp + (long long)jw * pitch, v);
             } else if (MODE == kRowEdge) {
                 // every column of the lane updated and stored alike (st_a == st_b);
                 // ghost rows 0 / nj+1 of the stored field are copies of rows 1 / nj
                 if (jw >= c.j0 && jw < c.j1 && c.st_a) {
                     double* drow = io.dp + (long long)jw * pitch;
-                    stv<NT>(drow, v);
-                    if (c.gb && jw == 1) stv<NT>(drow - pitch, v);
-                    if (c.gt && jw == c.nj) stv<NT>(drow + pitch, v);
+                    stv<(NT & 1) != 0>(drow, v);
+                    if (c.gb && jw == 1) stv<(NT & 1) != 0>(drow - pitch, v);
+                    if (c.gt && jw == c.nj) stv<(NT & 1) != 0>(drow + pitch, v);
                 }
             } else if (jw >= c.j0 && jw < c.j1) {
                 double* drow = io.dp + (long long)jw * pitch;
                 auto put = [&](double* p, d2 o) {
                     if (c.st_a && c.st_b) {
-                        stv<NT>(p, o);
+                        stv<(NT & 1) != 0>(p, o);
                     } else if (c.st_a) {
                         p[0] = o.x;
                     } else if (c.st_b) {
@@ -380,7 +396,7 @@ __device__ __forceinline__ void tb_step(March<T, D, LR>& m, const Lane& c, const
 // the colour a constant (Q0 = colour of row r0).  Steps r0 in
 // [j0+2T+1, j1-1] touch only owned rows and store unconditionally (kSteady);
 // the 4T+1 warm-up steps before and the 2T drain steps after are kWarm.
-template <int T, int D, int LR, bool NT, int Q0>
+template <int T, int D, int LR, int NT, int Q0>
 __device__ __forceinline__ void march_interior_q(March<T, D, LR>& m, const Lane& c,
                                                  const Io& io, int r0, int rend) {
     const int sbeg = c.j0 + 2 * T + 1, send = c.j1 - 1;
@@ -402,7 +418,7 @@ __device__ __forceinline__ void march_interior_q(March<T, D, LR>& m, const Lane&
 
 // Blocks with a physical side in their cone (kEdge / kRowEdge): every step
 // general, but still in colour pairs so the colour is a compile-time constant.
-template <int T, int D, int LR, bool NT, int Q0, int MODE>
+template <int T, int D, int LR, int NT, int Q0, int MODE>
 __device__ __forceinline__ void march_edge_q(March<T, D, LR>& m, const Lane& c, const Io& io,
                                              int r0, int rend) {
     for (; r0 + 1 <= rend; r0 += 2) {
@@ -412,7 +428,7 @@ __device__ __forceinline__ void march_edge_q(March<T, D, LR>& m, const Lane& c, 
     if (r0 <= rend) tb_step<T, D, LR, NT, Q0, MODE>(m, c, io, r0);
 }
 
-template <int T, int D, int LR, bool NT, int MODE>
+template <int T, int D, int LR, int NT, int MODE>
 __device__ __forceinline__ void march_edge(March<T, D, LR>& m, const Lane& c, const Io& io,
                                            int rs, int rend) {
     if (((c.parity + rs) & 1) == 0)
@@ -421,7 +437,7 @@ __device__ __forceinline__ void march_edge(March<T, D, LR>& m, const Lane& c, co
         march_edge_q<T, D, LR, NT, 1, MODE>(m, c, io, rs, rend);
 }
 
-template <int T, int D, int LR, bool NT>
+template <int T, int D, int LR, int NT>
 __device__ __forceinline__ void march_interior(March<T, D, LR>& m, const Lane& c, const Io& io,
                                                int rs, int rend) {
     if (((c.parity + rs) & 1) == 0)
@@ -432,7 +448,7 @@ __device__ __forceinline__ void march_interior(March<T, D, LR>& m, const Lane& c
 
 }  // namespace
 
-template <int T, int WAVES, int D, int LR, int MINW, bool NT>
+template <int T, int WAVES, int D, int LR, int MINW, int NT>
 __global__ __launch_bounds__(kLanes* WAVES, MINW) void rb_tb_kernel(
     SweepParams prm, const double* __restrict__ src, double* __restrict__ dst,
     const double* __restrict__ rhs, double* __restrict__ partials,
@@ -521,6 +537,14 @@ __global__ __launch_bounds__(kLanes* WAVES, MINW) void rb_tb_kernel(
         }
 #pragma unroll
         for (int t = 0; t < T; ++t) m.A[t] = m.M1[t] = m.M2[t] = d2{0.0, 0.0};
+        if (NT & 2) {
+            const unsigned long long a =
+                (unsigned long long)(dst + (long long)kYOff * pitch + kXOff + c_ld);
+            const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+            const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+            io.dwave = ((unsigned long long)hi << 32) | lo;
+            io.st_off = c.st_a ? (unsigned)lane * 16u : 0x80000000u;
+        }
         if (LR >= 2) {
             // wave-uniform descriptor over rows rs-1 .. rend of the strip's
             // 128 columns (the base is made scalar explicitly)
@@ -597,6 +621,9 @@ void launch_tb(hipStream_t s, int T, const SweepParams& prm, const double* src, 
 #define TB(TT, W, DD, LR, MW)                                                  \
     hipLaunchKernelGGL((rb_tb_kernel<TT, W, DD, LR, MW, true>), dim3(prm.nblocks), \
                        dim3(kLanes * W), 0, s, prm, src, dst, rhs, partials, st, force)
+#define TBN(TT, W, DD, LR, MW, NTF)                                           \
+    hipLaunchKernelGGL((rb_tb_kernel<TT, W, DD, LR, MW, NTF>), dim3(prm.nblocks), \
+                       dim3(kLanes * W), 0, s, prm, src, dst, rhs, partials, st, force)
 #define TB_T(TT)                              \
     switch (prm.variant) {                    \
     case 0: TB(TT, 4, 2, false, 1); break;    \
@@ -609,6 +636,7 @@ void launch_tb(hipStream_t s, int T, const SweepParams& prm, const double* src, 
     case 7: TB(TT, 6, 2, true, 1); break;     \
     case 8: TB(TT, 2, 3, false, 1); break;    \
     case 9: TB(TT, 1, 3, false, 1); break;    \
+    case 14: TBN(TT, 4, 3, 0, 1, 3); break;   \
     case 10: TB(TT, 4, 3, 8, 1); break;       \
     case 11: TB(TT, 4, 3, 2, 1); break;       \
     case 12: TB(TT, 4, 3, 3, 1); break;       \
@@ -626,6 +654,7 @@ void launch_tb(hipStream_t s, int T, const SweepParams& prm, const double* src, 
     default: TB_T(8); break;
     }
 #undef TB_T
+#undef TBN
 #undef TB
 }
 

@@ -185,7 +185,7 @@ def test_large_grid_few_sweeps(k):
 
 
 @pytest.mark.parametrize("T", [2, 3, 4, 5, 6, 7])
-@pytest.mark.parametrize("variant", range(14))
+@pytest.mark.parametrize("variant", range(15))
 def test_tb_converges_mid_pass(T, variant):
     """convergence inside a temporally blocked pass: the pass is recomputed
     with fewer iterations, so the count and p equal solveRB's for every T"""

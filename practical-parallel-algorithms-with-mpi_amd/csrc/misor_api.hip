@@ -116,6 +116,7 @@ struct misor_grid {
     SweepParams sp{};
     int nbx = 0, nby = 0, nparts = 0, partials_cap = 0;
     double* partials = nullptr;  // two slots of partials_cap doubles (by pass parity)
+    bool finish2 = true;  // single rank: two-level loop test (MISOR_FINISH2=0: one kernel)
     DevState* st = nullptr;
     DevState* st_host = nullptr;  // pinned
     int last_iters = 0;
@@ -369,7 +370,9 @@ static int ensure_partials(misor_grid* g, int n) {
     if (g->partials) (void)hipFree(g->partials);
     g->partials = nullptr;
     g->partials_cap = 0;
-    if (hipMalloc(&g->partials, sizeof(double) * 2 * (size_t)n) != hipSuccess)
+    // two slots of n (by pass parity) + the two-level finish's chunk sums
+    if (hipMalloc(&g->partials, sizeof(double) * (2 * (size_t)n + kMaxT * kFinishChunks)) !=
+        hipSuccess)
         return fail(MISOR_ENOMEM, "partials allocation failed");
     g->partials_cap = n;
     return MISOR_OK;
@@ -620,6 +623,10 @@ int misor_create(misor_grid** out, const misor_desc* d) {
             if (ncclCommInitRank(&g->comm, nranks, id, d->rank) != ncclSuccess)
                 CREATE_FAIL(MISOR_ECOMM, "ncclCommInitRank failed");
         }
+    }
+    {
+        const char* e = getenv("MISOR_FINISH2");
+        g->finish2 = !(e && e[0] == '0');
     }
     if (configure_tb(g, kDefaultTsteps, kDefaultTbVariant, 0) != MISOR_OK)
         CREATE_FAIL(MISOR_ENOMEM, "%s", g_err.c_str());
@@ -1081,6 +1088,9 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
                 int rc = allreduce(g, g->st->sum, Tk, 0);
                 if (rc) return rc;
                 launch_decide(g->stream, g->st, Tk, cells);
+            } else if (g->finish2) {
+                launch_finish2(g->stream, g->partials, nparts_of(Tk), Tk, g->st, cells,
+                               g->partials + 2 * (long long)g->partials_cap);
             } else {
                 launch_finish(g->stream, g->partials, nparts_of(Tk), Tk, g->st, cells, 1);
             }

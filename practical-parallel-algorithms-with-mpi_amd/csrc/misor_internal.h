@@ -123,6 +123,11 @@ void launch_sweep(hipStream_t s, const SweepParams& prm, const double* src, doub
 void launch_finish(hipStream_t s, const double* partials, int nparts, int T, DevState* st,
                    double cells, int decide);
 void launch_decide(hipStream_t s, DevState* st, int T, double cells);
+// single-rank loop test in two levels (chunk sums, then the finish kernel over
+// kFinishChunks values per stage); scratch holds kMaxT * kFinishChunks doubles
+constexpr int kFinishChunks = 32;
+void launch_finish2(hipStream_t s, const double* partials, int nparts, int T, DevState* st,
+                    double cells, double* scratch);
 void launch_tb(hipStream_t s, int T, const SweepParams& prm, const double* src, double* dst,
                const double* rhs, double* partials, const DevState* st, int force);
 // lexicographic Gauss-Seidel SOR, whole solve in one workgroup (lex_kernels.hip)

@@ -386,6 +386,47 @@ __global__ __launch_bounds__(kFinishThreads) void rb_finish_kernel(
     }
 }
 
+// Single-rank loop test, first level: workgroup (c, g) sums chunk c of stage
+// g's per-workgroup partials in a fixed order (strided by thread, then a
+// tree), so the finish kernel reads kFinishChunks values per stage instead of
+// one per sweep workgroup (14k at 32768^2: 65 -> ~10 us per pass)
+__global__ __launch_bounds__(256) void rb_partsum_kernel(const double* __restrict__ partials,
+                                                         int n, const DevState* __restrict__ st,
+                                                         double* __restrict__ out) {
+    __shared__ double sh[256];
+    if (st->done) return;
+    const int c = blockIdx.x, g = blockIdx.y, t = threadIdx.x;
+    const int lo = (int)((long long)n * c / kFinishChunks);
+    const int hi = (int)((long long)n * (c + 1) / kFinishChunks);
+    const double* q = partials + (long long)g * n;
+    double s0 = 0.0, s1 = 0.0;
+    int k = lo + t;
+    for (; k + 256 < hi; k += 512) {
+        s0 += q[k];
+        s1 += q[k + 256];
+    }
+    if (k < hi) s0 += q[k];
+    sh[t] = s0 + s1;
+    __syncthreads();
+#pragma unroll
+    for (int w = 128; w >= 64; w >>= 1) {
+        if (t < w) sh[t] += sh[t + w];
+        __syncthreads();
+    }
+    if (t < 64) {
+        const double v = wave_sum(sh[t]);
+        if (t == 0) out[g * kFinishChunks + c] = v;
+    }
+}
+
+void launch_finish2(hipStream_t s, const double* partials, int nparts, int T, DevState* st,
+                    double cells, double* scratch) {
+    hipLaunchKernelGGL(rb_partsum_kernel, dim3(kFinishChunks, T), dim3(256), 0, s, partials,
+                       nparts, st, scratch);
+    hipLaunchKernelGGL(rb_finish_kernel, dim3(1), dim3(kFinishThreads), 0, s, scratch,
+                       kFinishChunks, T, st, cells, 1);
+}
+
 int sweep_waves(int variant) { return kSweepVariants[variant].waves; }
 
 int sweep_partials(int ni, int nj, int rows_per_block, int waves, int* nbx, int* nby) {

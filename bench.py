@@ -15,20 +15,25 @@ region; the timed region is K iterations, barrier + device sync on both
 sides, max over ranks.  Rank 0 prints ONE JSON line.
 
 A launch (a "pass") of the default temporally blocked kernel performs T
-complete iterations (sor_tb.hip; T = iters_per_pass, default 6): it reads p
-and rhs once and writes p once per T iterations.
+complete iterations (sor_tb.hip; T = iters_per_pass): it reads p and rhs once
+and writes p once per T iterations.
 
-roofline: algorithmic bytes per launch = 24 B per lattice update (read p,
-read rhs, write p: SURVEY 8d) x local cells x T, divided by the kernel's
-average launch duration measured with HIP events recorded around every pass
-on the library's stream (misor_enable_timing).  peak = 8000 GB/s (MI355X HBM3E
-spec, MI355X_MICROARCH.md).  Because one launch does T iterations for one
-read/write of the fields, frac can exceed 1: it is the iteration-equivalent
-(algorithmic) rate.  hbm_achieved = the bytes one launch must move (24 B x
-cells, its own minimum) / launch time, i.e. the kernel's real HBM rate.
+roofline (the binding roof, frac <= 1): the algorithmic HBM bytes of ONE pass
+are 24 B per cell (read p, read rhs, write p: SURVEY 8d's 24 B/LUP with the
+T iterations of the pass sharing one read/write of the fields), so achieved =
+24 B x local cells / the kernel's average launch duration, measured with HIP
+events recorded around every pass on the library's stream
+(misor_enable_timing); peak = 8000 GB/s (MI355X HBM3E, MI355X_MICROARCH.md).
 traffic = HBM bytes per launch from the PMC profile committed under profiles/
-for this configuration and T (FETCH_SIZE x 2 + WRITE_SIZE, the gfx950
-correction of MI355X_MICROARCH.md §HBM), or null.
+for this size and T (FETCH_SIZE x 2 + WRITE_SIZE, the gfx950 correction of
+MI355X_MICROARCH.md), or null.  floors_ms: the launch's HBM floor (24 B x
+cells at 8 TB/s) and its FP64 VALU floor (11 FP64 operations per lattice
+update at 16 lanes/clk/SIMD x 1024 SIMDs x 2.4 GHz).  The iteration-equivalent
+rate (24 B/LUP x T iterations / launch time, > 8 TB/s because T iterations
+share one pass) is reported separately under iteration_equivalent.
+
+Warm-up: besides --warmup iterations, every kernel instantiation the timed
+region launches (T and the remainder steps % T) runs once before timing.
 
 cpu_baseline: the reference's own solveRB (assignment-4/src/solver.c:179-238,
 compiled in place by oracle/Makefile into oracle/_ref/libref.so) on one host
@@ -437,8 +442,11 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    if args.warmup > 0:
-        g.solve_rb(itermax=args.warmup)
+    # warm-up: --warmup iterations, then every instantiation the timed solve
+    # launches (full passes of T and the last pass of steps % T)
+    g.solve_rb(itermax=max(args.warmup, 1))
+    T_eff = g.stats()["iters_per_pass"] or 1
+    g.solve_rb(itermax=T_eff + args.steps % T_eff)
     g.enable_timing(True)
     g.reset_stats()
     barrier()
@@ -465,11 +473,14 @@ def main():
 
     total_lup = float(n) * float(n) * args.steps
     mlups = total_lup / elapsed / 1e6
-    bytes_launch = BYTES_PER_LUP * local_cells * iters_launch
-    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9  # GB/s per GPU, algorithmic
-    hbm_achieved = BYTES_PER_LUP * local_cells / (kern_ms * 1e-3) / 1e9
+    # one pass moves at least p in, rhs in, p out: 24 B per local cell
+    hbm_min = BYTES_PER_LUP * local_cells
+    achieved = hbm_min / (kern_ms * 1e-3) / 1e9  # GB/s per GPU
+    iter_eq = hbm_min * iters_launch / (kern_ms * 1e-3) / 1e9
+    fp64_floor_ms = 11.0 * local_cells * iters_launch / (16 * 1024 * 2.4e9) * 1e3
     dims = "%dx%d" % tuple(g.loc.dims)
     pmc = pmc_summary(n, world, T)
+    traffic = pmc.get("bytes_per_launch")
     out = {
         "metric": "red-black SOR MLUP/s + % HBM roofline at 1/2/4/8 MI355X, 32768^2 grid",
         "value": round(mlups, 1),
@@ -490,12 +501,17 @@ def main():
                    "decomposition": dims, "baseline_config": 4},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / PEAK_GBS, 4),
-                     "traffic": pmc.get("bytes_per_launch"),
+                     "traffic": traffic,
+                     "traffic_ratio": round(traffic / hbm_min, 4) if traffic else None,
                      "kernel": "rb_tb_kernel" if T > 1 else "rb_sweep_kernel",
                      "iters_per_launch": round(iters_launch, 3), "kernel_ms": round(kern_ms, 4),
-                     "bytes_per_launch": bytes_launch,
-                     "hbm_achieved": round(hbm_achieved, 1),
-                     "hbm_frac": round(hbm_achieved / PEAK_GBS, 4)},
+                     "bytes_per_launch": hbm_min,
+                     "floors_ms": {"hbm": round(hbm_min / (PEAK_GBS * 1e9) * 1e3, 4),
+                                   "fp64_valu": round(fp64_floor_ms, 4)},
+                     "iteration_equivalent": {
+                         "GBs": round(iter_eq, 1), "per_lup_bytes": BYTES_PER_LUP,
+                         "note": "24 B/LUP x iterations per launch / launch time; exceeds "
+                                 "the HBM peak because one pass carries T iterations"}},
     }
     if pmc.get("sq"):
         # what actually bounds the temporally blocked kernel: VALU issue
@@ -512,6 +528,10 @@ def main():
             out["cpu_baseline_multicore"] = cpu_baseline_multicore()
         except Exception as e:
             out["cpu_baseline_multicore"] = {"value": None, "error": repr(e)}
+        for key in ("cpu_baseline", "cpu_baseline_multicore"):
+            cb = out[key]
+            out["config"][key + "_sample"] = "%s; %s cores (%s)" % (
+                cb.get("sample"), cb.get("cores"), cb.get("kind"))
     g.close()
     if dist is not None:
         dist.barrier()

@@ -8,6 +8,7 @@
 #include <time.h>
 #include <unistd.h>
 
+#include "comm_file.h"
 #include "util.h"
 
 static __thread const RankCtx* tls_ctx;
@@ -36,42 +37,38 @@ static int env_int(const char* name, int dflt)
     return (s && *s) ? atoi(s) : dflt;
 }
 
-/* rank 0 writes the id (tmp file + rename: readers never see a partial id) */
+/* the communicator id of this launch: rank 0 creates and publishes it, the
+ * others read it (comm_file.h); rank 0 removes the file when the program ends */
+static char comm_path[1024];
+
+static void remove_comm_file(void) { unlink(comm_path); }
+
 static void publish_or_fetch_id(int rank, int world, char* id)
 {
-    char path[512], tmp[600];
-    const char* f = getenv("MISOR_COMM_FILE");
-    if (f && *f)
-        snprintf(path, sizeof path, "%s", f);
-    else
-        snprintf(path, sizeof path, "/tmp/misor_comm_%d.id", world);
+    char tag[COMM_TAG_BYTES];
+    if (commFileTag(tag, sizeof tag) != 0) {
+        if (!getenv("MISOR_COMM_FILE")) {
+            printf("Error: WORLD_SIZE > 1 needs MASTER_PORT, TORCHELASTIC_RUN_ID, MISOR_RUN_TAG "
+                   "or MISOR_COMM_FILE to tell this launch apart\n");
+            exit(EXIT_FAILURE);
+        }
+        snprintf(tag, sizeof tag, "file");
+    }
+    commFilePath(world, tag, comm_path, sizeof comm_path);
     if (rank == 0) {
+        unlink(comm_path); /* a file left by a crashed launch with the same tag */
         misorCheck(misor_comm_unique_id(id), "misor_comm_unique_id");
-        snprintf(tmp, sizeof tmp, "%s.%d.tmp", path, (int)getpid());
-        FILE* fp = fopen(tmp, "wb");
-        if (!fp || fwrite(id, 1, MISOR_COMM_ID_BYTES, fp) != MISOR_COMM_ID_BYTES) {
-            printf("Error: cannot write %s\n", tmp);
+        if (commFilePublish(comm_path, tag, id, MISOR_COMM_ID_BYTES) != 0) {
+            printf("Error: cannot publish %s\n", comm_path);
             exit(EXIT_FAILURE);
         }
-        fclose(fp);
-        if (rename(tmp, path) != 0) {
-            printf("Error: cannot publish %s\n", path);
-            exit(EXIT_FAILURE);
-        }
+        atexit(remove_comm_file);
         return;
     }
-    for (int tries = 0; tries < 1200; ++tries) { /* up to 60 s */
-        FILE* fp = fopen(path, "rb");
-        if (fp) {
-            size_t n = fread(id, 1, MISOR_COMM_ID_BYTES, fp);
-            fclose(fp);
-            if (n == MISOR_COMM_ID_BYTES) return;
-        }
-        struct timespec ts = { 0, 50000000 };
-        nanosleep(&ts, NULL);
+    if (commFileFetch(comm_path, tag, id, MISOR_COMM_ID_BYTES, 60.0) != 0) {
+        printf("Error: no communicator id for launch %s in %s\n", tag, comm_path);
+        exit(EXIT_FAILURE);
     }
-    printf("Error: no communicator id in %s\n", path);
-    exit(EXIT_FAILURE);
 }
 
 int runRanks(int (*fn)(const RankCtx*, void*), void* arg)

@@ -9,8 +9,8 @@
  *     on GPU r % device_count, so one process drives all GPUs of a node), or
  *   - a process per rank started by a launcher that sets WORLD_SIZE, RANK and
  *     LOCAL_RANK (torchrun style): RCCL between the processes, rank 0
- *     publishes the communicator id in the file MISOR_COMM_FILE
- *     (default /tmp/misor_comm_<WORLD_SIZE>.id).
+ *     publishes the communicator id in a file tagged with the launch
+ *     (comm_file.h: MISOR_COMM_FILE, default /tmp/misor_comm_<WORLD_SIZE>_<tag>.id).
  * With neither set the program is the single-GPU one.
  */
 #ifndef MISOR_HOST_RANKS_H

@@ -69,7 +69,7 @@ def assemble(parts, shape):
                                         (4, (1, 4)), (6, (0, 0)), (8, (0, 0))])
 @pytest.mark.parametrize("ni,nj,k", [(61, 43, 5), (300, 257, 3), (2100, 90, 2)])
 @pytest.mark.parametrize("overlap", [1, 0], ids=["overlap", "serial"])
-@pytest.mark.parametrize("T", [1, 2, 4, 6], ids=["t1", "t2", "t4", "t6"])
+@pytest.mark.parametrize("T", [1, 2, 4, 6, 7], ids=["t1", "t2", "t4", "t6", "t7"])
 def test_fixed_sweeps_partition_independent(world, dims, ni, nj, k, overlap, T):
     rng = np.random.default_rng(ni + 31 * nj + world)
     p = rng.standard_normal((nj + 2, ni + 2))

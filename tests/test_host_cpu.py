@@ -118,3 +118,37 @@ def test_reader_known_values(golden):
     assert float(d["xlength"]) == 30.0 and int(d["bcLeft"]) == 3 and int(d["itermax"]) == 500
     d = dump(os.path.join(golden, "a4_poisson.par"), poisson=True)
     assert float(d["omg"]) == 1.9 and int(d["itermax"]) == 1000000 and float(d["eps"]) == 1e-6
+
+
+COMM_FILE = os.path.join(ROOT, "practical-parallel-algorithms-with-mpi_amd", "bin", "comm-file")
+
+
+@pytest.mark.parametrize("fetch_first", [True, False])
+def test_comm_id_file_two_launches_in_a_row(tmp_path, fetch_first):
+    """The RCCL id handshake of WORLD_SIZE > 1 launches (host/comm_file.c):
+    two launches in a row with the same tag each hand their own id to the
+    other ranks -- a reader never takes a file left by the previous launch
+    (rank 0 removes it at the end and rewrites it atomically at the start),
+    and a file of another launch tag is ignored"""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT="29511")
+    env.pop("MISOR_COMM_FILE", None)
+    env.pop("TORCHELASTIC_RUN_ID", None)
+    env.pop("MISOR_RUN_TAG", None)
+    # a stale file of ANOTHER launch at the same path must never be read
+    stale = b"MISORID1" + b"other-launch".ljust(96, b"\0") + b"stale-id".ljust(128, b"\0")
+    (tmp_path / "x.id").write_bytes(stale)
+    env["MISOR_COMM_FILE"] = str(tmp_path / "x.id")
+    for launch in ("first-id", "second-id"):
+        readers = []
+        if fetch_first:
+            readers = [subprocess.Popen([COMM_FILE, "fetch", "3", str(k)], env=env,
+                                        stdout=subprocess.PIPE) for k in (1, 2)]
+        pub = subprocess.Popen([COMM_FILE, "publish", "3", launch, "2"], env=env)
+        if not fetch_first:
+            readers = [subprocess.Popen([COMM_FILE, "fetch", "3", str(k)], env=env,
+                                        stdout=subprocess.PIPE) for k in (1, 2)]
+        outs = [r.communicate(timeout=30)[0].decode().strip() for r in readers]
+        assert pub.wait(timeout=30) == 0
+        assert all(r.returncode == 0 for r in readers)
+        assert outs == [launch, launch]
+        assert not os.path.exists(env["MISOR_COMM_FILE"])

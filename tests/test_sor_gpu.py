@@ -38,8 +38,8 @@ def make_grid(ni, nj, xl=1.0, yl=1.0, omega=OMEGA, eps=EPS, itermax=1000000,
     return set_mode(g, small)
 
 
-PATHS = pytest.mark.parametrize("small", [1, "t1", "t2", "t3", "t4", "t5", "t6"],
-                                ids=["lds", "t1", "t2", "t3", "t4", "t5", "t6"])
+TS = ["t%d" % t for t in range(1, 8)]
+PATHS = pytest.mark.parametrize("small", [1] + TS, ids=["lds"] + TS)
 
 
 def test_poisson_init_bitwise():
@@ -165,10 +165,15 @@ def test_zero_iterations():
         assert g.solve_rb() == (0, 1.0)
 
 
+@pytest.mark.parametrize("finish2", ["1", "0"])
 @pytest.mark.parametrize("k", [2, 3])
-def test_large_grid_few_sweeps(k):
+def test_large_grid_few_sweeps(k, finish2, monkeypatch):
     """8192^2 (67M cells, 0.54 GB per field): bit-exact after 2 and 3 sweeps
-    (default path: temporally blocked, 3 = one full pass + one recomputed)"""
+    (default path: temporally blocked; a capped solve's passes run only the
+    iterations left, so these are single passes of T' = 2 and 3), with the
+    single-rank loop test in two levels (MISOR_FINISH2=1, default) and in
+    one kernel (0): same p, same iteration count"""
+    monkeypatch.setenv("MISOR_FINISH2", finish2)
     n = 8192
     p, rhs = orc.poisson_init(n, n)
     want = p.copy()

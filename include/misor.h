@@ -110,6 +110,13 @@ typedef struct {
     long long timed_passes; /* passes covered by sweep_ms */
     int iters_per_pass;     /* T of the last multi-block solve (1: single sweep) */
     int pad_;
+    /* decomposed solves, timing on: HIP events around every halo exchange
+     * (pack + transport + unpack) and every residual all-reduce (+ loop test)
+     * on the stream that runs it (the communication stream when overlapped) */
+    double halo_ms;         /* total device time of the solve's halo exchanges */
+    long long halos;        /* exchanges covered by halo_ms */
+    double allreduce_ms;    /* total device time of the residual all-reduces */
+    long long allreduces;   /* all-reduces covered by allreduce_ms */
 } misor_stats;
 
 const char* misor_last_error(void);

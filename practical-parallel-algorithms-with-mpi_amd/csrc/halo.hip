@@ -52,4 +52,24 @@ void launch_unpack(hipStream_t s, double* field, long long pitch, const HaloPlan
                        plan, const_cast<double*>(recvbuf));
 }
 
+// in-process transport's all-reduce: gather[q * kMaxT + k] holds rank q's
+// value k; every rank combines them in rank order (identical bits everywhere)
+__global__ void local_combine_kernel(const double* gather, int nranks, int n, int is_max,
+                                     double* out) {
+    const int k = threadIdx.x;
+    if (k >= n) return;
+    double a = gather[k];
+    for (int q = 1; q < nranks; ++q) {
+        const double b = gather[q * kMaxT + k];
+        a = is_max ? ((a > b) ? a : b) : a + b;
+    }
+    out[k] = a;
+}
+
+void launch_local_combine(hipStream_t s, const double* gather, int nranks, int n, int is_max,
+                          double* out) {
+    hipLaunchKernelGGL(local_combine_kernel, dim3(1), dim3(kMaxT), 0, s, gather, nranks, n,
+                       is_max, out);
+}
+
 }  // namespace misor

@@ -3,6 +3,7 @@
 // the NS step entry points and the 2D decomposition over RCCL.
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -12,6 +13,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "misor_internal.h"
@@ -153,6 +155,20 @@ struct misor_grid {
     double* recvbuf = nullptr;
     double* gbuf = nullptr;  // misor_gather: this rank's owned block, packed
     long long gbuf_cap = 0;
+    // in-process transport, event-driven: device work of different ranks is
+    // ordered by HIP events only (no host-device synchronisation); the host
+    // threads meet at barriers just to publish which event records to wait on
+    hipEvent_t lx_pk = nullptr, lx_cp = nullptr;  // exchange: my send buffer packed / copies done
+    hipEvent_t la_val[2] = {}, la_rd[2] = {}, la_cmb[2] = {};  // all-reduce, by parity
+    double* la_stage = nullptr;   // 2 x kMaxT: my value, by all-reduce parity
+    double* la_gather = nullptr;  // 2 x nranks x kMaxT: every rank's value, by parity
+    long long la_gen = 0;
+    bool comm_dead = false;       // the RCCL communicator was aborted (error / timeout)
+    // communication timing inside a timed solve: start/stop event pairs of the
+    // halo exchanges (0) and residual all-reduces (1) of the current batch
+    bool comm_timing = false;
+    std::vector<hipEvent_t> cev[2];
+    size_t cev_used[2] = {0, 0};
 
     // stats
     bool timing = false;
@@ -246,6 +262,13 @@ void misor_destroy(misor_grid* g) {
     if (g->ev_x) (void)hipEventDestroy(g->ev_x);
     if (g->ev_d) (void)hipEventDestroy(g->ev_d);
     for (auto e : g->ev) (void)hipEventDestroy(e);
+    for (auto& v : g->cev)
+        for (auto e : v) (void)hipEventDestroy(e);
+    for (hipEvent_t e : {g->lx_pk, g->lx_cp, g->la_val[0], g->la_val[1], g->la_rd[0], g->la_rd[1],
+                         g->la_cmb[0], g->la_cmb[1]})
+        if (e) (void)hipEventDestroy(e);
+    (void)hipFree(g->la_stage);
+    (void)hipFree(g->la_gather);
     if (g->comm) ncclCommDestroy(g->comm);
     if (g->own_stream && g->stream) (void)hipStreamDestroy(g->stream);
     delete g;
@@ -284,31 +307,131 @@ static void build_plan(misor_grid* g, int d) {
     P.total = so > ro ? so : ro;
 }
 
-// one 8-neighbour exchange of `field` at depth d over RCCL on the grid stream
+// a start/stop event pair for timing one communication step (kind 0: halo
+// exchange, 1: all-reduce) of the current batch; false when not timing
+static bool comm_pair(misor_grid* g, int kind, hipEvent_t* e0, hipEvent_t* e1) {
+    if (!g->comm_timing) return false;
+    std::vector<hipEvent_t>& v = g->cev[kind];
+    size_t& u = g->cev_used[kind];
+    while (v.size() < 2 * (u + 1)) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return false;
+        v.push_back(e);
+    }
+    *e0 = v[2 * u];
+    *e1 = v[2 * u + 1];
+    ++u;
+    return true;
+}
+
+// add the timed communication steps of the batch just synchronised to the stats
+static int collect_comm_times(misor_grid* g) {
+    for (int kind = 0; kind < 2; ++kind) {
+        for (size_t k = 0; k < g->cev_used[kind]; ++k) {
+            float ms = 0.f;
+            HIPCHK(hipEventElapsedTime(&ms, g->cev[kind][2 * k], g->cev[kind][2 * k + 1]));
+            if (kind == 0) {
+                g->stats.halo_ms += ms;
+                g->stats.halos++;
+            } else {
+                g->stats.allreduce_ms += ms;
+                g->stats.allreduces++;
+            }
+        }
+        g->cev_used[kind] = 0;
+    }
+    return MISOR_OK;
+}
+
+static double comm_timeout_s() {
+    const char* e = getenv("MISOR_COMM_TIMEOUT");
+    const double v = e && *e ? atof(e) : 0.0;
+    return v > 0 ? v : 600.0;
+}
+
+// Wait for stream s.  With an RCCL communicator, poll instead of blocking:
+// an asynchronous communicator error (a peer died, a link failed:
+// ncclCommGetAsyncError) or no progress for MISOR_COMM_TIMEOUT seconds
+// (default 600) aborts the communicator and returns MISOR_ECOMM on this rank,
+// where the reference's MPI default (MPI_ERRORS_ARE_FATAL) would end the job;
+// a blocked hipStreamSynchronize would hang instead.
+static int wait_stream(misor_grid* g, hipStream_t s) {
+    if (!g->comm) {
+        HIPCHK(hipStreamSynchronize(s));
+        return MISOR_OK;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    const double limit = comm_timeout_s();
+    for (long spins = 0;; ++spins) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e == hipSuccess) return MISOR_OK;
+        if (e != hipErrorNotReady)
+            return fail(MISOR_EHIP, "stream wait: %s", hipGetErrorString(e));
+        ncclResult_t ar = ncclSuccess;
+        const bool bad = ncclCommGetAsyncError(g->comm, &ar) == ncclSuccess &&
+                         ar != ncclSuccess && ar != ncclInProgress;
+        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (bad || el > limit) {
+            (void)ncclCommAbort(g->comm);
+            g->comm = nullptr;
+            g->comm_dead = true;
+            if (bad)
+                return fail(MISOR_ECOMM, "RCCL asynchronous error: %s", ncclGetErrorString(ar));
+            return fail(MISOR_ECOMM, "communication made no progress for %.0f s "
+                                     "(MISOR_COMM_TIMEOUT)", limit);
+        }
+        if (spins > 2000) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
+
+#define COMMCHK(g)                                                                        \
+    do {                                                                                  \
+        if ((g)->comm_dead)                                                               \
+            return fail(MISOR_ECOMM, "the communicator was aborted by an earlier error"); \
+    } while (0)
+
+// one 8-neighbour exchange of `field` at depth d on stream s (default: the
+// grid stream): pack kernel, transport, unpack kernel
 static int exchange(misor_grid* g, double* field, int d, hipStream_t s = nullptr) {
     if (!g->dist) return MISOR_OK;
+    COMMCHK(g);
     if (!s) s = g->stream;
     const HaloPlan& P = g->plan[d];
-    launch_pack(s, field, g->pitch, P, g->sendbuf);
+    hipEvent_t t0 = nullptr, t1 = nullptr;
+    const bool timed = comm_pair(g, 0, &t0, &t1);
+    if (timed) HIPCHK(hipEventRecord(t0, s));
     if (g->local) {
+        // In-process transport.  Rank q's copies of my send buffer and my own
+        // unpack of the previous exchange must be done before I pack again;
+        // my copies of q's buffer wait for q's pack.  Barrier 1: every rank has
+        // recorded its pack event; barrier 2: every rank has recorded its copy
+        // event (so the next exchange waits on this exchange's records).
         static const int opposite[kDirs] = {1, 0, 3, 2, 7, 6, 5, 4};
-        HIPCHK(hipStreamSynchronize(s));
-        g->local->barrier();  // every rank packed
+        LocalGroup& G = *g->local;
+        HIPCHK(hipStreamWaitEvent(s, g->lx_cp, 0));
+        for (int k = 0; k < kDirs; ++k)
+            if (g->nbr[k] >= 0) HIPCHK(hipStreamWaitEvent(s, G.members[g->nbr[k]]->lx_cp, 0));
+        launch_pack(s, field, g->pitch, P, g->sendbuf);
+        HIPCHK(hipEventRecord(g->lx_pk, s));
+        G.barrier();
         for (int k = 0; k < kDirs; ++k) {
             if (g->nbr[k] < 0) continue;
-            const misor_grid* q = g->local->members[g->nbr[k]];
+            const misor_grid* q = G.members[g->nbr[k]];
             const HaloRegion& sr = q->plan[d].send[opposite[k]];
             const HaloRegion& rr = P.recv[k];
+            HIPCHK(hipStreamWaitEvent(s, q->lx_pk, 0));
             HIPCHK(hipMemcpyAsync(g->recvbuf + rr.off, q->sendbuf + sr.off,
                                   sizeof(double) * (size_t)rr.w * rr.h,
                                   hipMemcpyDeviceToDevice, s));
         }
         launch_unpack(s, field, g->pitch, P, g->recvbuf);
-        HIPCHK(hipStreamSynchronize(s));
-        g->local->barrier();  // nobody repacks before every copy is done
+        HIPCHK(hipEventRecord(g->lx_cp, s));
+        if (timed) HIPCHK(hipEventRecord(t1, s));
         HIPCHK(hipGetLastError());
+        G.barrier();
         return MISOR_OK;
     }
+    launch_pack(s, field, g->pitch, P, g->sendbuf);
     NCCLCHK(ncclGroupStart());
     for (int k = 0; k < kDirs; ++k) {
         if (g->nbr[k] < 0) continue;
@@ -319,36 +442,50 @@ static int exchange(misor_grid* g, double* field, int d, hipStream_t s = nullptr
     }
     NCCLCHK(ncclGroupEnd());
     launch_unpack(s, field, g->pitch, P, g->recvbuf);
+    if (timed) HIPCHK(hipEventRecord(t1, s));
     HIPCHK(hipGetLastError());
     return MISOR_OK;
 }
 
-// all-reduce of n <= kMaxT device doubles (sum or max) across the ranks
+// all-reduce of n <= kMaxT device doubles (sum or max) across the ranks, on
+// stream s (default: the grid stream)
 static int allreduce(misor_grid* g, double* dev, int n, int is_max, hipStream_t s = nullptr) {
     if (!g->dist) return MISOR_OK;
+    COMMCHK(g);
     if (!s) s = g->stream;
+    hipEvent_t t0 = nullptr, t1 = nullptr;
+    const bool timed = comm_pair(g, 1, &t0, &t1);
+    if (timed) HIPCHK(hipEventRecord(t0, s));
     if (g->local) {
+        // In-process transport: every rank stages its values (slot by parity,
+        // reused two all-reduces later once every rank has read it), gathers
+        // every rank's staged values after barrier 1 and combines them in rank
+        // order on its device; barrier 2 publishes the read events.
         LocalGroup& G = *g->local;
-        double v[kMaxT];
-        HIPCHK(hipMemcpyAsync(v, dev, sizeof(double) * n, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        const int r = g->desc.rank;
-        for (int k = 0; k < n; ++k) G.vals[kMaxT * r + k] = v[k];
+        const int par = (int)(g->la_gen++ & 1);
+        double* stage = g->la_stage + par * kMaxT;
+        double* gather = g->la_gather + (size_t)par * G.n * kMaxT;
+        HIPCHK(hipStreamWaitEvent(s, g->la_cmb[par], 0));
+        for (int q = 0; q < G.n; ++q) HIPCHK(hipStreamWaitEvent(s, G.members[q]->la_rd[par], 0));
+        HIPCHK(hipMemcpyAsync(stage, dev, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipEventRecord(g->la_val[par], s));
         G.barrier();
-        for (int k = 0; k < n; ++k) {
-            double a = G.vals[k];
-            for (int q = 1; q < G.n; ++q) {
-                const double b = G.vals[kMaxT * q + k];
-                a = is_max ? ((a > b) ? a : b) : a + b;
-            }
-            v[k] = a;
+        for (int q = 0; q < G.n; ++q) {
+            const misor_grid* o = G.members[q];
+            HIPCHK(hipStreamWaitEvent(s, o->la_val[par], 0));
+            HIPCHK(hipMemcpyAsync(gather + (size_t)q * kMaxT, o->la_stage + par * kMaxT,
+                                  sizeof(double) * n, hipMemcpyDeviceToDevice, s));
         }
+        HIPCHK(hipEventRecord(g->la_rd[par], s));
+        launch_local_combine(s, gather, G.n, n, is_max, dev);
+        HIPCHK(hipEventRecord(g->la_cmb[par], s));
+        if (timed) HIPCHK(hipEventRecord(t1, s));
+        HIPCHK(hipGetLastError());
         G.barrier();
-        HIPCHK(hipMemcpyAsync(dev, v, sizeof(double) * n, hipMemcpyHostToDevice, s));
-        HIPCHK(hipStreamSynchronize(s));
         return MISOR_OK;
     }
     NCCLCHK(ncclAllReduce(dev, dev, n, ncclDouble, is_max ? ncclMax : ncclSum, g->comm, s));
+    if (timed) HIPCHK(hipEventRecord(t1, s));
     return MISOR_OK;
 }
 
@@ -409,26 +546,36 @@ static int effective_tsteps(const misor_grid* g) {
     return T;
 }
 
-static int pick_tb_nby(int ni, int nj, int T, int waves) {
-    // Block rows for a pass of T iterations.  A block streams H + 4T rows for
-    // its H, so tall blocks waste less; short ones give a launch more
-    // workgroups.  Measured at T = 6, 7 once the physical-side blocks stopped
-    // running the lane-masked path for whole block rows (tools/scale_proxy.py,
-    // profiles/r01_shape_sweep*.txt): H ~ 192 is within noise of the best from
-    // 32768^2 down to 8192 x 16384 (one rank of the 8-GPU split).  Taller
-    // blocks lose even where they fill the last round of resident workgroups
-    // exactly (r01_geom_sweep.txt: 8192 x 16384 at H = 225, 2.99 rounds of 512
-    // workgroups, is 7% slower than H = 191, 3.5 rounds).  Smaller grids halve
-    // H until the launch has ~1024 workgroups (4 per CU) to spread.  Heights
-    // inside a launch differ by at most one row.
-    const long long nbx = tb_nbx(ni, T, waves);
+// Block height H of a pass of T iterations.  A block streams H + 4T rows for
+// its H, so tall blocks waste less; short ones give a launch more workgroups,
+// and the workgroups resident together stream the same rows (page and L2
+// locality: round-1 measurements, profiles/r01_shape_sweep*.txt, put the
+// optimum near 192 rows from 32768^2 down to one rank's 8192 x 16384).  H is a
+// multiple of the static ring's S slots (sor_tb.hip: interior blocks march in
+// chunks of S steps); smaller grids halve it until the launch has ~1024
+// workgroups (4 per CU) to spread.  The last block row takes the rest
+// (between H/2 and 3H/2 rows) and marches in pairs.
+static int pick_tb_rows(int ni, int nj, int T, int variant) {
+    const long long nbx = tb_nbx(ni, T, tb_waves(variant));
+    const int S = tb_ring_slots(T, variant);
     int h = kDefaultTbRows;
     while (h / 2 >= kMinTbRows && nbx * ((nj + h - 1) / h) < 1024) h /= 2;
-    return (nj + h - 1) / h;
+    int k = (h + S / 2) / S;
+    if (k < 1) k = 1;
+    return k * S;
 }
 
-// geometry of the temporally blocked pass with T iterations into `tp`
+// geometry of the temporally blocked pass with T iterations into `tp`: the
+// block height of that T (an explicit MISOR_TUNE_TB_ROWS request for every T),
+// block rows, block columns
 static void tb_geometry(const misor_grid* g, int T, SweepParams& tp) {
+    const int nj = g->loc.nj, req = g->tb_rows_req;
+    int h = req > 0 ? req : pick_tb_rows(g->loc.ni, nj, T, tp.variant);
+    if (h > nj) h = nj;
+    // block rows: uniform H, the last one takes the rest (nearest count; an
+    // explicit request keeps ceil so every block but the last is H tall)
+    tp.nby = req > 0 ? (nj + h - 1) / h : std::max(1, (nj + h / 2) / h);
+    tp.rows_per_block = h;
     tp.nbx = tb_nbx(g->loc.ni, T, tb_waves(tp.variant));
     tp.nblocks = tp.nbx * tp.nby;
 }
@@ -437,24 +584,30 @@ static int configure_tb(misor_grid* g, int T, int variant, int rows) {
     if (T < 1 || T > kMaxT) return fail(MISOR_EINVAL, "iterations per pass must be 1..%d", kMaxT);
     if (variant < 0 || variant >= kNumTbVariants) return fail(MISOR_EINVAL, "bad tb variant");
     g->tsteps = T;
+    g->tb_rows_req = rows;
     SweepParams& tp = g->tp;
     tp.variant = variant;
-    const int Tg = effective_tsteps(g);
-    tp.nby = rows > 0 ? (g->loc.nj + rows - 1) / rows
-                      : pick_tb_nby(g->loc.ni, g->loc.nj, Tg, tb_waves(variant));
-    tp.rows_per_block = (g->loc.nj + tp.nby - 1) / tp.nby;
-    if (kTbVariants[variant].lds_ring >= 2 &&
-        (long long)(tp.rows_per_block + 4 * kMaxT + 4) * tp.pitch * 8 >= (1LL << 31)) {
-        // the rhs re-read variants address a block's rows with 32-bit buffer offsets
-        tp.variant = kDefaultTbVariant;
-        configure_tb(g, T, kDefaultTbVariant, rows);
-        return fail(MISOR_EINVAL, "tb variant %d: a block of rows exceeds 2 GiB", variant);
-    }
     tp.xcd_remap = g->sp.xcd_remap;
     const int Te = effective_tsteps(g);
-    tb_geometry(g, Te, tp);
+    // every pass length a solve may launch (T, the last pass of a capped
+    // solve, a pass recomputed after convergence) has its own geometry; the
+    // partials hold the largest
+    long long need = 1;
+    for (int Tp = 1; Tp <= std::max(1, Te); ++Tp) {
+        SweepParams q = tp;
+        tb_geometry(g, Tp, q);
+        // the steady march addresses a block's rows with 32-bit buffer offsets
+        // and marks lanes that do not store with offset 2^30
+        const long long last = g->loc.nj - (long long)(q.nby - 1) * q.rows_per_block;
+        if ((std::max<long long>(q.rows_per_block, last) + 4 * kMaxT + 8) * tp.pitch * 8 >=
+            (1LL << 30))
+            return fail(MISOR_EINVAL, "tb rows %d: a block of rows exceeds 1 GiB",
+                        q.rows_per_block);
+        need = std::max(need, (long long)Tp * q.nblocks);
+    }
+    tb_geometry(g, std::max(2, Te), tp);
     g->tb_nparts = tp.nblocks;
-    return ensure_partials(g, Te * tp.nblocks);
+    return ensure_partials(g, (int)need);
 }
 
 int misor_create(misor_grid** out, const misor_desc* d) {
@@ -616,7 +769,14 @@ int misor_create(misor_grid** out, const misor_desc* d) {
                 g->local = G;
                 if (++G->joined == nranks) g_groups.erase(name);  // name reusable
             }
+            bool lok = hipMalloc(&g->la_stage, sizeof(double) * 2 * kMaxT) == hipSuccess &&
+                       hipMalloc(&g->la_gather, sizeof(double) * 2 * kMaxT * (size_t)nranks) ==
+                           hipSuccess;
+            for (hipEvent_t* e : {&g->lx_pk, &g->lx_cp, &g->la_val[0], &g->la_val[1],
+                                  &g->la_rd[0], &g->la_rd[1], &g->la_cmb[0], &g->la_cmb[1]})
+                lok = lok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
             g->local->barrier();  // every member registered before any exchange
+            if (!lok) CREATE_FAIL(MISOR_EHIP, "in-process transport allocation failed");
         } else {
             ncclUniqueId id;
             memcpy(&id, d->comm_id, sizeof id);
@@ -661,7 +821,10 @@ int misor_set_stream(misor_grid* g, void* s) {
 
 int misor_synchronize(misor_grid* g) {
     if (!g) return fail(MISOR_EINVAL, "null grid");
-    HIPCHK(hipStreamSynchronize(g->stream));
+    {
+        int rc_ = wait_stream(g, g->stream);
+        if (rc_) return rc_;
+    }
     return MISOR_OK;
 }
 
@@ -750,23 +913,52 @@ int misor_gather(misor_grid* g, int field, double* host) {
             need = std::max(need, (long long)(L.ni + 2) * (L.nj + 2));
         }
     }
+    // every rank allocates its packing buffer (rank 0: large enough for any
+    // rank's block -- it is also the receive stage); all ranks agree on the
+    // outcome before any send / receive is posted, so a failed allocation is
+    // an error on every rank instead of a rank blocked in a send
+    int alloc_ok = 1;
     if (need > g->gbuf_cap) {
         (void)hipFree(g->gbuf);
         g->gbuf = nullptr;
         g->gbuf_cap = 0;
-        HIPCHK(hipMalloc(&g->gbuf, sizeof(double) * (size_t)need));
-        g->gbuf_cap = need;
+        if (hipMalloc(&g->gbuf, sizeof(double) * (size_t)need) == hipSuccess)
+            g->gbuf_cap = need;
+        else
+            alloc_ok = 0;
+    }
+    {
+        g->red_host[3] = alloc_ok ? 0.0 : 1.0;
+        HIPCHK(hipMemcpyAsync(g->red_out + 3, g->red_host + 3, sizeof(double),
+                              hipMemcpyHostToDevice, g->stream));
+        int rc = allreduce(g, g->red_out + 3, 1, 1);
+        if (rc) return rc;
+        HIPCHK(hipMemcpyAsync(g->red_host + 3, g->red_out + 3, sizeof(double),
+                              hipMemcpyDeviceToHost, g->stream));
+        {
+            int rc_ = wait_stream(g, g->stream);
+            if (rc_) return rc_;
+        }
+        if (g->red_host[3] != 0.0)
+            return fail(MISOR_ENOMEM, "gather: a rank could not allocate its %s buffer",
+                        alloc_ok ? "peer's" : "own");
     }
     const double* f = field_ptr(g, field);
     const double* src = origin(g, const_cast<double*>(f)) + (long long)mine.j0 * g->pitch + mine.i0;
     HIPCHK(hipMemcpy2DAsync(g->gbuf, sizeof(double) * mine.w, src, sizeof(double) * g->pitch,
                             sizeof(double) * mine.w, mine.h, hipMemcpyDeviceToDevice, g->stream));
-    HIPCHK(hipStreamSynchronize(g->stream));
+    {
+        int rc_ = wait_stream(g, g->stream);
+        if (rc_) return rc_;
+    }
     auto to_host = [&](const double* dev, const OwnedBlock& b) -> int {
         HIPCHK(hipMemcpy2DAsync(host + (size_t)b.gj0 * gw + b.gi0, sizeof(double) * gw, dev,
                                 sizeof(double) * b.w, sizeof(double) * b.w, b.h,
                                 hipMemcpyDeviceToHost, g->stream));
-        HIPCHK(hipStreamSynchronize(g->stream));
+        {
+            int rc_ = wait_stream(g, g->stream);
+            if (rc_) return rc_;
+        }
         return MISOR_OK;
     };
     if (g->local) {
@@ -782,12 +974,12 @@ int misor_gather(misor_grid* g, int field, double* host) {
         g->local->barrier();  // nobody repacks before rank 0 has read
         return MISOR_OK;
     }
-    // RCCL: rank r sends its packed block to rank 0, one peer at a time
-    double* stage = nullptr;
+    // RCCL: rank r sends its packed block to rank 0, one peer at a time; rank
+    // 0 receives into its own packing buffer once its block is on the host
+    double* const stage = g->gbuf;
     if (rank == 0) {
         int rc = to_host(g->gbuf, mine);
         if (rc) return rc;
-        HIPCHK(hipMalloc(&stage, sizeof(double) * (size_t)need));
     }
     int rc = MISOR_OK;
     for (int r = 1; r < g->desc.nranks && rc == MISOR_OK; ++r) {
@@ -806,9 +998,11 @@ int misor_gather(misor_grid* g, int field, double* host) {
                 rc = to_host(stage, b);
         }
     }
-    if (stage) (void)hipFree(stage);
     if (rc) return rc;
-    HIPCHK(hipStreamSynchronize(g->stream));
+    {
+        int rc_ = wait_stream(g, g->stream);
+        if (rc_) return rc_;
+    }
     return MISOR_OK;
 }
 
@@ -912,7 +1106,10 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
         if (g->timing) HIPCHK(hipEventRecord(g->ev[1], g->stream));
         HIPCHK(hipMemcpyAsync(g->st_host, g->st, sizeof(DevState), hipMemcpyDeviceToHost,
                               g->stream));
-        HIPCHK(hipStreamSynchronize(g->stream));
+        {
+            int rc_ = wait_stream(g, g->stream);
+            if (rc_) return rc_;
+        }
         const int it = g->st_host->it;
         if (g->timing) {
             float ms = 0.f;
@@ -930,6 +1127,9 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
     // multi-block path: passes of T iterations (T = 1: single-iteration sweep
     // kernel; T >= 2: temporally blocked kernel, sor_tb.hip)
     const int T = effective_tsteps(g);
+    // time the communication steps of the loop (collected after each batch)
+    g->comm_timing = g->timing && g->dist;
+    g->cev_used[0] = g->cev_used[1] = 0;
     const int depth = 2 * T;  // halo of src each pass needs
     const int nparts = T == 1 ? g->nparts : g->tb_nparts;
     double* const rhs = g->fld[kRhs];
@@ -1100,7 +1300,14 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
         g->stats.launches += batch;
         HIPCHK(hipMemcpyAsync(g->st_host, g->st, sizeof(DevState), hipMemcpyDeviceToHost,
                               g->stream));
-        HIPCHK(hipStreamSynchronize(g->stream));
+        {
+            int rc_ = wait_stream(g, g->stream);
+            if (rc_) return rc_;
+        }
+        if (g->comm_timing) {
+            int rc = collect_comm_times(g);
+            if (rc) return rc;
+        }
         if (g->timing) {
             // passes after convergence exit at once; count only the real ones
             const long long real_before = launched - batch;
@@ -1130,11 +1337,15 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
         pass(g->stream, 0, src, pbuf(g, g->cur), t_of(passes - 1) - over, 1, g->partials);
         HIPCHK(hipGetLastError());
     }
+    g->comm_timing = false;
     if (g->dist) {  // leave the halo of the final field consistent (adaptUV reads it)
         int rc = exchange(g, pbuf(g, g->cur), 2);
         if (rc) return rc;
     }
-    HIPCHK(hipStreamSynchronize(g->stream));
+    {
+        int rc_ = wait_stream(g, g->stream);
+        if (rc_) return rc_;
+    }
     g->last_iters = it;
     g->stats.sweeps += it;
     g->stats.iters_per_pass = T;
@@ -1235,7 +1446,10 @@ int misor_max_uv(misor_grid* g, double* umax, double* vmax) {
     }
     HIPCHK(hipMemcpyAsync(g->red_host, g->red_out, 2 * sizeof(double), hipMemcpyDeviceToHost,
                           g->stream));
-    HIPCHK(hipStreamSynchronize(g->stream));
+    {
+        int rc_ = wait_stream(g, g->stream);
+        if (rc_) return rc_;
+    }
     if (umax) *umax = g->red_host[0];
     if (vmax) *vmax = g->red_host[1];
     return MISOR_OK;
@@ -1296,19 +1510,48 @@ int misor_compute_rhs(misor_grid* g) {
     return MISOR_OK;
 }
 
+// normalizePressure (assignment-5/sequential/src/solver.c:204-217) with the
+// sum exact (ns_kernels.hip launch_exact_sum): the mean, and so p, is the same
+// for every decomposition -- the reference's MPI build all-reduces per-rank
+// partial sums (assignment-5/skeleton/src/solver.c:697), whose rounding depends
+// on the partition.  Two passes over p: the global max |p| (order-free) fixes
+// the fixed-point scale, then the exact sum; one host round trip per call
+// (every 100 time steps in the reference's main loop).
 int misor_normalize_pressure(misor_grid* g) {
     NEED_NS(g);
     double* p = pbuf(g, g->cur);
-    launch_sum(g->nl, p, g->red_partials);
-    launch_finish_reduce(g->stream, g->red_partials, reduce_blocks(g->loc.ni, g->loc.nj),
-                         kReduceSum, 1, g->red_out);
-    if (g->dist)
-    {
-        int rc = allreduce(g, g->red_out, 1, 0);
+    const int nb = reduce_blocks(g->loc.ni, g->loc.nj);
+    launch_absmax2(g->nl, p, p, g->red_partials);
+    launch_finish_reduce(g->stream, g->red_partials, nb, kReduceMax, 2, g->red_out);
+    HIPCHK(hipGetLastError());
+    if (g->dist) {
+        int rc = allreduce(g, g->red_out, 1, 1);
         if (rc) return rc;
     }
+    HIPCHK(hipMemcpyAsync(g->red_host, g->red_out, sizeof(double), hipMemcpyDeviceToHost,
+                          g->stream));
+    {
+        int rc_ = wait_stream(g, g->stream);
+        if (rc_) return rc_;
+    }
+    const double mx = g->red_host[0];
+    int E = 0;
+    (void)frexp(mx, &E);
+    launch_exact_sum(g->nl, p, E, g->red_partials, g->red_out);
+    HIPCHK(hipGetLastError());
+    if (g->dist) {
+        int rc = allreduce(g, g->red_out, 3, 0);  // integer limbs < 2^53: exact
+        if (rc) return rc;
+    }
+    HIPCHK(hipMemcpyAsync(g->red_host, g->red_out, 3 * sizeof(double), hipMemcpyDeviceToHost,
+                          g->stream));
+    {
+        int rc_ = wait_stream(g, g->stream);
+        if (rc_) return rc_;
+    }
     const double cells = (double)(g->desc.imax + 2) * (double)(g->desc.jmax + 2);
-    launch_sub_mean(g->nl, p, g->red_out, cells);
+    const double avg = exact_sum_value(g->red_host, E) / cells;  // solver.c:213
+    launch_sub_mean(g->nl, p, avg);
     HIPCHK(hipGetLastError());
     return MISOR_OK;
 }
@@ -1345,9 +1588,7 @@ int misor_set_tuning(misor_grid* g, int key, int value) {
     case MISOR_TUNE_OVERLAP: g->overlap = value != 0; return MISOR_OK;
     case MISOR_TUNE_TSTEPS: return configure_tb(g, value, g->tp.variant, g->tb_rows_req);
     case MISOR_TUNE_TB_VARIANT: return configure_tb(g, g->tsteps, value, g->tb_rows_req);
-    case MISOR_TUNE_TB_ROWS:
-        g->tb_rows_req = value;
-        return configure_tb(g, g->tsteps, g->tp.variant, value);
+    case MISOR_TUNE_TB_ROWS: return configure_tb(g, g->tsteps, g->tp.variant, value);
     default: return fail(MISOR_EINVAL, "unknown tuning key %d", key);
     }
 }

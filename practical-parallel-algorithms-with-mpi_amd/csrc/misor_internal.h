@@ -20,17 +20,19 @@ namespace misor {
 //  - kXOff = 15 puts the first interior column i = 1 on a 128-byte boundary,
 //    so every wave's 16-byte-per-lane row segment of 128 cells starts a cache
 //    line; the ghost column i = 0 is the last double of the preceding line.
-//  - kYOff = 2 * kMaxT rows below row 0 and as many (+ prefetch run-out)
+//  - kYOff = 2 * kMaxT + 2 rows below row 0 and as many (+ prefetch run-out)
 //    above row nj+1: a block of the temporally blocked sweep streams rows
-//    j0-2T .. j1-1+2T (+ rows in flight) without clamping.
+//    j0-2T-1 .. j1-1+2T (+ rows in flight) without clamping, and its first
+//    strip's columns from 1 - 2T (the tail of the row below, in the
+//    allocation: a left halo of depth 2 kMaxT too).
 //  - pitch = 160 + round_up(ni, kStripCells * kMaxWavesX): left pad line, the
 //    strips, the run-out of the last (overlapping) strip and pad; a multiple
 //    of 16 doubles (128 B) that is not a power of two.
 // Padding cells are zero and never feed an interior result.
 // ---------------------------------------------------------------------------
 constexpr int kXOff = 15;
-constexpr int kMaxT = 8;                 // iterations per temporally blocked pass (max)
-constexpr int kYOff = 2 * kMaxT;
+constexpr int kMaxT = 12;                // iterations per temporally blocked pass (max)
+constexpr int kYOff = 2 * kMaxT + 2;
 constexpr int kLanes = 64;                 // wavefront
 constexpr int kStripCells = 2 * kLanes;    // 128 columns per wave (2 per lane)
 constexpr int kMaxWavesX = 16;             // strips per sweep workgroup (max)
@@ -56,23 +58,19 @@ constexpr int kNumSweepVariants = 15;
 constexpr int kDefaultSweepVariant = 7;  // 8 strips, 2 rows ahead, nt stores (tools/tune_sweep.py)
 int sweep_waves(int variant);
 
-// temporally blocked sweep (sor_tb.hip): strips per workgroup, rows in flight,
-// rhs ring in registers (0), in LDS (1) or re-read from L2 by stages 1..K
-// (LR = K + 1 >= 2, the later stages keep the register ring),
-// minimum waves per SIMD (0: none)
+// temporally blocked sweep (sor_tb.hip): strips per workgroup, rows in flight
 struct TbVariant {
-    int waves, ahead, lds_ring, min_waves;
+    int waves, ahead;
 };
-constexpr TbVariant kTbVariants[] = {{4, 2, 0, 0}, {8, 2, 0, 0}, {4, 3, 0, 0}, {4, 2, 1, 0},
-                                     {4, 2, 1, 4}, {4, 3, 1, 0}, {8, 2, 1, 0}, {6, 2, 1, 0},
-                                     {2, 3, 0, 0}, {1, 3, 0, 0}, {4, 3, 8, 0}, {4, 3, 2, 0},
-                                     {4, 3, 3, 0}, {4, 3, 4, 0}, {4, 3, 0, 0}};
-constexpr int kNumTbVariants = 15;  // 14: as 2, branch-free steady stores
-constexpr int kDefaultTsteps = 7;      // iterations per pass (tools/scale_proxy.py, r01_shape_sweep)
-constexpr int kDefaultTbVariant = 2;   // 4 strips, 3 rows in flight, rhs ring in registers
-constexpr int kDefaultTbRows = 192;    // automatic rows per block (misor_api.hip pick_tb_rows)
+constexpr TbVariant kTbVariants[] = {{4, 2}, {8, 2}, {2, 2}, {1, 2}, {4, 3}};
+constexpr int kNumTbVariants = 5;
+constexpr int kDefaultTsteps = 7;      // iterations per pass
+constexpr int kDefaultTbVariant = 0;   // 4 strips, 2 rows in flight
+constexpr int kDefaultTbRows = 192;    // target rows per block (misor_api.hip pick_tb_nby) ...
 constexpr int kMinTbRows = 48;         // ... halved down to this while a launch has < 1024 WGs
 int tb_waves(int variant);
+// rhs ring slots of the steady march: interior block heights are multiples of it
+int tb_ring_slots(int T, int variant);
 int tb_out_width(int T);
 int tb_nbx(int ni, int T, int waves);           // block columns of a pass of T iterations
 
@@ -156,6 +154,10 @@ void launch_pack(hipStream_t s, const double* field, long long pitch, const Halo
 void launch_unpack(hipStream_t s, double* field, long long pitch, const HaloPlan& plan,
                    const double* recvbuf);
 int sweep_partials(int ni, int nj, int rows_per_block, int waves, int* nbx, int* nby);
+// in-process transport: out[k] = combination (sum / max, rank order) of
+// gather[q * kMaxT + k] over q < nranks, k < n
+void launch_local_combine(hipStream_t s, const double* gather, int nranks, int n, int is_max,
+                          double* out);
 
 void launch_fill(hipStream_t s, double* a, long long count, double v);
 // the message misor_last_error() returns (thread-local, shared by the 2D and 3D ABI)
@@ -184,11 +186,18 @@ void launch_adapt_uv(const NsLaunch& L, const double* f, const double* g, const 
 // reductions over ALL (ni+2)(nj+2) cells: partial per block, then a finish
 int reduce_blocks(int ni, int nj);
 void launch_absmax2(const NsLaunch& L, const double* u, const double* v, double* partials);
-void launch_sum(const NsLaunch& L, const double* p, double* partials);
+// normalizePressure's sum, exact (order- and decomposition-independent):
+// fixed-point terms at 2^(E - kSumFrac), E = exponent of the global max |p|;
+// limbs[0..2] = the local sum as three 44-bit integer limbs (doubles, summed
+// exactly by an all-reduce); exact_sum_value rounds the total once (host)
+constexpr int kSumFrac = 72;
+void launch_exact_sum(const NsLaunch& L, const double* p, int E, double* partials,
+                      double* limbs);
+double exact_sum_value(const double limbs[3], int E);
 void launch_finish_reduce(hipStream_t s, const double* partials, int n, int op, int width,
                           double* out);
-// p -= (*sum) / cells over the whole local array (normalizePressure)
-void launch_sub_mean(const NsLaunch& L, double* p, const double* sum, double cells);
+// p -= avg over the whole local array (normalizePressure)
+void launch_sub_mean(const NsLaunch& L, double* p, double avg);
 enum { kReduceSum = 0, kReduceMax = 1 };
 
 // ---------------------------------------------------------------------------

@@ -244,11 +244,6 @@ int reduce_blocks(int ni, int nj) {
 }
 
 namespace {
-__device__ __forceinline__ double wsum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
 __device__ __forceinline__ double wmax(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -307,29 +302,97 @@ void launch_absmax2(const NsLaunch& L, const double* u, const double* v, double*
                        L.s, CLay{u, L.pitch}, CLay{v, L.pitch}, region_of(L), partials);
 }
 
-__global__ __launch_bounds__(kRedThreads) void sum_kernel(CLay p, Region R, double* partials) {
-    __shared__ double sp[kRedThreads / 64];
-    double s = 0.0;
-    const long long n = (long long)R.w * R.h;
-    for (long long k = (long long)blockIdx.x * kRedThreads + threadIdx.x; k < n;
-         k += (long long)gridDim.x * kRedThreads) {
-        const int i = R.ilo + (int)(k % R.w), j = R.jlo + (int)(k / R.w);
-        s += p(i, j);
+// ---- normalizePressure's sum (:208-212), exact: independent of the
+// summation order, so of the block / rank decomposition.  Every cell
+// x = m * 2^(ex-53) (|m| < 2^53 an integer) becomes the fixed-point integer
+// trunc(x * 2^(kSumFrac - E)) with E the exponent of the largest |x| of the
+// whole (global) field, so |term| < 2^(kSumFrac+1); terms and their sums are
+// 128-bit integers, added exactly in any order.  The total is rounded to a
+// double once, on the host (exact_sum_value).  The truncation of each term is
+// a function of the cell alone: < 2^(E - kSumFrac) per cell, 2^17 times below
+// the rounding of one double addition at the field's scale.
+namespace {
+struct U128 {
+    unsigned long long lo, hi;
+};
+__device__ __forceinline__ U128 add128(U128 a, U128 b) {
+    U128 r;
+    r.lo = a.lo + b.lo;
+    r.hi = a.hi + b.hi + (r.lo < a.lo ? 1ull : 0ull);
+    return r;
+}
+__device__ __forceinline__ U128 term128(double x, int E) {
+    U128 r{0ull, 0ull};
+    if (x == 0.0) return r;
+    int ex;
+    const double f = frexp(fabs(x), &ex);                     // |x| = f 2^ex, f in [0.5, 1)
+    const unsigned long long m = (unsigned long long)ldexp(f, 53);  // exact
+    const int sh = ex - 53 - E + kSumFrac;                    // <= kSumFrac - 53
+    if (sh >= 0) {
+        r.lo = m << sh;
+        r.hi = sh == 0 ? 0ull : (m >> (64 - sh));
+    } else if (sh > -64) {
+        r.lo = m >> (-sh);
     }
-    s = wsum(s);
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    if (lane == 0) sp[w] = s;
+    if (x < 0.0) {  // two's complement
+        r.lo = ~r.lo;
+        r.hi = ~r.hi;
+        r = add128(r, U128{1ull, 0ull});
+    }
+    return r;
+}
+}  // namespace
+
+__global__ __launch_bounds__(kRedThreads) void exact_sum_kernel(CLay p, Region R, int E,
+                                                                unsigned long long* partials) {
+    __shared__ U128 sh[kRedThreads];
+    U128 s{0ull, 0ull};
+    // rows over blocks, columns over threads (coalesced; the sum is exact)
+    for (int jj = blockIdx.x; jj < R.h; jj += gridDim.x) {
+        const int j = R.jlo + jj;
+        for (int ii = threadIdx.x; ii < R.w; ii += kRedThreads)
+            s = add128(s, term128(p(R.ilo + ii, j), E));
+    }
+    sh[threadIdx.x] = s;
     __syncthreads();
+    for (int w = kRedThreads / 2; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) sh[threadIdx.x] = add128(sh[threadIdx.x], sh[threadIdx.x + w]);
+        __syncthreads();
+    }
     if (threadIdx.x == 0) {
-        double t = 0.0;
-        for (int k = 0; k < kRedThreads / 64; ++k) t += sp[k];
-        partials[blockIdx.x] = t;
+        partials[2 * blockIdx.x] = sh[0].lo;
+        partials[2 * blockIdx.x + 1] = sh[0].hi;
     }
 }
 
-void launch_sum(const NsLaunch& L, const double* p, double* partials) {
-    hipLaunchKernelGGL(sum_kernel, dim3(reduce_blocks(L.ni, L.nj)), dim3(kRedThreads), 0, L.s,
-                       CLay{p, L.pitch}, region_of(L), partials);
+// the block sums added (one thread: exact, so any order), written as three
+// limbs of 44 bits (the top one signed) as doubles: integers below 2^53, which
+// a floating-point all-reduce over the ranks adds exactly
+__global__ void exact_finish_kernel(const unsigned long long* partials, int n, double* limbs) {
+    U128 s{0ull, 0ull};
+    for (int k = 0; k < n; ++k) s = add128(s, U128{partials[2 * k], partials[2 * k + 1]});
+    const unsigned long long m44 = (1ull << 44) - 1;
+    limbs[0] = (double)(s.lo & m44);
+    limbs[1] = (double)(((s.lo >> 44) | (s.hi << 20)) & m44);
+    limbs[2] = (double)((long long)s.hi >> 24);  // bits 88..127, arithmetic shift
+}
+
+void launch_exact_sum(const NsLaunch& L, const double* p, int E, double* partials,
+                      double* limbs) {
+    const int nb = reduce_blocks(L.ni, L.nj);
+    hipLaunchKernelGGL(exact_sum_kernel, dim3(nb), dim3(kRedThreads), 0, L.s, CLay{p, L.pitch},
+                       region_of(L), E, reinterpret_cast<unsigned long long*>(partials));
+    hipLaunchKernelGGL(exact_finish_kernel, dim3(1), dim3(1), 0, L.s,
+                       reinterpret_cast<const unsigned long long*>(partials), nb, limbs);
+}
+
+double exact_sum_value(const double limbs[3], int E) {
+    // V = l2 2^88 + l1 2^44 + l0, rounded to a double once (gcc's conversion of
+    // a 128-bit integer rounds to nearest even), then scaled exactly
+    const __int128 v = (__int128)(long long)limbs[2] * ((__int128)1 << 88) +
+                       (__int128)(long long)limbs[1] * ((__int128)1 << 44) +
+                       (__int128)(long long)limbs[0];
+    return ldexp((double)v, E - kSumFrac);
 }
 
 // fixed-order combination of `n` partial records of `width` doubles
@@ -365,8 +428,7 @@ void launch_finish_reduce(hipStream_t s, const double* partials, int n, int op, 
 }
 
 // normalizePressure's second loop (:214-216): p -= avg over every cell
-__global__ void sub_mean_kernel(Lay p, int ni, int nj, const double* sum, double cells) {
-    const double avg = (*sum) / cells;
+__global__ void sub_mean_kernel(Lay p, int ni, int nj, double avg) {
     const long long n = (long long)(ni + 2) * (nj + 2);
     for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n;
          k += (long long)gridDim.x * blockDim.x) {
@@ -375,9 +437,9 @@ __global__ void sub_mean_kernel(Lay p, int ni, int nj, const double* sum, double
     }
 }
 
-void launch_sub_mean(const NsLaunch& L, double* p, const double* sum, double cells) {
+void launch_sub_mean(const NsLaunch& L, double* p, double avg) {
     hipLaunchKernelGGL(sub_mean_kernel, dim3(reduce_blocks(L.ni, L.nj)), dim3(256), 0, L.s,
-                       Lay{p, L.pitch}, L.ni, L.nj, sum, cells);
+                       Lay{p, L.pitch}, L.ni, L.nj, avg);
 }
 
 }  // namespace misor

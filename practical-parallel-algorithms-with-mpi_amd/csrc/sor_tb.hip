@@ -1,6 +1,6 @@
 // sor_tb.hip -- temporally blocked red-black SOR for gfx950: T complete
-// solveRB iterations (assignment-4/src/solver.c:197-229, T = 1..8) per pass
-// over HBM.
+// solveRB iterations (assignment-4/src/solver.c:197-229, T = 2..kMaxT) per
+// pass over HBM.
 //
 // The single-iteration sweep (sor_kernels.hip) already moves the algorithmic
 // minimum of one iteration -- read p, read rhs, write p: 24 B per lattice
@@ -21,16 +21,35 @@
 //          T .. 63-T hold correct values.  Overlapping loads between strips
 //          are L2 hits; nothing is exchanged between waves.
 //   rows = a block of H output rows [j0, j1); the wave streams OLD rows
-//          j0-2T .. j1-1+2T upward.  Stage t receives the output row stream of
-//          stage t-1 (stage 1: the old field) and, on receiving row rin,
-//          updates the red cells of row rin-1 and the black cells of row
-//          rin-2, emitting row rin-2 of iteration t.  Stage T's rows
-//          j0 .. j1-1 are stored.
+//          j0-2T .. j1-1+2T upward (N = H + 4T steps).  Stage t receives the
+//          output row stream of stage t-1 (stage 0: the old field) and, on
+//          receiving row rin, updates the red cells of row rin-1 and the black
+//          cells of row rin-2, emitting row rin-2 of iteration t+1.  The last
+//          stage's rows j0 .. j1-1 are stored.
 //   Every stage keeps 3 rows (A = row rin-1, M1 = rin-2 half updated, M2 =
-//   final rin-3) and the rhs rows it needs come from one ring of the last 2T
-//   streamed rows, so rhs is read from HBM once.  The ring lives in registers
-//   (8 VGPRs per stage) or -- to keep 3-4 waves per SIMD at T >= 4 -- in a
-//   lane-private LDS ring (LDS_RING variants).
+//   final rin-3); the rhs rows come from one register ring of the last 2T
+//   streamed rows (+ the D rows in flight), so rhs is read from HBM once.
+//
+// The static ring.  Every block of interior rows is H = a multiple of the
+// ring's S = 2T + D (+1 if odd) slots tall.  Its march starts with 4T
+// "warm-up" steps (no residual, no store; the ring shifts one register per
+// step, in pairs of steps) and then runs the remaining H steps in chunks of S
+// steps fully unrolled, with rhs row x in ring slot (x - rs + 1) mod S: every
+// ring register keeps its row for its whole life and the loads land in the
+// slot of the row that just died, so the steady march has no register moves
+// for the ring (the round-1 kernel spent 36 64-bit moves per step on it).
+// Stores go through a buffer descriptor with an out-of-range offset on lanes
+// that do not store, so a chunk is one basic block.
+//
+// Residual windows.  The residual of stage t is tallied over red rows
+// [j0 + 2T-1-2t, j1 + 2T-1-2t) and black rows [j0 + 2T-2-2t, j1 + 2T-2-2t)
+// of the block (shifted by the same amount in every block, so every cell is
+// counted exactly once per iteration; blocks on a physical bottom / top side
+// extend theirs to row 1 / nj).  In step numbers both windows are [4T, N) for
+// every stage: the steady chunks tally and store on every step, the warm-up
+// steps never do, and no drain steps exist.  Every row in a window lies inside
+// the stage's valid cone (red rows [rs+2t+1, rend-2t-1], black [rs+2t+2,
+// rend-2t-2]).
 //
 // Boundary handling per stage -- identical to the reference's end-of-
 // iteration ghost copy (:219-227), applied to every intermediate iteration:
@@ -41,26 +60,21 @@
 //   that borders another rank the 2T-deep halo (exchanged before the pass)
 //   supplies the neighbour's old values and the stages simply keep updating
 //   them: identical arithmetic, so identical bits to what the owner computes.
+//   Blocks whose cone reaches a physical side, and the last block row when
+//   its height is not a multiple of S, march in pairs of steps with run-time
+//   row tests (kRowEdge) and, at a physical left/right side, lane masks
+//   (kEdge).
 //
-// Residual: stage t accumulates r^2 of the cells this wave owns (output
-// lanes, rows [j0, j1)), partial per workgroup per stage in a fixed order;
-// the finish kernel decides iteration by iteration exactly like the
-// single-sweep path.  If convergence (or itermax) is reached at stage t < T,
-// the host recomputes that pass with T' = t from the untouched source buffer
-// (misor_api.hip), so the returned field is the one after exactly `it`
-// iterations.
-//
-// Instruction economy (the kernel is VALU-issue-bound once T >= 3):
-//  - strips whose 128 columns are all updated cells ("interior" strips: no
-//    physical ghost column, no padding) run a path with no per-lane masks,
-//    the row colour as a compile-time constant (rows unrolled by two) and the
-//    residual accumulated in every lane, non-owned lanes dropped at the end;
-//    only strips at a physical left/right side run the masked path;
-//  - lane shifts are DPP wave_shr:1 / wave_shl:1 moves, not LDS permutes;
-//  - r^2 is accumulated with an FMA (the residual's rounding is not part of
-//    the bit-exact contract; p is).
+// Residual: stage t accumulates r^2 of the cells this wave counts; partial per
+// workgroup per stage in a fixed order; the finish kernel decides iteration by
+// iteration exactly like the single-sweep path.  If convergence (or itermax)
+// is reached at stage t < T, the host recomputes that pass with T' = t from
+// the untouched source buffer (misor_api.hip), so the returned field is the
+// one after exactly `it` iterations.
 //
 // Bit-exactness: same expression order as the reference, -ffp-contract=off.
+
+#include <utility>
 
 #include "misor_internal.h"
 
@@ -99,12 +113,15 @@ typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ d2 ldv(const double* p) { return *reinterpret_cast<const d2*>(p); }
 
-template <bool NT>
 __device__ __forceinline__ void stv(double* p, d2 v) {
-    if (NT)
-        __builtin_nontemporal_store(v, reinterpret_cast<d2*>(p));
-    else
-        *reinterpret_cast<d2*>(p) = v;
+    __builtin_nontemporal_store(v, reinterpret_cast<d2*>(p));
+}
+
+// ring slots of the steady march: 2T rows in use + D in flight, even (the
+// colour of a chunk's first step is then the same for every chunk)
+template <int T, int D>
+__host__ __device__ constexpr int ring_slots() {
+    return 2 * T + D + (D & 1);
 }
 
 // per-lane constants shared by all stages
@@ -116,37 +133,38 @@ struct Lane {
     bool fixr_a, fixr_b;   // ia / ib == ni+1 on a physical right side
     bool st_a, st_b;       // columns this lane stores
     int lo_j, hi_j;        // updated rows
-    int j0, j1;            // owned rows
+    int j0, j1;            // owned (stored) rows
+    int wlo, whi;          // residual window reaches the physical bottom / top side
     int parity;
     int gb, gt, nj;
     double idx2, idy2, coef;
 };
 
 // How a step is compiled:
-//  kEdge   general: colour from the row, per-lane update / residual masks,
-//          ghost-row and ghost-column copies, row tests.  Blocks whose cone
-//          reaches a physical side (first/last strip, first/last block row).
-//  kWarm   interior: colour a constant, every streamed row is an updatable
-//          row (rows outside the valid cone hold garbage that never reaches a
-//          stored value); only the residual (select on the row's ownership)
-//          and the store are row-tested.  The 4T+1 warm-up and 2T drain steps.
-//  kSteady interior, every row touched is owned: no tests at all.
+//  kEdge    general: per-lane update / residual masks, ghost-row and
+//           ghost-column copies, row tests.  Strips at a physical left /
+//           right side.
+//  kPre     interior warm-up: every streamed row is an updatable row (rows
+//           outside the valid cone hold garbage that never reaches a stored
+//           value); no residual, no store.
+//  kSteady  interior, static ring: residual and store on every step.
 //  kRowEdge columns interior (every lane's two columns updated, ownership
-//          uniform per lane), rows general: the first/last block row at a
-//          physical bottom/top side.  Row tests and ghost-row copies are
-//          wave-uniform; no lane masks, the residual as in kWarm.
-enum { kEdge = 0, kWarm = 1, kSteady = 2, kRowEdge = 3 };
+//           uniform per lane), rows general: blocks whose cone reaches a
+//           physical bottom / top side, and a last block row whose height is
+//           not a multiple of the ring.  Row tests and ghost-row copies are
+//           wave-uniform; no lane masks.
+enum { kEdge = 0, kPre = 1, kSteady = 2, kRowEdge = 3 };
 
-// One iteration stage.  In = row rin of the previous stage's output (stage 1:
-// of the field in memory).  Returns row rin-2 of this stage's output.
-// fixrows (stages 2..T; a constant after unrolling): complete the previous
-// iteration's ghost-row copy on the incoming stream.  Stage 1 reads the ghost
-// rows as they are in memory -- the state after the previous pass, or
-// whatever the caller uploaded, as the reference's first iteration does.
-// Q: colour of the rows (0: column ia is red in row rin-1), -1 = from c.
-template <int Q, int MODE>
-__device__ __forceinline__ d2 stage(const Lane& c, bool fixrows, d2 In, int rin, d2& A, d2& M1,
-                                    d2& M2, d2 Ra, d2 Rb, double& acc) {
+// One iteration stage (stage index t, 0-based).  In = row rin of the previous
+// stage's output (stage 0: of the field in memory).  Returns row rin-2 of this
+// stage's output.  fixrows (stages 1..T-1; a constant after unrolling):
+// complete the previous iteration's ghost-row copy on the incoming stream.
+// Stage 0 reads the ghost rows as they are in memory -- the state after the
+// previous pass, or whatever the caller uploaded, as the reference's first
+// iteration does.  Q: colour of the rows (0: column ia is red in row rin-1).
+template <int T, int Q, int MODE>
+__device__ __forceinline__ d2 stage(const Lane& c, int t, bool fixrows, d2 In, int rin, d2& A,
+                                    d2& M1, d2& M2, d2 Ra, d2 Rb, double& acc) {
     constexpr bool EDGE = MODE == kEdge;                // lane masks
     constexpr bool ROWS = EDGE || MODE == kRowEdge;     // row tests, ghost rows
     if (ROWS && fixrows) {
@@ -161,59 +179,63 @@ __device__ __forceinline__ d2 stage(const Lane& c, bool fixrows, d2 In, int rin,
     }
     const int rr = rin - 1;  // red row
     const int rb = rin - 2;  // black row
-    const int q = Q >= 0 ? Q : ((c.parity + 1 + rr) & 1);
     const double idx2 = c.idx2, idy2 = c.idy2, coef = c.coef;
-    // r^2 into the stage's residual if (row, column) is owned
-    auto tally = [&](double r, bool own_row, bool own_col) {
+    // residual windows of this stage (header): red rows [j0 + sh, j1 + sh),
+    // black rows one lower, extended to the physical sides
+    const int sh = 2 * T - 1 - 2 * t;
+    auto tally = [&](double r, int row, int wsh, bool own_col) {
         if (MODE == kSteady) {
             acc = __builtin_fma(r, r, acc);
-        } else if (MODE == kWarm || MODE == kRowEdge) {
-            const double rm = own_row ? r : 0.0;  // uniform select: no branch, NaN-safe
-            acc = __builtin_fma(rm, rm, acc);
-        } else if (own_row && own_col) {
-            acc = __builtin_fma(r, r, acc);
+        } else if (MODE == kPre) {
+        } else {
+            const bool own_row = row >= (c.wlo ? 1 : c.j0 + wsh) &&
+                                 row < (c.whi ? c.nj + 1 : c.j1 + wsh);
+            if (!EDGE) {
+                const double rm = own_row ? r : 0.0;  // uniform select: no branch, NaN-safe
+                acc = __builtin_fma(rm, rm, acc);
+            } else if (own_row && own_col) {
+                acc = __builtin_fma(r, r, acc);
+            }
         }
     };
 
     // red pass on row rr
     d2 Mr = A;
     if (!ROWS || (rr >= c.lo_j && rr <= c.hi_j)) {
-        const bool own = (rr >= c.j0) && (rr < c.j1);
-        if (q == 0) {
+        if (Q == 0) {
             const double Lf = from_left(A.y);
             const double cc = A.x;
             const double r = Ra.x - ((m2c(A.y, cc) + Lf) * idx2 +
                                      (m2c(In.x, cc) + M1.x) * idy2);
             if (!EDGE || c.up_a) Mr.x = cc - coef * r;
-            tally(r, own, c.own_a);
+            tally(r, rr, sh, c.own_a);
         } else {
             const double Rf = from_right(A.x);
             const double cc = A.y;
             const double r = Ra.y - ((m2c(Rf, cc) + A.x) * idx2 +
                                      (m2c(In.y, cc) + M1.y) * idy2);
             if (!EDGE || c.up_b) Mr.y = cc - coef * r;
-            tally(r, own, c.own_b);
+            tally(r, rr, sh, c.own_b);
         }
     }
 
     // black pass on row rb (+ the ghost column copy of this finished row)
     d2 F = M1;
     if (!ROWS || (rb >= c.lo_j && rb <= c.hi_j)) {
-        const bool own = (rb >= c.j0) && (rb < c.j1);
-        if (q == 0) {
+        if (Q == 0) {
             const double Ln = from_left(M1.y);
             const double cc = M1.x;
             const double r = Rb.x - ((m2c(M1.y, cc) + Ln) * idx2 +
                                      (m2c(Mr.x, cc) + M2.x) * idy2);
             if (!EDGE || c.up_a) F.x = cc - coef * r;
-            tally(r, own, c.own_a);
+            tally(r, rb, sh - 1, c.own_a);
         } else {
             const double Rn = from_right(M1.x);
             const double cc = M1.y;
             const double r = Rb.y - ((m2c(Rn, cc) + M1.x) * idx2 +
                                      (m2c(Mr.y, cc) + M2.y) * idy2);
             if (!EDGE || c.up_b) F.y = cc - coef * r;
-            tally(r, own, c.own_b);
+            tally(r, rb, sh - 1, c.own_b);
         }
         if (EDGE) {
             const double f1 = from_right(F.x);  // column ib+1 (lane l+1's ia)
@@ -230,15 +252,13 @@ __device__ __forceinline__ d2 stage(const Lane& c, bool fixrows, d2 In, int rin,
 }
 
 // the registers of one wave's march
-template <int T, int D, int LR>
+template <int T, int D>
 struct March {
     d2 A[T], M1[T], M2[T];
-    // LR 0: register rhs ring, R[k] = rhs(r0 - 1 - k).  LR 2 (re-read): R[2t] =
-    // rhs(r0 - 2t - 1) for stage t >= 1, loaded during the previous step, and
-    // R[2t + 1] = rhs(r0 - 2t - 2), stage t's red row of the previous step
-    d2 R[LR == 1 ? 1 : 2 * T];
-    d2 Pq[D], Rq[D];       // rows in flight: p(r0 .. r0+D-1), rhs(r0-1 .. r0+D-2)
+    d2 R[2 * T];     // paired march: R[k] = rhs(r0 - 1 - k)
+    d2 Pq[D], Rq[D];  // rows in flight: p(r0 .. r0+D-1), rhs(r0-1 .. r0+D-2)
     double acc[T];
+    d2 keep[2];
 };
 
 struct Io {
@@ -246,115 +266,41 @@ struct Io {
     const double* rp;
     double* dp;
     long long pitch;
-    // LDS rhs ring (LDS_RING variants): this lane's element (row slot k,
-    // component c) at ring[k * 128 + c * 64].  Lane-private (a lane reads back
-    // only what it wrote: no barrier), component-major so each wave access is
-    // one contiguous 512-byte ds_*_b64.  Row x lives in slot x mod 2T.
-    double* ring;
-    // re-read rhs (LR == 2): buffer descriptor whose base is row rlo of this
-    // wave's strip (wave-uniform), lane byte offset, row stride in bytes
-    __amdgpu_buffer_rsrc_t rrs;
-    int lane_off, rlo, row_bytes;
-    // steady-state stores (SST variants): the strip's 128 columns of row 0 of
-    // dst as a wave-uniform address, and this lane's byte offset in a row, out
-    // of range (the store is dropped) on lanes that do not store
-    unsigned long long dwave;
-    unsigned st_off;
 };
 
-// LR >= 2: stages 1 .. K re-read their rhs rows (K = LR - 1, at most T - 1)
-template <int T, int LR>
-__device__ __forceinline__ constexpr int rr_stages() {
-    return LR - 1 < T - 1 ? LR - 1 : T - 1;
-}
-
-// slot of row x in a ring of 2T rows (x >= -kYOff - 2T - 1; scalar arithmetic)
-template <int T>
-__device__ __forceinline__ int ring_slot(int x) {
-    return (x + 2 * T * 64) % (2 * T);
-}
-
-// one step of the march: stream in old row r0, push it through the T stages,
+// one paired-march step: stream in old row r0, push it through the T stages,
 // store the row the last stage finished (r0 - 2T) if this block owns it
-template <int T, int D, int LR, int NT, int Q, int MODE>
-__device__ __forceinline__ void tb_step(March<T, D, LR>& m, const Lane& c, const Io& io, int r0) {
-    // NT bit 0: non-temporal stores; bit 1: branch-free steady-state stores
-    constexpr bool SST = (NT & 2) != 0;
+template <int T, int D, int Q, int MODE>
+__device__ __forceinline__ void tb_step(March<T, D>& m, const Lane& c, const Io& io, int r0) {
     const long long pitch = io.pitch;
     const d2 nP = ldv(io.sp + (long long)(r0 + D) * pitch);
     const d2 nR = ldv(io.rp + (long long)(r0 - 1 + D) * pitch);
-    if (LR == 1) {  // rhs(r0 - 1) joins the LDS ring
-        double* w = io.ring + ring_slot<T>(r0 - 1) * 128;
-        w[0] = m.Rq[0].x;
-        w[64] = m.Rq[0].y;
-    } else if (LR == 0) {
 #pragma unroll
-        for (int k = 2 * T - 1; k > 0; --k) m.R[k] = m.R[k - 1];
-        m.R[0] = m.Rq[0];
-    }
+    for (int k = 2 * T - 1; k > 0; --k) m.R[k] = m.R[k - 1];
+    m.R[0] = m.Rq[0];
 
     d2 v = m.Pq[0];
-    d2 Rk = d2{0.0, 0.0};  // LR >= 2: stage K's black rhs row, the ring's next newest
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         const d2 prevM2 = m.M2[t];
-        d2 Ra, Rb;
-        if (LR == 1) {  // only component q of rows r0-2t-1 (red) and r0-2t-2 (black) is used
-            const int q = Q >= 0 ? Q : ((c.parity + r0) & 1);
-            const double ra = io.ring[ring_slot<T>(r0 - 2 * t - 1) * 128 + q * 64];
-            const double rb = io.ring[ring_slot<T>(r0 - 2 * t - 2) * 128 + q * 64];
-            Ra = d2{ra, ra};
-            Rb = d2{rb, rb};
-        } else if (LR == 0) {
-            Ra = m.R[2 * t];
-            Rb = m.R[2 * t + 1];
-        } else {
-            Ra = t == 0 ? m.Rq[0] : m.R[2 * t];
-            Rb = m.R[2 * t + 1];
-        }
-        constexpr int K = LR >= 2 ? rr_stages<T, LR>() : 0;
-        v = stage<Q, MODE>(c, t > 0, v, r0 - 2 * t, m.A[t], m.M1[t], m.M2[t], Ra, Rb, m.acc[t]);
-        if (LR >= 2 && t <= K) {
-            // Rb is dead: its register takes next step's red row (loaded from L2:
-            // this wave streamed it 2t + D steps ago); rows below the stream
-            // start were zeros in the ring and only feed cells outside the cone
-            if (t == K) Rk = Rb;
-            m.R[2 * t + 1] = Ra;
-            if (t > 0) {
-                const int row = max(r0 - 2 * t, io.rlo);
-                m.R[2 * t] = __builtin_bit_cast(
-                    d2, __builtin_amdgcn_raw_buffer_load_b128(
-                            io.rrs, io.lane_off, (row - io.rlo) * io.row_bytes, 0));
-            }
-        }
-        if (t == T - 1) {
+        v = stage<T, Q, MODE>(c, t, t > 0, v, r0 - 2 * t, m.A[t], m.M1[t], m.M2[t], m.R[2 * t],
+                              m.R[2 * t + 1], m.acc[t]);
+        if (t == T - 1 && MODE != kPre) {
             const int jw = r0 - 2 * T;  // row finished by the last stage
-            if (MODE == kSteady && SST) {
-                // no branch around the store: the two steps of a colour pair stay one
-                // basic block, which the scheduler can interleave
-                const unsigned long long a = io.dwave + (unsigned long long)jw * (pitch * 8);
-                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                    (void*)a, (short)0, kStripCells * 8, 0x00020000);
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), rs, io.st_off,
-                                                       0, (NT & 1) ? 2 : 0);
-            } else if (MODE == kSteady) {
-                if (c.st_a) stv<(NT & 1) != 0>(io.dp + (long long)jw * pitch, v);
-            } else if (MODE == kWarm) {
-                if (jw >= c.j0 && jw < c.j1 && c.st_a) stv<(NT & 1) != 0>(io.dp + (long long)jw * pitch, v);
-            } else if (MODE == kRowEdge) {
+            if (MODE == kRowEdge) {
                 // every column of the lane updated and stored alike (st_a == st_b);
                 // ghost rows 0 / nj+1 of the stored field are copies of rows 1 / nj
                 if (jw >= c.j0 && jw < c.j1 && c.st_a) {
                     double* drow = io.dp + (long long)jw * pitch;
-                    stv<(NT & 1) != 0>(drow, v);
-                    if (c.gb && jw == 1) stv<(NT & 1) != 0>(drow - pitch, v);
-                    if (c.gt && jw == c.nj) stv<(NT & 1) != 0>(drow + pitch, v);
+                    stv(drow, v);
+                    if (c.gb && jw == 1) stv(drow - pitch, v);
+                    if (c.gt && jw == c.nj) stv(drow + pitch, v);
                 }
             } else if (jw >= c.j0 && jw < c.j1) {
                 double* drow = io.dp + (long long)jw * pitch;
                 auto put = [&](double* p, d2 o) {
                     if (c.st_a && c.st_b) {
-                        stv<(NT & 1) != 0>(p, o);
+                        stv(p, o);
                     } else if (c.st_a) {
                         p[0] = o.x;
                     } else if (c.st_b) {
@@ -375,14 +321,6 @@ __device__ __forceinline__ void tb_step(March<T, D, LR>& m, const Lane& c, const
             }
         }
     }
-    if (LR >= 2) {
-        // stages K+1 .. T-1 keep the register ring, R[k] = rhs(r0 - 1 - k) for
-        // k >= 2K + 2 (shifted after every stage has read it)
-        constexpr int K = rr_stages<T, LR>();
-#pragma unroll
-        for (int k = 2 * T - 1; k > 2 * K + 2; --k) m.R[k] = m.R[k - 1];
-        if (K < T - 1) m.R[2 * K + 2] = Rk;
-    }
 #pragma unroll
     for (int k = 0; k + 1 < D; ++k) {
         m.Pq[k] = m.Pq[k + 1];
@@ -392,70 +330,121 @@ __device__ __forceinline__ void tb_step(March<T, D, LR>& m, const Lane& c, const
     m.Rq[D - 1] = nR;
 }
 
-// Interior blocks: the colour alternates by row, so steps go in pairs with
-// the colour a constant (Q0 = colour of row r0).  Steps r0 in
-// [j0+2T+1, j1-1] touch only owned rows and store unconditionally (kSteady);
-// the 4T+1 warm-up steps before and the 2T drain steps after are kWarm.
-template <int T, int D, int LR, int NT, int Q0>
-__device__ __forceinline__ void march_interior_q(March<T, D, LR>& m, const Lane& c,
-                                                 const Io& io, int r0, int rend) {
-    const int sbeg = c.j0 + 2 * T + 1, send = c.j1 - 1;
-    // warm-up, in pairs (keeps the colour phase); may run into the steady range
-    for (; r0 + 1 < sbeg && r0 + 1 <= rend; r0 += 2) {
-        tb_step<T, D, LR, NT, Q0, kWarm>(m, c, io, r0);
-        tb_step<T, D, LR, NT, 1 - Q0, kWarm>(m, c, io, r0 + 1);
-    }
-    for (; r0 + 1 <= send; r0 += 2) {
-        tb_step<T, D, LR, NT, Q0, kSteady>(m, c, io, r0);
-        tb_step<T, D, LR, NT, 1 - Q0, kSteady>(m, c, io, r0 + 1);
-    }
+// paired march over steps r0 = rs .. rend (the colour Q0 of row rs a constant)
+template <int T, int D, int Q0, int MODE>
+__device__ __forceinline__ void march_pairs(March<T, D>& m, const Lane& c, const Io& io, int r0,
+                                            int rend) {
     for (; r0 + 1 <= rend; r0 += 2) {
-        tb_step<T, D, LR, NT, Q0, kWarm>(m, c, io, r0);
-        tb_step<T, D, LR, NT, 1 - Q0, kWarm>(m, c, io, r0 + 1);
+        tb_step<T, D, Q0, MODE>(m, c, io, r0);
+        tb_step<T, D, 1 - Q0, MODE>(m, c, io, r0 + 1);
     }
-    if (r0 <= rend) tb_step<T, D, LR, NT, Q0, kWarm>(m, c, io, r0);
+    if (r0 <= rend) tb_step<T, D, Q0, MODE>(m, c, io, r0);
 }
 
-// Blocks with a physical side in their cone (kEdge / kRowEdge): every step
-// general, but still in colour pairs so the colour is a compile-time constant.
-template <int T, int D, int LR, int NT, int Q0, int MODE>
-__device__ __forceinline__ void march_edge_q(March<T, D, LR>& m, const Lane& c, const Io& io,
-                                             int r0, int rend) {
-    for (; r0 + 1 <= rend; r0 += 2) {
-        tb_step<T, D, LR, NT, Q0, MODE>(m, c, io, r0);
-        tb_step<T, D, LR, NT, 1 - Q0, MODE>(m, c, io, r0 + 1);
+// Steady march: buffer descriptors over the wave's strip (wave-uniform base,
+// lane byte offset); the byte offset of a row is a scalar
+struct Sio {
+    __amdgpu_buffer_rsrc_t p, r, d;  // p rows from rs, rhs rows from rs-1, dst rows from j0
+    unsigned lane;                   // lane * 16
+    unsigned st_lane;                // lane * 16 if the lane stores, else out of range
+    unsigned row_bytes;              // pitch * 8
+};
+
+__device__ __forceinline__ d2 bload(__amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned soff) {
+    return __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
+}
+
+// one step of the steady march: stream row r0 = rs + n, tally and store.  PH
+// = n mod S (a constant): rhs row rs - 1 + j lives in ring slot j mod S, and
+// stage t reads rows j = n - 2t (red) and n - 2t - 1 (black)
+template <int T, int D, int Q, int PH>
+__device__ __forceinline__ void steady_step(March<T, D>& m, d2* R, const Lane& c, const Sio& io,
+                                            int r0, unsigned off_n) {
+    constexpr int S = ring_slots<T, D>();
+    // p row r0 + D (p descriptor starts at row rs), rhs row r0 - 1 + D (rhs
+    // descriptor starts at row rs - 1): both n + D rows in; the rhs row lands
+    // in the slot of the row stage T-1 finished with in the previous step
+    const unsigned ld = off_n + (unsigned)D * io.row_bytes;
+    const d2 nP = bload(io.p, io.lane, ld);
+    R[(PH + D) % S] = bload(io.r, io.lane, ld);
+    d2 v = m.Pq[0];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        v = stage<T, Q, kSteady>(c, t, t > 0, v, r0 - 2 * t, m.A[t], m.M1[t], m.M2[t],
+                                 R[(PH - 2 * t + 4 * S) % S], R[(PH - 2 * t - 1 + 4 * S) % S],
+                                 m.acc[t]);
     }
-    if (r0 <= rend) tb_step<T, D, LR, NT, Q0, MODE>(m, c, io, r0);
+    // row r0 - 2T = j0 + (n - 4T): dst descriptor starts at row j0; lanes that
+    // do not store carry an out-of-range offset (the write is dropped)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), io.d, io.st_lane,
+                                           off_n - 4u * T * io.row_bytes, 2);
+    // The store reads its data VGPRs after it issues, and on gfx950 a later
+    // buffer_load can land in those VGPRs first: with the registers of step
+    // n's row reused by a load a few instructions after the store, lanes 12-15
+    // of every 16 stored the loaded rhs instead (tools/debug_tb.py).
+    // The compiler does not guard this, so the row stays live through the
+    // next two steps' loads (one step already suffices in every test).
+    asm volatile("" ::"v"(m.keep[0]));
+    m.keep[0] = m.keep[1];
+    m.keep[1] = v;
+#pragma unroll
+    for (int k = 0; k + 1 < D; ++k) m.Pq[k] = m.Pq[k + 1];
+    m.Pq[D - 1] = nP;
+    // steps are scheduled one at a time (one basic block per chunk, but no
+    // code motion across steps: measured faster, 0.856 vs 0.867 ms/iteration)
+    __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int T, int D, int LR, int NT, int MODE>
-__device__ __forceinline__ void march_edge(March<T, D, LR>& m, const Lane& c, const Io& io,
-                                           int rs, int rend) {
-    if (((c.parity + rs) & 1) == 0)
-        march_edge_q<T, D, LR, NT, 0, MODE>(m, c, io, rs, rend);
-    else
-        march_edge_q<T, D, LR, NT, 1, MODE>(m, c, io, rs, rend);
+// S steps of the steady march, the first at slot phase P0 (colour Q0)
+template <int T, int D, int Q0, int P0, int... NN>
+__device__ __forceinline__ void steady_chunk(March<T, D>& m, d2* R, const Lane& c, const Sio& io,
+                                             int r0, unsigned off_n,
+                                             std::integer_sequence<int, NN...>) {
+    constexpr int S = ring_slots<T, D>();
+    (steady_step<T, D, Q0 ^ (NN & 1), (P0 + NN) % S>(m, R, c, io, r0 + NN,
+                                                       off_n + (unsigned)NN * io.row_bytes),
+     ...);
 }
 
-template <int T, int D, int LR, int NT>
-__device__ __forceinline__ void march_interior(March<T, D, LR>& m, const Lane& c, const Io& io,
-                                               int rs, int rend) {
-    if (((c.parity + rs) & 1) == 0)
-        march_interior_q<T, D, LR, NT, 0>(m, c, io, rs, rend);
-    else
-        march_interior_q<T, D, LR, NT, 1>(m, c, io, rs, rend);
+// interior block of H = k * S rows: 4T paired warm-up steps, then k chunks of
+// S statically unrolled steps
+template <int T, int D, int Q0>
+__device__ __forceinline__ void march_interior(March<T, D>& m, const Lane& c, const Io& io,
+                                               const Sio& sio, int rs, int nchunks) {
+    constexpr int S = ring_slots<T, D>();
+    march_pairs<T, D, Q0, kPre>(m, c, io, rs, rs + 4 * T - 1);  // 4T is even
+    // ring in static slots: rhs row rs - 1 + j in slot j mod S; at step n = 4T
+    // the paired ring holds j = 4T - 1 - k (k < 2T), the rows in flight j = 4T + k
+    d2 R[S];
+#pragma unroll
+    for (int k = 0; k < S; ++k) R[k] = d2{0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < 2 * T; ++k) R[(4 * T - 1 - k) % S] = m.R[k];
+#pragma unroll
+    for (int k = 0; k < D; ++k) R[(4 * T + k) % S] = m.Rq[k];
+    // every chunk starts at slot phase 4T mod S (S is even, so colour Q0 too)
+    constexpr int P0 = (4 * T) % S;
+    int r0 = rs + 4 * T;
+    unsigned off = 4u * T * sio.row_bytes;
+    for (int k = 0; k < nchunks; ++k) {
+        steady_chunk<T, D, Q0, P0>(m, R, c, sio, r0, off, std::make_integer_sequence<int, S>{});
+        r0 += S;
+        off += (unsigned)S * sio.row_bytes;
+    }
 }
 
 }  // namespace
 
-template <int T, int WAVES, int D, int LR, int MINW, int NT>
-__global__ __launch_bounds__(kLanes* WAVES, MINW) void rb_tb_kernel(
+// occupancy target: 2 waves per SIMD (the register file of one wave is 256
+// VGPRs; below that the compiler would rather use AGPRs and run one wave)
+template <int T, int WAVES, int D>
+__global__ __launch_bounds__(kLanes* WAVES, 2) void rb_tb_kernel(
     SweepParams prm, const double* __restrict__ src, double* __restrict__ dst,
     const double* __restrict__ rhs, double* __restrict__ partials,
     const DevState* __restrict__ st, int force) {
     constexpr int OW = kStripCells - 4 * T;
+    constexpr int S = ring_slots<T, D>();
     __shared__ double wsum[T][WAVES];
-    __shared__ double ring[LR == 1 ? WAVES : 1][LR == 1 ? 2 * T * kStripCells : 1];
     if (!force && st->done) return;
 
     int L = blockIdx.x;
@@ -465,8 +454,10 @@ __global__ __launch_bounds__(kLanes* WAVES, MINW) void rb_tb_kernel(
     }
     const int bx = L % prm.nbx, by = L / prm.nbx;
     const int ni = prm.ni, nj = prm.nj;
-    const int j0 = 1 + (int)(((long long)by * nj) / prm.nby);
-    const int j1 = 1 + (int)(((long long)(by + 1) * nj) / prm.nby);
+    // block rows of H = rows_per_block rows; the last one takes the rest
+    const int H = prm.rows_per_block;
+    const int j0 = 1 + by * H;
+    const int j1 = by == prm.nby - 1 ? nj + 1 : j0 + H;
     if (prm.part != 0) {  // overlapped decomposed pass: blocks clear of the halo first
         const int lo = 1 + bx * WAVES * OW - 2 * T;
         const int hi = 1 + (bx * WAVES + WAVES - 1) * OW - 2 * T + kStripCells - 1;
@@ -500,6 +491,8 @@ __global__ __launch_bounds__(kLanes* WAVES, MINW) void rb_tb_kernel(
     c.hi_j = prm.upd_hi_j;
     c.j0 = j0;
     c.j1 = j1;
+    c.wlo = by == 0 && prm.ghost_bottom;
+    c.whi = by == prm.nby - 1 && prm.ghost_top;
     c.parity = prm.parity;
     c.gb = prm.ghost_bottom;
     c.gt = prm.ghost_top;
@@ -508,9 +501,10 @@ __global__ __launch_bounds__(kLanes* WAVES, MINW) void rb_tb_kernel(
     c.idy2 = prm.idy2;
     c.coef = prm.coef;
 
-    March<T, D, LR> m;
+    March<T, D> m;
 #pragma unroll
     for (int t = 0; t < T; ++t) m.acc[t] = 0.0;
+    m.keep[0] = m.keep[1] = d2{0.0, 0.0};
 
     // physical corners are never touched by solveRB; carry them into dst
     if (L == 0 && threadIdx.x < 4) {
@@ -526,8 +520,7 @@ __global__ __launch_bounds__(kLanes* WAVES, MINW) void rb_tb_kernel(
 
     if (c_out <= ni) {  // wave-uniform
         const long long base = (long long)kYOff * pitch + kXOff + c.ia;
-        Io io{src + base, rhs + base, dst + base, pitch,
-              LR == 1 ? &ring[LR == 1 ? wave : 0][LR == 1 ? lane : 0] : nullptr};
+        Io io{src + base, rhs + base, dst + base, pitch};
         const int rs = j0 - 2 * T;  // first streamed row
         const int rend = j1 - 1 + 2 * T;
 #pragma unroll
@@ -537,52 +530,50 @@ __global__ __launch_bounds__(kLanes* WAVES, MINW) void rb_tb_kernel(
         }
 #pragma unroll
         for (int t = 0; t < T; ++t) m.A[t] = m.M1[t] = m.M2[t] = d2{0.0, 0.0};
-        if (NT & 2) {
-            const unsigned long long a =
-                (unsigned long long)(dst + (long long)kYOff * pitch + kXOff + c_ld);
-            const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
-            const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
-            io.dwave = ((unsigned long long)hi << 32) | lo;
-            io.st_off = c.st_a ? (unsigned)lane * 16u : 0x80000000u;
-        }
-        if (LR >= 2) {
-            // wave-uniform descriptor over rows rs-1 .. rend of the strip's
-            // 128 columns (the base is made scalar explicitly)
-            io.rlo = rs - 1;
-            io.row_bytes = (int)(pitch * 8);
-            io.lane_off = lane * 16;
-            const long long off = ((long long)(kYOff + rs - 1) * pitch + kXOff + c_ld) * 8;
-            const unsigned long long a = (unsigned long long)(const char*)rhs + off;
-            const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
-            const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
-            const int nrec = (rend - rs + 2) * io.row_bytes;
-            io.rrs = __builtin_amdgcn_make_buffer_rsrc(
-                (void*)(((unsigned long long)hi << 32) | lo), (short)0, nrec, 0x00020000);
-        }
-        if (LR == 1) {
 #pragma unroll
-            for (int k = 0; k < 4 * T; ++k) io.ring[k * 64] = 0.0;
-        } else {
-#pragma unroll
-            for (int k = 0; k < 2 * T; ++k) m.R[k] = d2{0.0, 0.0};
-        }
+        for (int k = 0; k < 2 * T; ++k) m.R[k] = d2{0.0, 0.0};
+        // the colour of row rs: the same for every block of the launch (H even)
+        const bool q1 = ((c.parity + rs) & 1) != 0;
 
         // columns interior: every column of the cone an updated cell (no lane
         // masks, no ghost columns) and ownership uniform per lane -- the strip
         // is whole, or it runs past column ni into a neighbour's halo (or the
         // padding beyond it) with ni even, so ni | ni+1 falls between lanes;
         // those lanes are neither stored nor counted.  Rows interior: no
-        // ghost rows in the cone.
+        // ghost rows in the cone, and a block height the static ring divides.
         const bool cols_in = c_ld >= prm.upd_lo_i && c_ld + kStripCells - 1 <= prm.upd_hi_i &&
                              (c_out + OW - 1 <= ni || (ni & 1) == 0);
-        const bool rows_in = rs >= prm.upd_lo_j && rend <= prm.upd_hi_j;
+        const bool rows_in = rs >= prm.upd_lo_j && rend <= prm.upd_hi_j &&
+                             (j1 - j0) % S == 0 && j1 - j0 > 0;
         if (!cols_in) {
-            march_edge<T, D, LR, NT, kEdge>(m, c, io, rs, rend);
+            if (q1) march_pairs<T, D, 1, kEdge>(m, c, io, rs, rend);
+            else    march_pairs<T, D, 0, kEdge>(m, c, io, rs, rend);
         } else {
-            if (rows_in)
-                march_interior<T, D, LR, NT>(m, c, io, rs, rend);
-            else
-                march_edge<T, D, LR, NT, kRowEdge>(m, c, io, rs, rend);
+            if (rows_in) {
+                // wave-uniform descriptors over the strip's 128 columns
+                auto rsrc = [&](const double* b, int row0, int rows) {
+                    const unsigned long long a = (unsigned long long)(
+                        b + (long long)(kYOff + row0) * pitch + kXOff + c_ld);
+                    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+                    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+                    return __builtin_amdgcn_make_buffer_rsrc(
+                        (void*)(((unsigned long long)hi << 32) | lo), (short)0,
+                        (int)((long long)rows * pitch * 8), 0x00020000);
+                };
+                Sio sio;
+                sio.p = rsrc(src, rs, rend - rs + 1 + D);
+                sio.r = rsrc(rhs, rs - 1, rend - rs + 1 + D);
+                sio.d = rsrc(dst, j0, j1 - j0);
+                sio.lane = (unsigned)lane * 16u;
+                sio.st_lane = c.own_a ? (unsigned)lane * 16u : 0x40000000u;
+                sio.row_bytes = (unsigned)(pitch * 8);
+                const int nchunks = (j1 - j0) / S;
+                if (q1) march_interior<T, D, 1>(m, c, io, sio, rs, nchunks);
+                else    march_interior<T, D, 0>(m, c, io, sio, rs, nchunks);
+            } else {
+                if (q1) march_pairs<T, D, 1, kRowEdge>(m, c, io, rs, rend);
+                else    march_pairs<T, D, 0, kRowEdge>(m, c, io, rs, rend);
+            }
             if (!c.own_a) {
 #pragma unroll
                 for (int t = 0; t < T; ++t) m.acc[t] = 0.0;
@@ -610,6 +601,11 @@ int tb_out_width(int T) { return kStripCells - 4 * T; }
 
 int tb_waves(int variant) { return kTbVariants[variant].waves; }
 
+int tb_ring_slots(int T, int variant) {
+    const int D = kTbVariants[variant].ahead;
+    return 2 * T + D + (D & 1);
+}
+
 int tb_nbx(int ni, int T, int waves) {
     const int ow = tb_out_width(T);
     const int strips = (ni + ow - 1) / ow;
@@ -618,43 +614,41 @@ int tb_nbx(int ni, int T, int waves) {
 
 void launch_tb(hipStream_t s, int T, const SweepParams& prm, const double* src, double* dst,
                const double* rhs, double* partials, const DevState* st, int force) {
-#define TB(TT, W, DD, LR, MW)                                                  \
-    hipLaunchKernelGGL((rb_tb_kernel<TT, W, DD, LR, MW, true>), dim3(prm.nblocks), \
-                       dim3(kLanes * W), 0, s, prm, src, dst, rhs, partials, st, force)
-#define TBN(TT, W, DD, LR, MW, NTF)                                           \
-    hipLaunchKernelGGL((rb_tb_kernel<TT, W, DD, LR, MW, NTF>), dim3(prm.nblocks), \
-                       dim3(kLanes * W), 0, s, prm, src, dst, rhs, partials, st, force)
-#define TB_T(TT)                              \
-    switch (prm.variant) {                    \
-    case 0: TB(TT, 4, 2, false, 1); break;    \
-    case 1: TB(TT, 8, 2, false, 1); break;    \
-    case 2: TB(TT, 4, 3, false, 1); break;    \
-    case 3: TB(TT, 4, 2, true, 1); break;     \
-    case 4: TB(TT, 4, 2, true, (TT <= 4 ? 4 : 1)); break; \
-    case 5: TB(TT, 4, 3, true, 1); break;     \
-    case 6: TB(TT, 8, 2, true, 1); break;     \
-    case 7: TB(TT, 6, 2, true, 1); break;     \
-    case 8: TB(TT, 2, 3, false, 1); break;    \
-    case 9: TB(TT, 1, 3, false, 1); break;    \
-    case 14: TBN(TT, 4, 3, 0, 1, 3); break;   \
-    case 10: TB(TT, 4, 3, 8, 1); break;       \
-    case 11: TB(TT, 4, 3, 2, 1); break;       \
-    case 12: TB(TT, 4, 3, 3, 1); break;       \
-    default: TB(TT, 4, 3, 4, 1); break;       \
+#define TB(TT, W, DD)                                                                \
+    hipLaunchKernelGGL((rb_tb_kernel<TT, W, DD>), dim3(prm.nblocks), dim3(kLanes * W), 0, s, \
+                       prm, src, dst, rhs, partials, st, force)
+#define TB_T(TT)                       \
+    switch (prm.variant) {             \
+    case 1: TB(TT, 8, 2); break;       \
+    case 2: TB(TT, 2, 2); break;       \
+    case 3: TB(TT, 1, 2); break;       \
+    case 4: TB(TT, 4, 3); break;       \
+    default: TB(TT, 4, 2); break;      \
     }
     // must match kTbVariants (misor_internal.h)
+#ifdef MISOR_TB_QUICK  // experiment builds only: T = 7..9, default variant
     switch (T) {
-    case 1: TB_T(1); break;
+    case 7: TB(7, 4, 2); break;
+    case 8: TB(8, 4, 2); break;
+    default: TB(9, 4, 2); break;
+    }
+#else
+    switch (T) {
+    case 1: TB_T(1); break;  // the last pass of a capped solve, or a recompute
     case 2: TB_T(2); break;
     case 3: TB_T(3); break;
     case 4: TB_T(4); break;
     case 5: TB_T(5); break;
     case 6: TB_T(6); break;
     case 7: TB_T(7); break;
-    default: TB_T(8); break;
+    case 8: TB_T(8); break;
+    case 9: TB_T(9); break;
+    case 10: TB_T(10); break;
+    case 11: TB_T(11); break;
+    default: TB_T(12); break;
     }
+#endif
 #undef TB_T
-#undef TBN
 #undef TB
 }
 

@@ -56,7 +56,9 @@ class Local(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("sweeps", C.c_longlong), ("launches", C.c_longlong), ("sweep_ms", C.c_double),
                 ("timed_sweeps", C.c_longlong), ("timed_passes", C.c_longlong),
-                ("iters_per_pass", C.c_int), ("pad_", C.c_int)]
+                ("iters_per_pass", C.c_int), ("pad_", C.c_int),
+                ("halo_ms", C.c_double), ("halos", C.c_longlong),
+                ("allreduce_ms", C.c_double), ("allreduces", C.c_longlong)]
 
 
 class Desc3(C.Structure):
@@ -310,7 +312,8 @@ class Grid:
         _check(lib().misor_get_stats(self.h, C.byref(s)))
         return {"sweeps": s.sweeps, "launches": s.launches, "sweep_ms": s.sweep_ms,
                 "timed_sweeps": s.timed_sweeps, "timed_passes": s.timed_passes,
-                "iters_per_pass": s.iters_per_pass}
+                "iters_per_pass": s.iters_per_pass, "halo_ms": s.halo_ms, "halos": s.halos,
+                "allreduce_ms": s.allreduce_ms, "allreduces": s.allreduces}
 
     def reset_stats(self):
         _check(lib().misor_reset_stats(self.h))

@@ -84,7 +84,7 @@ def main():
 
 def main_tb(args):
     n = args.size
-    sweeps = args.sweeps - args.sweeps % 12 or 12  # whole passes for T = 1..4
+    sweeps = args.sweeps
     g = M.Grid(n, n, 1.0 / n, 1.0 / n, 1.9, 1e-300, sweeps, device=0)
     g.poisson_init(1.0, 1.0, 2)
     g.enable_timing(True)
@@ -93,13 +93,16 @@ def main_tb(args):
                                     [int(r) for r in args.rows.split(",")]))
     times = {c: [] for c in combos}
     for rnd in range(args.rounds):
+        # untimed lead-in: the first solve of a round runs slow (clocks ramp)
+        g.set_tuning(M.TUNE_TSTEPS, combos[0][0])
+        g.solve_rb(itermax=combos[0][0] * max(1, args.sweeps // combos[0][0]))
         for c in combos:
             T, v, rows = c
             g.set_tuning(M.TUNE_TSTEPS, T)
             g.set_tuning(M.TUNE_TB_VARIANT, v)
             g.set_tuning(M.TUNE_TB_ROWS, rows)
             g.reset_stats()
-            g.solve_rb(itermax=sweeps)
+            g.solve_rb(itermax=T * max(1, args.sweeps // T))  # whole passes of T
             st = g.stats()
             assert st["iters_per_pass"] == T
             times[c].append(st["sweep_ms"] / st["timed_sweeps"])  # per iteration

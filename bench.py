@@ -513,6 +513,27 @@ def main():
                          "note": "24 B/LUP x iterations per launch / launch time; exceeds "
                                  "the HBM peak because one pass carries T iterations"}},
     }
+    if world > 1:
+        # the decomposed loop's communication (HIP events on the stream that
+        # runs it, misor_stats): per exchange / all-reduce, and how much of it
+        # the interior sweeps hide -- per pass, the wall time beyond the sweep
+        # kernels' own span is the exposed communication (max over ranks)
+        passes_all = max(st["timed_passes"], 1)
+        vals = [st["halo_ms"] / max(st["halos"], 1), st["allreduce_ms"] / max(st["allreduces"], 1),
+                st["sweep_ms"] / passes_all, elapsed * 1e3 / passes_all,
+                (st["halo_ms"] + st["allreduce_ms"]) / passes_all]
+        tt = torch.tensor(vals, dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        halo, ared, comp, wall, comm = tt.tolist()
+        exposed = max(0.0, wall - comp)
+        out["comm"] = {"halo_ms_per_exchange": round(halo, 4),
+                       "allreduce_ms_per_call": round(ared, 4),
+                       "sweep_ms_per_pass": round(comp, 4), "wall_ms_per_pass": round(wall, 4),
+                       "comm_ms_per_pass": round(comm, 4),
+                       "overlap": round(1.0 - min(1.0, exposed / comm), 3) if comm > 0 else None,
+                       "transport": "RCCL send/recv (pack/unpack kernels) + ncclAllReduce",
+                       "note": "max over ranks; overlap = 1 - (wall - sweep span) / comm time "
+                               "per pass"}
     if pmc.get("sq"):
         # what actually bounds the temporally blocked kernel: VALU issue
         # (SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES per wave, 2 waves per SIMD)

@@ -198,13 +198,17 @@ enum {
     MISOR_TUNE_OVERLAP = 5,        /* decomposed: 1 (default) = halo exchange and residual
                                     * all-reduce on a second stream, overlapped with the
                                     * interior blocks of the sweep; 0 = serial */
-    MISOR_TUNE_TSTEPS = 6,         /* iterations per pass over HBM, 1..8: 1 = single-
+    MISOR_TUNE_TSTEPS = 6,         /* iterations per pass over HBM, 1..12: 1 = single-
                                     * iteration sweep kernel, T >= 2 = temporally blocked
                                     * kernel (T iterations per read of p and rhs); the
                                     * iteration count and every bit of p are unchanged */
-    MISOR_TUNE_TB_VARIANT = 7,     /* temporally blocked kernel: 0..13 strips x rows in flight
-                                    * x rhs ring in registers / LDS / re-read from L2 */
-    MISOR_TUNE_TB_ROWS = 8         /* temporally blocked kernel: rows per block; <= 0: auto */
+    MISOR_TUNE_TB_VARIANT = 7,     /* temporally blocked kernel: 0..4 strips per workgroup x
+                                    * rows in flight */
+    MISOR_TUNE_TB_ROWS = 8,        /* temporally blocked kernel: rows per block; <= 0: auto
+                                    * (a multiple of the kernel's rhs ring) */
+    MISOR_TUNE_TB_PERSISTENT = 9   /* temporally blocked kernel: 1 (default) = as many
+                                    * workgroups as are resident, taking blocks from per-XCD
+                                    * work queues; 0 = one workgroup per block */
 };
 int misor_set_tuning(misor_grid* g, int key, int value);
 int misor_get_tuning(const misor_grid* g, int key, int* value);

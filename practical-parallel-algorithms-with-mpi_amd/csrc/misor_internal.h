@@ -59,6 +59,8 @@ constexpr int kDefaultSweepVariant = 7;  // 8 strips, 2 rows ahead, nt stores (t
 int sweep_waves(int variant);
 
 // temporally blocked sweep (sor_tb.hip): strips per workgroup, rows in flight
+// (x-neighbour shifts through ds_bpermute instead of DPP -- the kernel's BP
+// template flag -- measured 5% slower: profiles/r02_tune_bperm.txt)
 struct TbVariant {
     int waves, ahead;
 };
@@ -68,9 +70,13 @@ constexpr int kDefaultTsteps = 7;      // iterations per pass
 constexpr int kDefaultTbVariant = 0;   // 4 strips, 2 rows in flight
 constexpr int kDefaultTbRows = 192;    // target rows per block (misor_api.hip pick_tb_nby) ...
 constexpr int kMinTbRows = 48;         // ... halved down to this while a launch has < 1024 WGs
+constexpr int kTbSmallRows = 32;       // short block rows the work order takes last ...
+constexpr int kTbSmallRounds = 2;      // ... about this many resident rounds of them
 int tb_waves(int variant);
 // rhs ring slots of the steady march: interior block heights are multiples of it
 int tb_ring_slots(int T, int variant);
+// workgroups of a persistent pass resident on the device at once
+int tb_resident(int T, int variant);
 int tb_out_width(int T);
 int tb_nbx(int ni, int T, int waves);           // block columns of a pass of T iterations
 
@@ -90,9 +96,10 @@ struct DevState {
 struct SweepParams {
     long long pitch;
     int ni, nj;          // local interior size
-    int rows_per_block;  // H (temporally blocked: the tallest block, ceil(nj / nby))
-    int nby;             // temporally blocked: block rows; block row by owns rows
-                         // [1 + by*nj/nby, 1 + (by+1)*nj/nby) -- heights differ by <= 1
+    int rows_per_block;  // H (temporally blocked: block rows 0 .. nby_big-1 are H tall)
+    int nby;             // temporally blocked: block rows; rows nby_big .. nby-2 are
+                         // h_small tall, the last one takes the rest
+    int nby_big, h_small;
     int parity;          // (ioff + joff) & 1 : global colour of local cell (0,0)
     int ghost_left, ghost_right, ghost_bottom, ghost_top;  // physical boundary -> Neumann copy
     int red_lo_i, red_hi_i, red_lo_j, red_hi_j;  // cells whose red value is computed
@@ -126,8 +133,10 @@ void launch_decide(hipStream_t s, DevState* st, int T, double cells);
 constexpr int kFinishChunks = 32;
 void launch_finish2(hipStream_t s, const double* partials, int nparts, int T, DevState* st,
                     double cells, double* scratch);
+// queue: 8 device ints (zeroed by the launch) for a persistent launch whose
+// workgroups take blocks from per-XCD queues; nullptr: one workgroup per block
 void launch_tb(hipStream_t s, int T, const SweepParams& prm, const double* src, double* dst,
-               const double* rhs, double* partials, const DevState* st, int force);
+               const double* rhs, double* partials, const DevState* st, int force, int* queue);
 // lexicographic Gauss-Seidel SOR, whole solve in one workgroup (lex_kernels.hip)
 void launch_solve_lex(hipStream_t s, double* p, const double* rhs, int ni, int nj,
                       long long pitch, double idx2, double idy2, double factor, double cells,

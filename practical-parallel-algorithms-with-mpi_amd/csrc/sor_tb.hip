@@ -74,6 +74,7 @@
 //
 // Bit-exactness: same expression order as the reference, -ffp-contract=off.
 
+#include <algorithm>
 #include <utility>
 
 #include "misor_internal.h"
@@ -95,6 +96,13 @@ __device__ __forceinline__ double from_left(double v) {
 __device__ __forceinline__ double from_right(double v) {
     return __hiloint2double(__builtin_amdgcn_mov_dpp(__double2hiint(v), 0x130, 0xf, 0xf, true),
                             __builtin_amdgcn_mov_dpp(__double2loint(v), 0x130, 0xf, 0xf, true));
+}
+
+// the same shifts through the LDS crossbar (ds_bpermute: an LDS-pipe
+// instruction, so the shift costs no VALU issue slot); addr = source lane * 4
+__device__ __forceinline__ double bperm(double v, int addr) {
+    return __hiloint2double(__builtin_amdgcn_ds_bpermute(addr, __double2hiint(v)),
+                            __builtin_amdgcn_ds_bpermute(addr, __double2loint(v)));
 }
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -137,6 +145,7 @@ struct Lane {
     int wlo, whi;          // residual window reaches the physical bottom / top side
     int parity;
     int gb, gt, nj;
+    int bl, br;            // ds_bpermute addresses of lanes l-1 and l+1
     double idx2, idy2, coef;
 };
 
@@ -162,9 +171,12 @@ enum { kEdge = 0, kPre = 1, kSteady = 2, kRowEdge = 3 };
 // Stage 0 reads the ghost rows as they are in memory -- the state after the
 // previous pass, or whatever the caller uploaded, as the reference's first
 // iteration does.  Q: colour of the rows (0: column ia is red in row rin-1).
-template <int T, int Q, int MODE>
+template <int T, int Q, int MODE, bool BP = false>
 __device__ __forceinline__ d2 stage(const Lane& c, int t, bool fixrows, d2 In, int rin, d2& A,
                                     d2& M1, d2& M2, d2 Ra, d2 Rb, double& acc) {
+    // BP: x-neighbours through ds_bpermute instead of DPP (interior modes)
+    auto fl = [&](double v) { return BP ? bperm(v, c.bl) : from_left(v); };
+    auto fr = [&](double v) { return BP ? bperm(v, c.br) : from_right(v); };
     constexpr bool EDGE = MODE == kEdge;                // lane masks
     constexpr bool ROWS = EDGE || MODE == kRowEdge;     // row tests, ghost rows
     if (ROWS && fixrows) {
@@ -203,14 +215,14 @@ __device__ __forceinline__ d2 stage(const Lane& c, int t, bool fixrows, d2 In, i
     d2 Mr = A;
     if (!ROWS || (rr >= c.lo_j && rr <= c.hi_j)) {
         if (Q == 0) {
-            const double Lf = from_left(A.y);
+            const double Lf = fl(A.y);
             const double cc = A.x;
             const double r = Ra.x - ((m2c(A.y, cc) + Lf) * idx2 +
                                      (m2c(In.x, cc) + M1.x) * idy2);
             if (!EDGE || c.up_a) Mr.x = cc - coef * r;
             tally(r, rr, sh, c.own_a);
         } else {
-            const double Rf = from_right(A.x);
+            const double Rf = fr(A.x);
             const double cc = A.y;
             const double r = Ra.y - ((m2c(Rf, cc) + A.x) * idx2 +
                                      (m2c(In.y, cc) + M1.y) * idy2);
@@ -223,14 +235,14 @@ __device__ __forceinline__ d2 stage(const Lane& c, int t, bool fixrows, d2 In, i
     d2 F = M1;
     if (!ROWS || (rb >= c.lo_j && rb <= c.hi_j)) {
         if (Q == 0) {
-            const double Ln = from_left(M1.y);
+            const double Ln = fl(M1.y);
             const double cc = M1.x;
             const double r = Rb.x - ((m2c(M1.y, cc) + Ln) * idx2 +
                                      (m2c(Mr.x, cc) + M2.x) * idy2);
             if (!EDGE || c.up_a) F.x = cc - coef * r;
             tally(r, rb, sh - 1, c.own_a);
         } else {
-            const double Rn = from_right(M1.x);
+            const double Rn = fr(M1.x);
             const double cc = M1.y;
             const double r = Rb.y - ((m2c(Rn, cc) + M1.x) * idx2 +
                                      (m2c(Mr.y, cc) + M2.y) * idy2);
@@ -270,7 +282,7 @@ struct Io {
 
 // one paired-march step: stream in old row r0, push it through the T stages,
 // store the row the last stage finished (r0 - 2T) if this block owns it
-template <int T, int D, int Q, int MODE>
+template <int T, int D, int Q, int MODE, bool BP = false>
 __device__ __forceinline__ void tb_step(March<T, D>& m, const Lane& c, const Io& io, int r0) {
     const long long pitch = io.pitch;
     const d2 nP = ldv(io.sp + (long long)(r0 + D) * pitch);
@@ -283,8 +295,8 @@ __device__ __forceinline__ void tb_step(March<T, D>& m, const Lane& c, const Io&
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         const d2 prevM2 = m.M2[t];
-        v = stage<T, Q, MODE>(c, t, t > 0, v, r0 - 2 * t, m.A[t], m.M1[t], m.M2[t], m.R[2 * t],
-                              m.R[2 * t + 1], m.acc[t]);
+        v = stage<T, Q, MODE, BP>(c, t, t > 0, v, r0 - 2 * t, m.A[t], m.M1[t], m.M2[t],
+                                  m.R[2 * t], m.R[2 * t + 1], m.acc[t]);
         if (t == T - 1 && MODE != kPre) {
             const int jw = r0 - 2 * T;  // row finished by the last stage
             if (MODE == kRowEdge) {
@@ -331,14 +343,14 @@ __device__ __forceinline__ void tb_step(March<T, D>& m, const Lane& c, const Io&
 }
 
 // paired march over steps r0 = rs .. rend (the colour Q0 of row rs a constant)
-template <int T, int D, int Q0, int MODE>
+template <int T, int D, int Q0, int MODE, bool BP = false>
 __device__ __forceinline__ void march_pairs(March<T, D>& m, const Lane& c, const Io& io, int r0,
                                             int rend) {
     for (; r0 + 1 <= rend; r0 += 2) {
-        tb_step<T, D, Q0, MODE>(m, c, io, r0);
-        tb_step<T, D, 1 - Q0, MODE>(m, c, io, r0 + 1);
+        tb_step<T, D, Q0, MODE, BP>(m, c, io, r0);
+        tb_step<T, D, 1 - Q0, MODE, BP>(m, c, io, r0 + 1);
     }
-    if (r0 <= rend) tb_step<T, D, Q0, MODE>(m, c, io, r0);
+    if (r0 <= rend) tb_step<T, D, Q0, MODE, BP>(m, c, io, r0);
 }
 
 // Steady march: buffer descriptors over the wave's strip (wave-uniform base,
@@ -357,7 +369,7 @@ __device__ __forceinline__ d2 bload(__amdgpu_buffer_rsrc_t rs, unsigned voff, un
 // one step of the steady march: stream row r0 = rs + n, tally and store.  PH
 // = n mod S (a constant): rhs row rs - 1 + j lives in ring slot j mod S, and
 // stage t reads rows j = n - 2t (red) and n - 2t - 1 (black)
-template <int T, int D, int Q, int PH>
+template <int T, int D, int Q, int PH, bool BP>
 __device__ __forceinline__ void steady_step(March<T, D>& m, d2* R, const Lane& c, const Sio& io,
                                             int r0, unsigned off_n) {
     constexpr int S = ring_slots<T, D>();
@@ -370,7 +382,7 @@ __device__ __forceinline__ void steady_step(March<T, D>& m, d2* R, const Lane& c
     d2 v = m.Pq[0];
 #pragma unroll
     for (int t = 0; t < T; ++t) {
-        v = stage<T, Q, kSteady>(c, t, t > 0, v, r0 - 2 * t, m.A[t], m.M1[t], m.M2[t],
+        v = stage<T, Q, kSteady, BP>(c, t, t > 0, v, r0 - 2 * t, m.A[t], m.M1[t], m.M2[t],
                                  R[(PH - 2 * t + 4 * S) % S], R[(PH - 2 * t - 1 + 4 * S) % S],
                                  m.acc[t]);
     }
@@ -396,23 +408,23 @@ __device__ __forceinline__ void steady_step(March<T, D>& m, d2* R, const Lane& c
 }
 
 // S steps of the steady march, the first at slot phase P0 (colour Q0)
-template <int T, int D, int Q0, int P0, int... NN>
+template <int T, int D, int Q0, int P0, bool BP, int... NN>
 __device__ __forceinline__ void steady_chunk(March<T, D>& m, d2* R, const Lane& c, const Sio& io,
                                              int r0, unsigned off_n,
                                              std::integer_sequence<int, NN...>) {
     constexpr int S = ring_slots<T, D>();
-    (steady_step<T, D, Q0 ^ (NN & 1), (P0 + NN) % S>(m, R, c, io, r0 + NN,
+    (steady_step<T, D, Q0 ^ (NN & 1), (P0 + NN) % S, BP>(m, R, c, io, r0 + NN,
                                                        off_n + (unsigned)NN * io.row_bytes),
      ...);
 }
 
 // interior block of H = k * S rows: 4T paired warm-up steps, then k chunks of
 // S statically unrolled steps
-template <int T, int D, int Q0>
+template <int T, int D, int Q0, bool BP>
 __device__ __forceinline__ void march_interior(March<T, D>& m, const Lane& c, const Io& io,
                                                const Sio& sio, int rs, int nchunks) {
     constexpr int S = ring_slots<T, D>();
-    march_pairs<T, D, Q0, kPre>(m, c, io, rs, rs + 4 * T - 1);  // 4T is even
+    march_pairs<T, D, Q0, kPre, BP>(m, c, io, rs, rs + 4 * T - 1);  // 4T is even
     // ring in static slots: rhs row rs - 1 + j in slot j mod S; at step n = 4T
     // the paired ring holds j = 4T - 1 - k (k < 2T), the rows in flight j = 4T + k
     d2 R[S];
@@ -427,7 +439,8 @@ __device__ __forceinline__ void march_interior(March<T, D>& m, const Lane& c, co
     int r0 = rs + 4 * T;
     unsigned off = 4u * T * sio.row_bytes;
     for (int k = 0; k < nchunks; ++k) {
-        steady_chunk<T, D, Q0, P0>(m, R, c, sio, r0, off, std::make_integer_sequence<int, S>{});
+        steady_chunk<T, D, Q0, P0, BP>(m, R, c, sio, r0, off,
+                                       std::make_integer_sequence<int, S>{});
         r0 += S;
         off += (unsigned)S * sio.row_bytes;
     }
@@ -435,29 +448,22 @@ __device__ __forceinline__ void march_interior(March<T, D>& m, const Lane& c, co
 
 }  // namespace
 
-// occupancy target: 2 waves per SIMD (the register file of one wave is 256
-// VGPRs; below that the compiler would rather use AGPRs and run one wave)
-template <int T, int WAVES, int D>
-__global__ __launch_bounds__(kLanes* WAVES, 2) void rb_tb_kernel(
-    SweepParams prm, const double* __restrict__ src, double* __restrict__ dst,
-    const double* __restrict__ rhs, double* __restrict__ partials,
-    const DevState* __restrict__ st, int force) {
+// one block (bx, by) of a pass: logical block L
+template <int T, int WAVES, int D, bool BP>
+__device__ __forceinline__ void tb_block(const SweepParams& prm, const double* __restrict__ src,
+                                         double* __restrict__ dst, const double* __restrict__ rhs,
+                                         double* __restrict__ partials, const int L,
+                                         double (*wsum)[WAVES]) {
     constexpr int OW = kStripCells - 4 * T;
     constexpr int S = ring_slots<T, D>();
-    __shared__ double wsum[T][WAVES];
-    if (!force && st->done) return;
-
-    int L = blockIdx.x;
-    if (prm.xcd_remap) {
-        const int nwg = prm.nblocks, qq = nwg / 8, rr = nwg % 8, x = L % 8;
-        L = (x < rr ? x * (qq + 1) : rr * (qq + 1) + (x - rr) * qq) + L / 8;
-    }
     const int bx = L % prm.nbx, by = L / prm.nbx;
     const int ni = prm.ni, nj = prm.nj;
-    // block rows of H = rows_per_block rows; the last one takes the rest
+    // block rows: nby_big of H = rows_per_block rows, then h_small-row ones
+    // (short blocks, which the work order takes last), the last takes the rest
     const int H = prm.rows_per_block;
-    const int j0 = 1 + by * H;
-    const int j1 = by == prm.nby - 1 ? nj + 1 : j0 + H;
+    const int j0 = by < prm.nby_big ? 1 + by * H
+                                    : 1 + prm.nby_big * H + (by - prm.nby_big) * prm.h_small;
+    const int j1 = by == prm.nby - 1 ? nj + 1 : j0 + (by < prm.nby_big ? H : prm.h_small);
     if (prm.part != 0) {  // overlapped decomposed pass: blocks clear of the halo first
         const int lo = 1 + bx * WAVES * OW - 2 * T;
         const int hi = 1 + (bx * WAVES + WAVES - 1) * OW - 2 * T + kStripCells - 1;
@@ -500,6 +506,8 @@ __global__ __launch_bounds__(kLanes* WAVES, 2) void rb_tb_kernel(
     c.idx2 = prm.idx2;
     c.idy2 = prm.idy2;
     c.coef = prm.coef;
+    c.bl = ((lane + 63) & 63) * 4;
+    c.br = ((lane + 1) & 63) * 4;
 
     March<T, D> m;
 #pragma unroll
@@ -568,8 +576,8 @@ __global__ __launch_bounds__(kLanes* WAVES, 2) void rb_tb_kernel(
                 sio.st_lane = c.own_a ? (unsigned)lane * 16u : 0x40000000u;
                 sio.row_bytes = (unsigned)(pitch * 8);
                 const int nchunks = (j1 - j0) / S;
-                if (q1) march_interior<T, D, 1>(m, c, io, sio, rs, nchunks);
-                else    march_interior<T, D, 0>(m, c, io, sio, rs, nchunks);
+                if (q1) march_interior<T, D, 1, BP>(m, c, io, sio, rs, nchunks);
+                else    march_interior<T, D, 0, BP>(m, c, io, sio, rs, nchunks);
             } else {
                 if (q1) march_pairs<T, D, 1, kRowEdge>(m, c, io, rs, rend);
                 else    march_pairs<T, D, 0, kRowEdge>(m, c, io, rs, rend);
@@ -595,6 +603,75 @@ __global__ __launch_bounds__(kLanes* WAVES, 2) void rb_tb_kernel(
         for (int w = 0; w < WAVES; ++w) s += wsum[t][w];
         partials[(long long)t * prm.nblocks + L] = s;
     }
+    __syncthreads();  // wsum is reused by the workgroup's next block
+}
+
+// occupancy target: 2 waves per SIMD (the register file of one wave is 256
+// VGPRs; below that the compiler would rather use AGPRs and run one wave).
+//
+// Two ways to hand out blocks:
+//  - one workgroup per block (queue == nullptr): block L of workgroup
+//    blockIdx.x, dealt to XCDs in contiguous runs (xcd_remap);
+//  - persistent (queue != nullptr): as many workgroups as fit on the GPU at
+//    once; workgroup w (on XCD w % 8, the hardware's round-robin) takes
+//    tickets from its XCD's queue -- a contiguous run of blocks, as above --
+//    and, once that is empty, from the other XCDs' queues.  The makespan then
+//    ends within one block of the last one started, instead of a last,
+//    partly filled round of workgroups (one rank's block at 8 GPUs runs
+//    3.5 rounds of 512 workgroups).  queue[0..7] are zeroed before the launch.
+template <int T, int WAVES, int D, bool BP>
+__global__ __launch_bounds__(kLanes* WAVES, 2) void rb_tb_kernel(
+    SweepParams prm, const double* __restrict__ src, double* __restrict__ dst,
+    const double* __restrict__ rhs, double* __restrict__ partials,
+    const DevState* __restrict__ st, int force, int* __restrict__ queue) {
+    __shared__ double wsum[T][WAVES];
+    __shared__ int ticket;
+    if (!force && st->done) return;
+    const int nwg = prm.nblocks, qq = nwg / 8, rr = nwg % 8;
+    auto run_start = [&](int x) { return x < rr ? x * (qq + 1) : rr * (qq + 1) + (x - rr) * qq; };
+    // Work order (persistent launches): the blocks on the grid's border first
+    // (the slower lane-masked / row-tested marches: strips at a physical
+    // left/right side, block rows at a physical bottom/top side, the last
+    // block row of non-uniform height), then the rest in row-major order (the
+    // short block rows last); the XCD queues hold contiguous runs of that
+    // order.  Slow blocks start early and the pass ends on short ones.
+    const int nbx = prm.nbx, nby = prm.nby;
+    auto order = [&](int k) -> int {  // k-th block of the work order -> L
+        if (nby <= 2 || nbx <= 2) return k;
+        if (k < nbx) return k;                                 // bottom row
+        k -= nbx;
+        if (k < nbx) return (nby - 1) * nbx + k;               // top row
+        k -= nbx;
+        if (k < nby - 2) return (1 + k) * nbx;                 // left column
+        k -= nby - 2;
+        if (k < nby - 2) return (1 + k) * nbx + nbx - 1;       // right column
+        k -= nby - 2;
+        const int w = nbx - 2;                                 // the rest
+        return (1 + k / w) * nbx + 1 + k % w;
+    };
+    const int home = blockIdx.x % 8;
+    bool first = true;
+    for (int probe = 0; probe < 8;) {
+        int L;
+        if (!queue) {  // one workgroup per block: one trip
+            if (!first) break;
+            L = blockIdx.x;
+            if (prm.xcd_remap) L = run_start(L % 8) + L / 8;
+        } else {
+            const int x = (home + probe) & 7;
+            if (threadIdx.x == 0) ticket = atomicAdd(&queue[x], 1);
+            __syncthreads();
+            const int b = ticket;
+            __syncthreads();
+            if (b >= (x < rr ? qq + 1 : qq)) {
+                ++probe;
+                continue;
+            }
+            L = order(run_start(x) + b);
+        }
+        first = false;
+        tb_block<T, WAVES, D, BP>(prm, src, dst, rhs, partials, L, wsum);
+    }
 }
 
 int tb_out_width(int T) { return kStripCells - 4 * T; }
@@ -612,11 +689,34 @@ int tb_nbx(int ni, int T, int waves) {
     return (strips + waves - 1) / waves;
 }
 
+// workgroups of a persistent launch: as many as are resident at once
+template <int T, int W, int D, bool B>
+static int persistent_grid() {
+    static int n = 0;
+    if (n == 0) {
+        int per_cu = 0, dev = 0, cus = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rb_tb_kernel<T, W, D, B>,
+                                                           kLanes * W, 0);
+        n = std::max(8, per_cu * cus);
+    }
+    return n;
+}
+
 void launch_tb(hipStream_t s, int T, const SweepParams& prm, const double* src, double* dst,
-               const double* rhs, double* partials, const DevState* st, int force) {
-#define TB(TT, W, DD)                                                                \
-    hipLaunchKernelGGL((rb_tb_kernel<TT, W, DD>), dim3(prm.nblocks), dim3(kLanes * W), 0, s, \
-                       prm, src, dst, rhs, partials, st, force)
+               const double* rhs, double* partials, const DevState* st, int force, int* queue) {
+#define TBB(TT, W, DD, BB)                                                                    \
+    do {                                                                                     \
+        int grid_ = prm.nblocks;                                                             \
+        if (queue) {                                                                         \
+            (void)hipMemsetAsync(queue, 0, 8 * sizeof(int), s);                              \
+            grid_ = std::min(grid_, persistent_grid<TT, W, DD, BB>());                      \
+        }                                                                                    \
+        hipLaunchKernelGGL((rb_tb_kernel<TT, W, DD, BB>), dim3(grid_), dim3(kLanes * W), 0, s, \
+                           prm, src, dst, rhs, partials, st, force, queue);                  \
+    } while (0)
+#define TB(TT, W, DD) TBB(TT, W, DD, false)
 #define TB_T(TT)                       \
     switch (prm.variant) {             \
     case 1: TB(TT, 8, 2); break;       \
@@ -626,12 +726,9 @@ void launch_tb(hipStream_t s, int T, const SweepParams& prm, const double* src, 
     default: TB(TT, 4, 2); break;      \
     }
     // must match kTbVariants (misor_internal.h)
-#ifdef MISOR_TB_QUICK  // experiment builds only: T = 7..9, default variant
-    switch (T) {
-    case 7: TB(7, 4, 2); break;
-    case 8: TB(8, 4, 2); break;
-    default: TB(9, 4, 2); break;
-    }
+#ifdef MISOR_TB_QUICK  // experiment builds only: T = 7, default variant
+    TB(7, 4, 2);
+    (void)T;
 #else
     switch (T) {
     case 1: TB_T(1); break;  // the last pass of a capped solve, or a recompute
@@ -650,6 +747,41 @@ void launch_tb(hipStream_t s, int T, const SweepParams& prm, const double* src, 
 #endif
 #undef TB_T
 #undef TB
+#undef TBB
+}
+
+int tb_resident(int T, int variant) {
+#define RES(TT, W, DD, BB) return persistent_grid<TT, W, DD, BB>()
+#define RES_T(TT)                                      \
+    switch (variant) {                                 \
+    case 1: RES(TT, 8, 2, false);                      \
+    case 2: RES(TT, 2, 2, false);                      \
+    case 3: RES(TT, 1, 2, false);                      \
+    case 4: RES(TT, 4, 3, false);                      \
+    default: RES(TT, 4, 2, false);                     \
+    }
+#ifdef MISOR_TB_QUICK
+    (void)T;
+    (void)variant;
+    RES(7, 4, 2, false);
+#else
+    switch (T) {
+    case 1: RES_T(1);
+    case 2: RES_T(2);
+    case 3: RES_T(3);
+    case 4: RES_T(4);
+    case 5: RES_T(5);
+    case 6: RES_T(6);
+    case 7: RES_T(7);
+    case 8: RES_T(8);
+    case 9: RES_T(9);
+    case 10: RES_T(10);
+    case 11: RES_T(11);
+    default: RES_T(12);
+    }
+#endif
+#undef RES_T
+#undef RES
 }
 
 }  // namespace misor

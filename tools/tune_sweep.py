@@ -36,7 +36,10 @@ def main():
     ap.add_argument("--remap", default="0,1")
     ap.add_argument("--tb", action="store_true")
     ap.add_argument("--tsteps", default="2,3,4")
+    ap.add_argument("--lib", default="", help="load this libmisor.so instead (A/B builds)")
     args = ap.parse_args()
+    if args.lib:
+        M.LIBPATH = os.path.abspath(args.lib)
     if args.tb:
         return main_tb(args)
     n = args.size

@@ -550,22 +550,30 @@ static int effective_tsteps(const misor_grid* g) {
 }
 
 // Block height H of a pass of T iterations.  A block streams H + 4T rows for
-// its H, so tall blocks waste less; short ones give a launch more workgroups,
-// and the workgroups resident together stream the same rows (page and L2
-// locality: round-1 measurements, profiles/r01_shape_sweep*.txt, put the
-// optimum near 192 rows from 32768^2 down to one rank's 8192 x 16384).  H is a
-// multiple of the static ring's S slots (sor_tb.hip: interior blocks march in
-// chunks of S steps); smaller grids halve it until the launch has ~1024
-// workgroups (4 per CU) to spread.  The last block row takes the rest
+// its H, so tall blocks waste less; short ones give a launch more workgroups.
+// With one workgroup per block, round-1 measurements put the optimum near 192
+// rows (profiles/r01_shape_sweep*.txt); with the persistent work-queue passes
+// (the 64 workgroups of an XCD stream neighbouring blocks of one block row,
+// and the pass ends on a band of short blocks) taller blocks pay off: 384 rows
+// 0.796 vs 0.821 ms per iteration at 32768^2, 576-768 within noise of 384,
+// 1536 slower (profiles/r02_tb_rows_persistent.txt).  H is a multiple of the
+// static ring's S slots (sor_tb.hip: interior blocks march in chunks of S
+// steps); smaller grids halve it until the launch has ~1024 workgroups.  The last block row takes the rest
 // (at most H rows) and marches in pairs.
 static int pick_tb_rows(int ni, int nj, int T, int variant) {
     const long long nbx = tb_nbx(ni, T, tb_waves(variant));
     const int S = tb_ring_slots(T, variant);
-    int h = kDefaultTbRows;
-    while (h / 2 >= kMinTbRows && nbx * ((nj + h - 1) / h) < 1024) h /= 2;
-    int k = (h + S / 2) / S;
-    if (k < 1) k = 1;
-    return k * S;
+    auto on_ring = [&](int h) { return S * std::max(1, (h + S / 2) / S); };
+    const char* e = getenv("MISOR_TB_TARGET_ROWS");  // tuning experiments (tools/)
+    if (e && atoi(e) > 0) return on_ring(atoi(e));
+    // the tallest of the ladder that still gives the launch ~6 blocks per
+    // resident workgroup (3000 blocks)
+    int h = kTbRowLadder[0];
+    for (int k = 0; k < kTbRowLadderLen; ++k) {
+        h = kTbRowLadder[k];
+        if (nbx * ((nj + on_ring(h) - 1) / on_ring(h)) >= 3000) break;
+    }
+    return on_ring(h);
 }
 
 // geometry of the temporally blocked pass with T iterations into `tp`: the
@@ -812,7 +820,9 @@ int misor_create(misor_grid** out, const misor_desc* d) {
         const char* e = getenv("MISOR_FINISH2");
         g->finish2 = !(e && e[0] == '0');
     }
-    if (configure_tb(g, kDefaultTsteps, kDefaultTbVariant, 0) != MISOR_OK)
+    const int T0 = (long long)g->loc.ni * g->loc.nj >= kTsteps8Cells ? kDefaultTsteps
+                                                                      : kSmallBlockTsteps;
+    if (configure_tb(g, T0, kDefaultTbVariant, 0) != MISOR_OK)
         CREATE_FAIL(MISOR_ENOMEM, "%s", g_err.c_str());
     if (hipStreamSynchronize(g->stream) != hipSuccess)
         CREATE_FAIL(MISOR_EHIP, "hipStreamSynchronize failed");

@@ -66,10 +66,17 @@ struct TbVariant {
 };
 constexpr TbVariant kTbVariants[] = {{4, 2}, {8, 2}, {2, 2}, {1, 2}, {4, 3}};
 constexpr int kNumTbVariants = 5;
-constexpr int kDefaultTsteps = 7;      // iterations per pass
+// iterations per pass: 8 on large local blocks, 7 below kTsteps8Cells cells
+// (32768^2 0.744 vs 0.785 ms/iteration, profiles/r02_tune_t789.txt; one rank's
+// 8192 x 16384 block at 8 GPUs 0.118-0.122 at T = 7 vs 0.125 at T = 8,
+// profiles/r02_small_rows.txt, r02_tb_rows_t8.txt)
+constexpr int kDefaultTsteps = 8;
+constexpr int kSmallBlockTsteps = 7;
+constexpr long long kTsteps8Cells = 1LL << 28;
 constexpr int kDefaultTbVariant = 0;   // 4 strips, 2 rows in flight
-constexpr int kDefaultTbRows = 192;    // target rows per block (misor_api.hip pick_tb_nby) ...
-constexpr int kMinTbRows = 48;         // ... halved down to this while a launch has < 1024 WGs
+// block heights tried, tallest first (misor_api.hip pick_tb_rows)
+constexpr int kTbRowLadder[] = {576, 384, 288, 192};
+constexpr int kTbRowLadderLen = 4;
 constexpr int kTbSmallRows = 32;       // short block rows the work order takes last ...
 constexpr int kTbSmallRounds = 2;      // ... about this many resident rounds of them
 int tb_waves(int variant);

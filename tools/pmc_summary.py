@@ -38,9 +38,13 @@ def main():
     ap.add_argument("--size", type=int, default=32768)
     ap.add_argument("--nranks", type=int, default=1)
     ap.add_argument("--iters", type=int, required=True)
-    ap.add_argument("--kernel", default="rb_tb_kernel")
+    ap.add_argument("--kernel", default=None,
+                    help="kernel name substring (default: rb_tb_kernel<ITERS, -- only the "
+                         "full passes, not the warm-up or remainder instantiations)")
     ap.add_argument("--rows", type=int, default=0)
     a = ap.parse_args()
+    if a.kernel is None:
+        a.kernel = "rb_tb_kernel<%d," % a.iters
     f = rows(a.dir, "fetch", a.kernel)
     w = rows(a.dir, "write", a.kernel)
     s = rows(a.dir, "sq", a.kernel)

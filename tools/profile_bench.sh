@@ -7,7 +7,7 @@ tag=$1; shift
 out=gpurun_out/prof_$tag
 mkdir -p $out
 timeout -k 10 300 python bench.py "$@" > $out/bench.json 2> $out/bench.err
-B="python bench.py --steps 28 --warmup 7 --no-cpu-baseline $*"
+B="python bench.py --steps 32 --warmup 8 --no-cpu-baseline $*"
 # the kernel trace runs the bench's own default steps, so its average launch
 # duration is comparable with roofline.kernel_ms of bench.json
 timeout -s KILL 180 rocprofv3 --kernel-trace --stats -d $out -o trace --output-format csv -- python bench.py --no-cpu-baseline "$@" > $out/trace.log 2>&1

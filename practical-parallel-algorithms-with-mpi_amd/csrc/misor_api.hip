@@ -113,6 +113,10 @@ struct misor_grid {
     int np = 2;   // pressure buffers: 2 (ping-pong), 3 on decomposed runs
     int cur = 0;  // which one (0 .. np-1, see pbuf) holds the current pressure
     int rhs_halo = 0;  // depth of rhs's exchanged halo still valid (0: rhs changed)
+    // u, v versions: every entry point that writes u or v bumps uv_ver;
+    // adaptUV leaves max |u|, |v| partials in max_partials (max_ver = uv_ver)
+    unsigned uv_ver = 1, max_ver = 0;
+    double* max_partials = nullptr;
 
     // sweep
     SweepParams sp{};
@@ -247,6 +251,7 @@ void misor_destroy(misor_grid* g) {
     (void)hipFree(g->st);
     (void)hipHostFree(g->st_host);
     (void)hipFree(g->red_partials);
+    (void)hipFree(g->max_partials);
     (void)hipFree(g->red_out);
     (void)hipHostFree(g->red_host);
     (void)hipFree(g->sendbuf);
@@ -561,7 +566,7 @@ static int effective_tsteps(const misor_grid* g) {
 // steps); smaller grids halve it until the launch has ~1024 workgroups.  The last block row takes the rest
 // (at most H rows) and marches in pairs.
 static int pick_tb_rows(int ni, int nj, int T, int variant) {
-    const long long nbx = tb_nbx(ni, T, tb_waves(variant));
+    const long long nbx = tb_nbx(ni, T, variant);
     const int S = tb_ring_slots(T, variant);
     auto on_ring = [&](int h) { return S * std::max(1, (h + S / 2) / S); };
     const char* e = getenv("MISOR_TB_TARGET_ROWS");  // tuning experiments (tools/)
@@ -584,7 +589,7 @@ static void tb_geometry(const misor_grid* g, int T, SweepParams& tp) {
     int h = req > 0 ? req : pick_tb_rows(g->loc.ni, nj, T, tp.variant);
     if (h > nj) h = nj;
     tp.rows_per_block = h;
-    tp.nbx = tb_nbx(g->loc.ni, T, tb_waves(tp.variant));
+    tp.nbx = tb_nbx(g->loc.ni, T, tp.variant);
     // block rows: H tall, then (automatic geometry) about one resident round of
     // short ones -- the work order takes them last, so the pass ends on blocks
     // about a quarter as long (the makespan of a pass runs ~half a block past
@@ -615,6 +620,9 @@ static void tb_geometry(const misor_grid* g, int T, SweepParams& tp) {
 static int configure_tb(misor_grid* g, int T, int variant, int rows) {
     if (T < 1 || T > kMaxT) return fail(MISOR_EINVAL, "iterations per pass must be 1..%d", kMaxT);
     if (variant < 0 || variant >= kNumTbVariants) return fail(MISOR_EINVAL, "bad tb variant");
+    if (T > tb_max_t(variant))
+        return fail(MISOR_EINVAL, "TB variant %d runs at most %d iterations per pass", variant,
+                    tb_max_t(variant));
     g->tsteps = T;
     g->tb_rows_req = rows;
     SweepParams& tp = g->tp;
@@ -707,6 +715,13 @@ int misor_create(misor_grid** out, const misor_desc* d) {
     const double dx2 = d->dx * d->dx, dy2 = d->dy * d->dy;
     sp.idx2 = 1.0 / dx2;
     sp.idy2 = 1.0 / dy2;
+    {
+        // power-of-two spacing (sor_tb.h resid<true>): 1/dx^2 == 1/dy^2 == 2^m, m >= 0
+        int e = 0;
+        const double mant = frexp(sp.idx2, &e);
+        const char* no = getenv("MISOR_NO_POW2");  // A/B switch (tools/ab_env.py)
+        sp.pow2 = sp.idx2 == sp.idy2 && mant == 0.5 && e >= 1 && !(no && no[0] == '1');
+    }
     if (d->variant == MISOR_SOLVE_RBA) {
         const double factor = 0.5 * (dx2 * dy2) / (dx2 + dy2);  // solver.c:250
         sp.coef = d->omega * factor;                            // (omega*factor)*r, :273
@@ -740,6 +755,7 @@ int misor_create(misor_grid** out, const misor_desc* d) {
         CREATE_FAIL(MISOR_ENOMEM, "state allocation failed");
     const int rb = reduce_blocks(L.ni, L.nj);
     if (hipMalloc(&g->red_partials, sizeof(double) * 2 * rb) != hipSuccess ||
+        hipMalloc(&g->max_partials, sizeof(double) * 2 * rb) != hipSuccess ||
         hipMalloc(&g->red_out, sizeof(double) * 4) != hipSuccess ||
         hipHostMalloc(&g->red_host, sizeof(double) * 4, hipHostMallocDefault) != hipSuccess)
         CREATE_FAIL(MISOR_ENOMEM, "reduction allocation failed");
@@ -884,6 +900,7 @@ int misor_upload(misor_grid* g, int field, const double* host) {
     const size_t w = (size_t)(g->loc.ni + 2) * sizeof(double);
     const size_t h = (size_t)(g->loc.nj + 2);
     if (field == MISOR_RHS) g->rhs_halo = 0;
+    if (field == MISOR_U || field == MISOR_V) ++g->uv_ver;
     if (field == MISOR_P) {  // every pressure buffer: corners and ghosts must agree
         g->cur = 0;
         for (int b = 0; b < g->np; ++b)
@@ -1051,6 +1068,7 @@ int misor_fill(misor_grid* g, int field, double value) {
     HIPCHK(hipSetDevice(g->device));
     // whole padded array: ghosts included, pads too (pads never feed results)
     if (field == MISOR_RHS) g->rhs_halo = 0;
+    if (field == MISOR_U || field == MISOR_V) ++g->uv_ver;
     if (field == MISOR_P) {
         g->cur = 0;
         for (int b = 0; b < g->np; ++b) launch_fill(g->stream, pbuf(g, b), g->elems, value);
@@ -1459,6 +1477,7 @@ int misor_ns_setup(misor_grid* g, const misor_ns_desc* ns) {
     L.joff = g->loc.joff;
     L.imax_g = g->desc.imax;
     L.jmax_g = g->desc.jmax;
+    ++g->uv_ver;
     g->ns_ready = true;
     return MISOR_OK;
 }
@@ -1472,8 +1491,13 @@ int misor_ns_setup(misor_grid* g, const misor_ns_desc* ns) {
 
 int misor_max_uv(misor_grid* g, double* umax, double* vmax) {
     NEED_NS(g);
-    launch_absmax2(g->nl, g->fld[kU], g->fld[kV], g->red_partials);
-    launch_finish_reduce(g->stream, g->red_partials, reduce_blocks(g->loc.ni, g->loc.nj),
+    // the partials adaptUV computed, when no u, v write came after it
+    const double* part = g->max_partials;
+    if (g->max_ver != g->uv_ver) {
+        launch_absmax2(g->nl, g->fld[kU], g->fld[kV], g->red_partials);
+        part = g->red_partials;
+    }
+    launch_finish_reduce(g->stream, part, reduce_blocks(g->loc.ni, g->loc.nj),
                          kReduceMax, 2, g->red_out);
     HIPCHK(hipGetLastError());
     if (g->dist)
@@ -1514,6 +1538,7 @@ int misor_set_dt(misor_grid* g, double dt) {
 
 int misor_set_boundary_conditions(misor_grid* g) {
     NEED_NS(g);
+    ++g->uv_ver;
     launch_set_bc(g->nl, g->fld[kU], g->fld[kV]);
     HIPCHK(hipGetLastError());
     return MISOR_OK;
@@ -1521,6 +1546,7 @@ int misor_set_boundary_conditions(misor_grid* g) {
 
 int misor_set_special_boundary_condition(misor_grid* g) {
     NEED_NS(g);
+    ++g->uv_ver;
     launch_special_bc(g->nl, g->fld[kU]);
     HIPCHK(hipGetLastError());
     return MISOR_OK;
@@ -1595,7 +1621,9 @@ int misor_normalize_pressure(misor_grid* g) {
 
 int misor_adapt_uv(misor_grid* g) {
     NEED_NS(g);
-    launch_adapt_uv(g->nl, g->fld[kF], g->fld[kG], pbuf(g, g->cur), g->fld[kU], g->fld[kV]);
+    launch_adapt_absmax(g->nl, g->fld[kF], g->fld[kG], pbuf(g, g->cur), g->fld[kU], g->fld[kV],
+                        g->max_partials);
+    g->max_ver = ++g->uv_ver;
     HIPCHK(hipGetLastError());
     return MISOR_OK;
 }

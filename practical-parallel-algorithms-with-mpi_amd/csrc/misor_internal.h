@@ -61,11 +61,17 @@ int sweep_waves(int variant);
 // temporally blocked sweep (sor_tb.hip): strips per workgroup, rows in flight
 // (x-neighbour shifts through ds_bpermute instead of DPP -- the kernel's BP
 // template flag -- measured 5% slower: profiles/r02_tune_bperm.txt)
+// columns per lane: 2 (128-column strips, rhs ring in registers, 2 waves per
+// SIMD) or 4 (256-column strips, rhs ring in LDS, 1 wave per SIMD; T <= kMaxQuadT)
+// quad variants: sched = how far the compiler may interleave steps (sor_tb.h
+// qstep), max_t = the largest T whose LDS ring fits (2T + D (+1) rows of 2 KB per wave)
 struct TbVariant {
-    int waves, ahead;
+    int waves, ahead, cols, sched, max_t;
 };
-constexpr TbVariant kTbVariants[] = {{4, 2}, {8, 2}, {2, 2}, {1, 2}, {4, 3}};
-constexpr int kNumTbVariants = 5;
+constexpr TbVariant kTbVariants[] = {{4, 2, 2, 0, kMaxT}, {8, 2, 2, 0, kMaxT}, {2, 2, 2, 0, kMaxT},
+                                     {1, 2, 2, 0, kMaxT}, {4, 3, 2, 0, kMaxT}, {4, 2, 4, 0, 8}};
+constexpr int kNumTbVariants = 6;
+constexpr int kQuadTbVariant = 5;
 // iterations per pass: 8 on large local blocks, 7 below kTsteps8Cells cells
 // (32768^2 0.744 vs 0.785 ms/iteration, profiles/r02_tune_t789.txt; one rank's
 // 8192 x 16384 block at 8 GPUs 0.118-0.122 at T = 7 vs 0.125 at T = 8,
@@ -84,8 +90,10 @@ int tb_waves(int variant);
 int tb_ring_slots(int T, int variant);
 // workgroups of a persistent pass resident on the device at once
 int tb_resident(int T, int variant);
-int tb_out_width(int T);
-int tb_nbx(int ni, int T, int waves);           // block columns of a pass of T iterations
+int tb_cols(int variant);
+int tb_max_t(int variant);
+int tb_out_width(int T, int variant);           // owned columns of one wave's strip
+int tb_nbx(int ni, int T, int variant);         // block columns of a pass of T iterations
 
 // Solver state that lives on the device between launches.  Written only by
 // the finish kernel (one workgroup) and read by the next sweep launch.
@@ -119,6 +127,7 @@ struct SweepParams {
                                                  // (1..n on physical sides, all on
                                                  // neighbour sides)
     double idx2, idy2, coef;  // 1/dx^2, 1/dy^2, factor (RB) or omega*factor (RBA)
+    int pow2;                 // idx2 == idy2 == 2^m, m >= 0: the default TB kernel's P2 form
 };
 
 struct NsParams {
@@ -144,6 +153,16 @@ void launch_finish2(hipStream_t s, const double* partials, int nparts, int T, De
 // workgroups take blocks from per-XCD queues; nullptr: one workgroup per block
 void launch_tb(hipStream_t s, int T, const SweepParams& prm, const double* src, double* dst,
                const double* rhs, double* partials, const DevState* st, int force, int* queue);
+// the same for one T (sor_tb_inst.hip, one unit per T)
+#define MISOR_DECL_TB(N)                                                                      \
+    void launch_tb_t##N(hipStream_t s, const SweepParams& prm, const double* src, double* dst, \
+                        const double* rhs, double* partials, const DevState* st, int force,   \
+                        int* queue);                                                          \
+    int tb_resident_t##N(int variant);
+MISOR_DECL_TB(1) MISOR_DECL_TB(2) MISOR_DECL_TB(3) MISOR_DECL_TB(4) MISOR_DECL_TB(5)
+MISOR_DECL_TB(6) MISOR_DECL_TB(7) MISOR_DECL_TB(8) MISOR_DECL_TB(9) MISOR_DECL_TB(10)
+MISOR_DECL_TB(11) MISOR_DECL_TB(12)
+#undef MISOR_DECL_TB
 // lexicographic Gauss-Seidel SOR, whole solve in one workgroup (lex_kernels.hip)
 void launch_solve_lex(hipStream_t s, double* p, const double* rhs, int ni, int nj,
                       long long pitch, double idx2, double idy2, double factor, double cells,
@@ -202,6 +221,9 @@ void launch_adapt_uv(const NsLaunch& L, const double* f, const double* g, const 
 // reductions over ALL (ni+2)(nj+2) cells: partial per block, then a finish
 int reduce_blocks(int ni, int nj);
 void launch_absmax2(const NsLaunch& L, const double* u, const double* v, double* partials);
+// adaptUV + the partials of launch_absmax2 over the fields it leaves
+void launch_adapt_absmax(const NsLaunch& L, const double* f, const double* g, const double* p,
+                         double* u, double* v, double* partials);
 // normalizePressure's sum, exact (order- and decomposition-independent):
 // fixed-point terms at 2^(E - kSumFrac), E = exponent of the global max |p|;
 // limbs[0..2] = the local sum as three 44-bit integer limbs (doubles, summed

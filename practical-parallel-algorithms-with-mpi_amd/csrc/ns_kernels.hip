@@ -302,6 +302,68 @@ void launch_absmax2(const NsLaunch& L, const double* u, const double* v, double*
                        L.s, CLay{u, L.pitch}, CLay{v, L.pitch}, region_of(L), partials);
 }
 
+// adaptUV (:438-455) fused with the maxElement partials of the NEXT step's
+// computeTimestep (:193-234): the reference's main loop changes no u, v
+// between adaptUV and computeTimestep (main.c:43-60), so the maxima of the
+// fields adaptUV leaves are the ones computeTimestep needs.  The walk is
+// absmax2_kernel's (rows over blocks, columns over threads, over the cells
+// the reduction visits); cells inside [1, ni] x [1, nj] get adaptUV's update
+// and contribute their new value, the physical ghost cells their unchanged
+// one.  One pass over f, g, p -> u, v instead of that pass plus a 16-B/cell
+// re-read of u, v (misor_api.hip misor_adapt_uv / misor_max_uv).
+__global__ __launch_bounds__(kRedThreads) void adapt_absmax_kernel(CLay f, CLay g, CLay p, Lay u,
+                                                                   Lay v, int ni, int nj,
+                                                                   double fx, double fy, Region R,
+                                                                   double* partials) {
+    __shared__ double su[kRedThreads / 64], sv[kRedThreads / 64];
+    double mu = 2.2250738585072014e-308, mv = 2.2250738585072014e-308;  // DBL_MIN
+    for (int jj = blockIdx.x; jj < R.h; jj += gridDim.x) {
+        const int j = R.jlo + jj;
+        const bool jin = j >= 1 && j <= nj;
+        for (int ii = threadIdx.x; ii < R.w; ii += kRedThreads) {
+            const int i = R.ilo + ii;
+            double a, b;
+            if (jin && i >= 1 && i <= ni) {
+                const double pc = p(i, j);
+                a = f(i, j) - (p(i + 1, j) - pc) * fx;
+                b = g(i, j) - (p(i, j + 1) - pc) * fy;
+                u(i, j) = a;
+                v(i, j) = b;
+            } else {
+                a = u(i, j);
+                b = v(i, j);
+            }
+            a = fabs(a);
+            b = fabs(b);
+            mu = (mu > a) ? mu : a;
+            mv = (mv > b) ? mv : b;
+        }
+    }
+    mu = wmax(mu);
+    mv = wmax(mv);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) { su[w] = mu; sv[w] = mv; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < kRedThreads / 64; ++k) {
+            mu = (mu > su[k]) ? mu : su[k];
+            mv = (mv > sv[k]) ? mv : sv[k];
+        }
+        mu = (su[0] > mu) ? su[0] : mu;
+        mv = (sv[0] > mv) ? sv[0] : mv;
+        partials[2 * blockIdx.x] = mu;
+        partials[2 * blockIdx.x + 1] = mv;
+    }
+}
+
+void launch_adapt_absmax(const NsLaunch& L, const double* f, const double* g, const double* p,
+                         double* u, double* v, double* partials) {
+    hipLaunchKernelGGL(adapt_absmax_kernel, dim3(reduce_blocks(L.ni, L.nj)), dim3(kRedThreads), 0,
+                       L.s, CLay{f, L.pitch}, CLay{g, L.pitch}, CLay{p, L.pitch},
+                       Lay{u, L.pitch}, Lay{v, L.pitch}, L.ni, L.nj, L.prm.dt / L.prm.dx,
+                       L.prm.dt / L.prm.dy, region_of(L), partials);
+}
+
 // ---- normalizePressure's sum (:208-212), exact: independent of the
 // summation order, so of the block / rank decomposition.  Every cell
 // x = m * 2^(ex-53) (|m| < 2^53 an integer) becomes the fixed-point integer

@@ -1,680 +1,16 @@
-// sor_tb.hip -- temporally blocked red-black SOR for gfx950: T complete
-// solveRB iterations (assignment-4/src/solver.c:197-229, T = 2..kMaxT) per
-// pass over HBM.
-//
-// The single-iteration sweep (sor_kernels.hip) already moves the algorithmic
-// minimum of one iteration -- read p, read rhs, write p: 24 B per lattice
-// update -- and runs at ~93% of the measured HBM copy rate, so one iteration
-// per pass cannot go meaningfully faster.  The dependency cone of an
-// iteration is only two cells wide in each direction (red needs the old
-// 5-point neighbourhood, black needs the new red one), so a wave that streams
-// rows of the OLD field can push them through T iteration stages held in
-// registers and write only the field after the last stage: p and rhs are read
-// once and p written once per T iterations, 24/T B of HBM traffic per update.
-//
-// Work decomposition
-//   wave = one strip: loads 128 columns (lane l: ia = c_ld + 2l, ib = ia + 1,
-//          one 16-byte load per array per row), outputs the inner OW = 128-4T
-//          columns [c_out, c_out + OW), c_ld = c_out - 2T.  Each iteration
-//          stage loses two columns of validity per side (red reads +-1, black
-//          reads the new red +-1), so after T stages exactly lanes
-//          T .. 63-T hold correct values.  Overlapping loads between strips
-//          are L2 hits; nothing is exchanged between waves.
-//   rows = a block of H output rows [j0, j1); the wave streams OLD rows
-//          j0-2T .. j1-1+2T upward (N = H + 4T steps).  Stage t receives the
-//          output row stream of stage t-1 (stage 0: the old field) and, on
-//          receiving row rin, updates the red cells of row rin-1 and the black
-//          cells of row rin-2, emitting row rin-2 of iteration t+1.  The last
-//          stage's rows j0 .. j1-1 are stored.
-//   Every stage keeps 3 rows (A = row rin-1, M1 = rin-2 half updated, M2 =
-//   final rin-3); the rhs rows come from one register ring of the last 2T
-//   streamed rows (+ the D rows in flight), so rhs is read from HBM once.
-//
-// The static ring.  Every block of interior rows is H = a multiple of the
-// ring's S = 2T + D (+1 if odd) slots tall.  Its march starts with 4T
-// "warm-up" steps (no residual, no store; the ring shifts one register per
-// step, in pairs of steps) and then runs the remaining H steps in chunks of S
-// steps fully unrolled, with rhs row x in ring slot (x - rs + 1) mod S: every
-// ring register keeps its row for its whole life and the loads land in the
-// slot of the row that just died, so the steady march has no register moves
-// for the ring (the round-1 kernel spent 36 64-bit moves per step on it).
-// Stores go through a buffer descriptor with an out-of-range offset on lanes
-// that do not store, so a chunk is one basic block.
-//
-// Residual windows.  The residual of stage t is tallied over red rows
-// [j0 + 2T-1-2t, j1 + 2T-1-2t) and black rows [j0 + 2T-2-2t, j1 + 2T-2-2t)
-// of the block (shifted by the same amount in every block, so every cell is
-// counted exactly once per iteration; blocks on a physical bottom / top side
-// extend theirs to row 1 / nj).  In step numbers both windows are [4T, N) for
-// every stage: the steady chunks tally and store on every step, the warm-up
-// steps never do, and no drain steps exist.  Every row in a window lies inside
-// the stage's valid cone (red rows [rs+2t+1, rend-2t-1], black [rs+2t+2,
-// rend-2t-2]).
-//
-// Boundary handling per stage -- identical to the reference's end-of-
-// iteration ghost copy (:219-227), applied to every intermediate iteration:
-//   column 0 := column 1, column ni+1 := column ni for rows 1..nj (physical
-//   left/right sides); row 0 := row 1 and row nj+1 := row nj for columns
-//   1..ni (physical bottom/top: done on the receiving side of the row stream,
-//   when the row it copies from arrives); corners never change.  On a side
-//   that borders another rank the 2T-deep halo (exchanged before the pass)
-//   supplies the neighbour's old values and the stages simply keep updating
-//   them: identical arithmetic, so identical bits to what the owner computes.
-//   Blocks whose cone reaches a physical side, and the last block row when
-//   its height is not a multiple of S, march in pairs of steps with run-time
-//   row tests (kRowEdge) and, at a physical left/right side, lane masks
-//   (kEdge).
-//
-// Residual: stage t accumulates r^2 of the cells this wave counts; partial per
-// workgroup per stage in a fixed order; the finish kernel decides iteration by
-// iteration exactly like the single-sweep path.  If convergence (or itermax)
-// is reached at stage t < T, the host recomputes that pass with T' = t from
-// the untouched source buffer (misor_api.hip), so the returned field is the
-// one after exactly `it` iterations.
-//
-// Bit-exactness: same expression order as the reference, -ffp-contract=off.
-
-#include <algorithm>
-#include <utility>
-
+// sor_tb.hip -- host side of the temporally blocked sweep: strip geometry and
+// the launch dispatch over T (each T's kernels are instantiated in its own
+// unit, sor_tb_inst.hip compiled with MISOR_TB_T = T, so the build runs in
+// parallel).  Device code: sor_tb.h.
 #include "misor_internal.h"
 
 namespace misor {
 
-namespace {
+int tb_cols(int variant) { return kTbVariants[variant].cols; }
 
-// Lane shifts by DPP wave_shr:1 / wave_shl:1 (bound_ctrl: the lane shifted in
-// from outside the wave reads 0).  Lanes 0 and 63 are never output lanes (the
-// T outermost lanes on each side are the strip's halo), so their value is
-// irrelevant; no copy of the old value is needed.
-// lane l receives lane l-1's value
-__device__ __forceinline__ double from_left(double v) {
-    return __hiloint2double(__builtin_amdgcn_mov_dpp(__double2hiint(v), 0x138, 0xf, 0xf, true),
-                            __builtin_amdgcn_mov_dpp(__double2loint(v), 0x138, 0xf, 0xf, true));
-}
-// lane l receives lane l+1's value
-__device__ __forceinline__ double from_right(double v) {
-    return __hiloint2double(__builtin_amdgcn_mov_dpp(__double2hiint(v), 0x130, 0xf, 0xf, true),
-                            __builtin_amdgcn_mov_dpp(__double2loint(v), 0x130, 0xf, 0xf, true));
-}
+int tb_max_t(int variant) { return kTbVariants[variant].max_t; }
 
-// the same shifts through the LDS crossbar (ds_bpermute: an LDS-pipe
-// instruction, so the shift costs no VALU issue slot); addr = source lane * 4
-__device__ __forceinline__ double bperm(double v, int addr) {
-    return __hiloint2double(__builtin_amdgcn_ds_bpermute(addr, __double2hiint(v)),
-                            __builtin_amdgcn_ds_bpermute(addr, __double2loint(v)));
-}
-
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
-// a - 2c as one FMA: 2c is exact in binary floating point, so the single
-// rounding of fma(-2, c, a) equals the rounding of the reference's a - 2.0*c
-// (bit-exact, one VALU instruction instead of a multiply and a subtract)
-__device__ __forceinline__ double m2c(double a, double c) { return __builtin_fma(-2.0, c, a); }
-
-typedef double d2 __attribute__((ext_vector_type(2)));
-typedef unsigned v4u __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ d2 ldv(const double* p) { return *reinterpret_cast<const d2*>(p); }
-
-__device__ __forceinline__ void stv(double* p, d2 v) {
-    __builtin_nontemporal_store(v, reinterpret_cast<d2*>(p));
-}
-
-// ring slots of the steady march: 2T rows in use + D in flight, even (the
-// colour of a chunk's first step is then the same for every chunk)
-template <int T, int D>
-__host__ __device__ constexpr int ring_slots() {
-    return 2 * T + D + (D & 1);
-}
-
-// per-lane constants shared by all stages
-struct Lane {
-    int ia, ib;            // the lane's two columns (ia odd)
-    bool up_a, up_b;       // columns that are updated (inside [upd_lo_i, upd_hi_i])
-    bool own_a, own_b;     // columns whose residual this lane counts
-    bool fix0_b;           // ib == 0 on a physical left side: column 0 := column 1
-    bool fixr_a, fixr_b;   // ia / ib == ni+1 on a physical right side
-    bool st_a, st_b;       // columns this lane stores
-    int lo_j, hi_j;        // updated rows
-    int j0, j1;            // owned (stored) rows
-    int wlo, whi;          // residual window reaches the physical bottom / top side
-    int parity;
-    int gb, gt, nj;
-    int bl, br;            // ds_bpermute addresses of lanes l-1 and l+1
-    double idx2, idy2, coef;
-};
-
-// How a step is compiled:
-//  kEdge    general: per-lane update / residual masks, ghost-row and
-//           ghost-column copies, row tests.  Strips at a physical left /
-//           right side.
-//  kPre     interior warm-up: every streamed row is an updatable row (rows
-//           outside the valid cone hold garbage that never reaches a stored
-//           value); no residual, no store.
-//  kSteady  interior, static ring: residual and store on every step.
-//  kRowEdge columns interior (every lane's two columns updated, ownership
-//           uniform per lane), rows general: blocks whose cone reaches a
-//           physical bottom / top side, and a last block row whose height is
-//           not a multiple of the ring.  Row tests and ghost-row copies are
-//           wave-uniform; no lane masks.
-enum { kEdge = 0, kPre = 1, kSteady = 2, kRowEdge = 3 };
-
-// One iteration stage (stage index t, 0-based).  In = row rin of the previous
-// stage's output (stage 0: of the field in memory).  Returns row rin-2 of this
-// stage's output.  fixrows (stages 1..T-1; a constant after unrolling):
-// complete the previous iteration's ghost-row copy on the incoming stream.
-// Stage 0 reads the ghost rows as they are in memory -- the state after the
-// previous pass, or whatever the caller uploaded, as the reference's first
-// iteration does.  Q: colour of the rows (0: column ia is red in row rin-1).
-template <int T, int Q, int MODE, bool BP = false>
-__device__ __forceinline__ d2 stage(const Lane& c, int t, bool fixrows, d2 In, int rin, d2& A,
-                                    d2& M1, d2& M2, d2 Ra, d2 Rb, double& acc) {
-    // BP: x-neighbours through ds_bpermute instead of DPP (interior modes)
-    auto fl = [&](double v) { return BP ? bperm(v, c.bl) : from_left(v); };
-    auto fr = [&](double v) { return BP ? bperm(v, c.br) : from_right(v); };
-    constexpr bool EDGE = MODE == kEdge;                // lane masks
-    constexpr bool ROWS = EDGE || MODE == kRowEdge;     // row tests, ghost rows
-    if (ROWS && fixrows) {
-        if (c.gb && rin == 1) {  // row 0 := row 1 (A holds row 0)
-            if (!EDGE || c.up_a) A.x = In.x;
-            if (!EDGE || c.up_b) A.y = In.y;
-        }
-        if (c.gt && rin == c.nj + 1) {  // row nj+1 := row nj (A holds row nj)
-            if (!EDGE || c.up_a) In.x = A.x;
-            if (!EDGE || c.up_b) In.y = A.y;
-        }
-    }
-    const int rr = rin - 1;  // red row
-    const int rb = rin - 2;  // black row
-    const double idx2 = c.idx2, idy2 = c.idy2, coef = c.coef;
-    // residual windows of this stage (header): red rows [j0 + sh, j1 + sh),
-    // black rows one lower, extended to the physical sides
-    const int sh = 2 * T - 1 - 2 * t;
-    auto tally = [&](double r, int row, int wsh, bool own_col) {
-        if (MODE == kSteady) {
-            acc = __builtin_fma(r, r, acc);
-        } else if (MODE == kPre) {
-        } else {
-            const bool own_row = row >= (c.wlo ? 1 : c.j0 + wsh) &&
-                                 row < (c.whi ? c.nj + 1 : c.j1 + wsh);
-            if (!EDGE) {
-                const double rm = own_row ? r : 0.0;  // uniform select: no branch, NaN-safe
-                acc = __builtin_fma(rm, rm, acc);
-            } else if (own_row && own_col) {
-                acc = __builtin_fma(r, r, acc);
-            }
-        }
-    };
-
-    // red pass on row rr
-    d2 Mr = A;
-    if (!ROWS || (rr >= c.lo_j && rr <= c.hi_j)) {
-        if (Q == 0) {
-            const double Lf = fl(A.y);
-            const double cc = A.x;
-            const double r = Ra.x - ((m2c(A.y, cc) + Lf) * idx2 +
-                                     (m2c(In.x, cc) + M1.x) * idy2);
-            if (!EDGE || c.up_a) Mr.x = cc - coef * r;
-            tally(r, rr, sh, c.own_a);
-        } else {
-            const double Rf = fr(A.x);
-            const double cc = A.y;
-            const double r = Ra.y - ((m2c(Rf, cc) + A.x) * idx2 +
-                                     (m2c(In.y, cc) + M1.y) * idy2);
-            if (!EDGE || c.up_b) Mr.y = cc - coef * r;
-            tally(r, rr, sh, c.own_b);
-        }
-    }
-
-    // black pass on row rb (+ the ghost column copy of this finished row)
-    d2 F = M1;
-    if (!ROWS || (rb >= c.lo_j && rb <= c.hi_j)) {
-        if (Q == 0) {
-            const double Ln = fl(M1.y);
-            const double cc = M1.x;
-            const double r = Rb.x - ((m2c(M1.y, cc) + Ln) * idx2 +
-                                     (m2c(Mr.x, cc) + M2.x) * idy2);
-            if (!EDGE || c.up_a) F.x = cc - coef * r;
-            tally(r, rb, sh - 1, c.own_a);
-        } else {
-            const double Rn = fr(M1.x);
-            const double cc = M1.y;
-            const double r = Rb.y - ((m2c(Rn, cc) + M1.x) * idx2 +
-                                     (m2c(Mr.y, cc) + M2.y) * idy2);
-            if (!EDGE || c.up_b) F.y = cc - coef * r;
-            tally(r, rb, sh - 1, c.own_b);
-        }
-        if (EDGE) {
-            const double f1 = from_right(F.x);  // column ib+1 (lane l+1's ia)
-            const double fl = from_left(F.y);   // column ia-1 (lane l-1's ib)
-            if (c.fix0_b) F.y = f1;
-            if (c.fixr_a) F.x = fl;
-            if (c.fixr_b) F.y = F.x;
-        }
-    }
-    M2 = F;
-    M1 = Mr;
-    A = In;
-    return F;
-}
-
-// the registers of one wave's march
-template <int T, int D>
-struct March {
-    d2 A[T], M1[T], M2[T];
-    d2 R[2 * T];     // paired march: R[k] = rhs(r0 - 1 - k)
-    d2 Pq[D], Rq[D];  // rows in flight: p(r0 .. r0+D-1), rhs(r0-1 .. r0+D-2)
-    double acc[T];
-    d2 keep[2];
-};
-
-struct Io {
-    const double* sp;
-    const double* rp;
-    double* dp;
-    long long pitch;
-};
-
-// one paired-march step: stream in old row r0, push it through the T stages,
-// store the row the last stage finished (r0 - 2T) if this block owns it
-template <int T, int D, int Q, int MODE, bool BP = false>
-__device__ __forceinline__ void tb_step(March<T, D>& m, const Lane& c, const Io& io, int r0) {
-    const long long pitch = io.pitch;
-    const d2 nP = ldv(io.sp + (long long)(r0 + D) * pitch);
-    const d2 nR = ldv(io.rp + (long long)(r0 - 1 + D) * pitch);
-#pragma unroll
-    for (int k = 2 * T - 1; k > 0; --k) m.R[k] = m.R[k - 1];
-    m.R[0] = m.Rq[0];
-
-    d2 v = m.Pq[0];
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-        const d2 prevM2 = m.M2[t];
-        v = stage<T, Q, MODE, BP>(c, t, t > 0, v, r0 - 2 * t, m.A[t], m.M1[t], m.M2[t],
-                                  m.R[2 * t], m.R[2 * t + 1], m.acc[t]);
-        if (t == T - 1 && MODE != kPre) {
-            const int jw = r0 - 2 * T;  // row finished by the last stage
-            if (MODE == kRowEdge) {
-                // every column of the lane updated and stored alike (st_a == st_b);
-                // ghost rows 0 / nj+1 of the stored field are copies of rows 1 / nj
-                if (jw >= c.j0 && jw < c.j1 && c.st_a) {
-                    double* drow = io.dp + (long long)jw * pitch;
-                    stv(drow, v);
-                    if (c.gb && jw == 1) stv(drow - pitch, v);
-                    if (c.gt && jw == c.nj) stv(drow + pitch, v);
-                }
-            } else if (jw >= c.j0 && jw < c.j1) {
-                double* drow = io.dp + (long long)jw * pitch;
-                auto put = [&](double* p, d2 o) {
-                    if (c.st_a && c.st_b) {
-                        stv(p, o);
-                    } else if (c.st_a) {
-                        p[0] = o.x;
-                    } else if (c.st_b) {
-                        p[1] = o.y;
-                    }
-                };
-                put(drow, v);
-                // ghost rows of the stored field: interior columns from the
-                // finished row, corners from the (unchanged) ghost row
-                if (c.gb && jw == 1) {
-                    const d2 g0 = prevM2;  // the stage's row 0
-                    put(drow - pitch, d2{c.up_a ? v.x : g0.x, c.up_b ? v.y : g0.y});
-                }
-                if (c.gt && jw == c.nj) {
-                    const d2 gn = m.M1[t];  // the stage's row nj+1 (after its fix)
-                    put(drow + pitch, d2{c.up_a ? v.x : gn.x, c.up_b ? v.y : gn.y});
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int k = 0; k + 1 < D; ++k) {
-        m.Pq[k] = m.Pq[k + 1];
-        m.Rq[k] = m.Rq[k + 1];
-    }
-    m.Pq[D - 1] = nP;
-    m.Rq[D - 1] = nR;
-}
-
-// paired march over steps r0 = rs .. rend (the colour Q0 of row rs a constant)
-template <int T, int D, int Q0, int MODE, bool BP = false>
-__device__ __forceinline__ void march_pairs(March<T, D>& m, const Lane& c, const Io& io, int r0,
-                                            int rend) {
-    for (; r0 + 1 <= rend; r0 += 2) {
-        tb_step<T, D, Q0, MODE, BP>(m, c, io, r0);
-        tb_step<T, D, 1 - Q0, MODE, BP>(m, c, io, r0 + 1);
-    }
-    if (r0 <= rend) tb_step<T, D, Q0, MODE, BP>(m, c, io, r0);
-}
-
-// Steady march: buffer descriptors over the wave's strip (wave-uniform base,
-// lane byte offset); the byte offset of a row is a scalar
-struct Sio {
-    __amdgpu_buffer_rsrc_t p, r, d;  // p rows from rs, rhs rows from rs-1, dst rows from j0
-    unsigned lane;                   // lane * 16
-    unsigned st_lane;                // lane * 16 if the lane stores, else out of range
-    unsigned row_bytes;              // pitch * 8
-};
-
-__device__ __forceinline__ d2 bload(__amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned soff) {
-    return __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
-}
-
-// one step of the steady march: stream row r0 = rs + n, tally and store.  PH
-// = n mod S (a constant): rhs row rs - 1 + j lives in ring slot j mod S, and
-// stage t reads rows j = n - 2t (red) and n - 2t - 1 (black)
-template <int T, int D, int Q, int PH, bool BP>
-__device__ __forceinline__ void steady_step(March<T, D>& m, d2* R, const Lane& c, const Sio& io,
-                                            int r0, unsigned off_n) {
-    constexpr int S = ring_slots<T, D>();
-    // p row r0 + D (p descriptor starts at row rs), rhs row r0 - 1 + D (rhs
-    // descriptor starts at row rs - 1): both n + D rows in; the rhs row lands
-    // in the slot of the row stage T-1 finished with in the previous step
-    const unsigned ld = off_n + (unsigned)D * io.row_bytes;
-    const d2 nP = bload(io.p, io.lane, ld);
-    R[(PH + D) % S] = bload(io.r, io.lane, ld);
-    d2 v = m.Pq[0];
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-        v = stage<T, Q, kSteady, BP>(c, t, t > 0, v, r0 - 2 * t, m.A[t], m.M1[t], m.M2[t],
-                                 R[(PH - 2 * t + 4 * S) % S], R[(PH - 2 * t - 1 + 4 * S) % S],
-                                 m.acc[t]);
-    }
-    // row r0 - 2T = j0 + (n - 4T): dst descriptor starts at row j0; lanes that
-    // do not store carry an out-of-range offset (the write is dropped)
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), io.d, io.st_lane,
-                                           off_n - 4u * T * io.row_bytes, 2);
-    // The store reads its data VGPRs after it issues, and on gfx950 a later
-    // buffer_load can land in those VGPRs first: with the registers of step
-    // n's row reused by a load a few instructions after the store, lanes 12-15
-    // of every 16 stored the loaded rhs instead (tools/debug_tb.py).
-    // The compiler does not guard this, so the row stays live through the
-    // next two steps' loads (one step already suffices in every test).
-    asm volatile("" ::"v"(m.keep[0]));
-    m.keep[0] = m.keep[1];
-    m.keep[1] = v;
-#pragma unroll
-    for (int k = 0; k + 1 < D; ++k) m.Pq[k] = m.Pq[k + 1];
-    m.Pq[D - 1] = nP;
-    // steps are scheduled one at a time (one basic block per chunk, but no
-    // code motion across steps: measured faster, 0.856 vs 0.867 ms/iteration)
-    __builtin_amdgcn_sched_barrier(0);
-}
-
-// S steps of the steady march, the first at slot phase P0 (colour Q0)
-template <int T, int D, int Q0, int P0, bool BP, int... NN>
-__device__ __forceinline__ void steady_chunk(March<T, D>& m, d2* R, const Lane& c, const Sio& io,
-                                             int r0, unsigned off_n,
-                                             std::integer_sequence<int, NN...>) {
-    constexpr int S = ring_slots<T, D>();
-    (steady_step<T, D, Q0 ^ (NN & 1), (P0 + NN) % S, BP>(m, R, c, io, r0 + NN,
-                                                       off_n + (unsigned)NN * io.row_bytes),
-     ...);
-}
-
-// interior block of H = k * S rows: 4T paired warm-up steps, then k chunks of
-// S statically unrolled steps
-template <int T, int D, int Q0, bool BP>
-__device__ __forceinline__ void march_interior(March<T, D>& m, const Lane& c, const Io& io,
-                                               const Sio& sio, int rs, int nchunks) {
-    constexpr int S = ring_slots<T, D>();
-    march_pairs<T, D, Q0, kPre, BP>(m, c, io, rs, rs + 4 * T - 1);  // 4T is even
-    // ring in static slots: rhs row rs - 1 + j in slot j mod S; at step n = 4T
-    // the paired ring holds j = 4T - 1 - k (k < 2T), the rows in flight j = 4T + k
-    d2 R[S];
-#pragma unroll
-    for (int k = 0; k < S; ++k) R[k] = d2{0.0, 0.0};
-#pragma unroll
-    for (int k = 0; k < 2 * T; ++k) R[(4 * T - 1 - k) % S] = m.R[k];
-#pragma unroll
-    for (int k = 0; k < D; ++k) R[(4 * T + k) % S] = m.Rq[k];
-    // every chunk starts at slot phase 4T mod S (S is even, so colour Q0 too)
-    constexpr int P0 = (4 * T) % S;
-    int r0 = rs + 4 * T;
-    unsigned off = 4u * T * sio.row_bytes;
-    for (int k = 0; k < nchunks; ++k) {
-        steady_chunk<T, D, Q0, P0, BP>(m, R, c, sio, r0, off,
-                                       std::make_integer_sequence<int, S>{});
-        r0 += S;
-        off += (unsigned)S * sio.row_bytes;
-    }
-}
-
-}  // namespace
-
-// one block (bx, by) of a pass: logical block L
-template <int T, int WAVES, int D, bool BP>
-__device__ __forceinline__ void tb_block(const SweepParams& prm, const double* __restrict__ src,
-                                         double* __restrict__ dst, const double* __restrict__ rhs,
-                                         double* __restrict__ partials, const int L,
-                                         double (*wsum)[WAVES]) {
-    constexpr int OW = kStripCells - 4 * T;
-    constexpr int S = ring_slots<T, D>();
-    const int bx = L % prm.nbx, by = L / prm.nbx;
-    const int ni = prm.ni, nj = prm.nj;
-    // block rows: nby_big of H = rows_per_block rows, then h_small-row ones
-    // (short blocks, which the work order takes last), the last takes the rest
-    const int H = prm.rows_per_block;
-    const int j0 = by < prm.nby_big ? 1 + by * H
-                                    : 1 + prm.nby_big * H + (by - prm.nby_big) * prm.h_small;
-    const int j1 = by == prm.nby - 1 ? nj + 1 : j0 + (by < prm.nby_big ? H : prm.h_small);
-    if (prm.part != 0) {  // overlapped decomposed pass: blocks clear of the halo first
-        const int lo = 1 + bx * WAVES * OW - 2 * T;
-        const int hi = 1 + (bx * WAVES + WAVES - 1) * OW - 2 * T + kStripCells - 1;
-        const bool interior = lo >= prm.int_lo_i && hi <= prm.int_hi_i &&
-                              j0 - 2 * T >= prm.int_lo_j && j1 - 1 + 2 * T <= prm.int_hi_j;
-        if (interior != (prm.part == 1)) return;
-    }
-
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int strip = bx * WAVES + wave;
-    const int c_out = 1 + strip * OW;
-    const int c_ld = c_out - 2 * T;
-    const long long pitch = prm.pitch;
-
-    Lane c;
-    c.ia = c_ld + 2 * lane;
-    c.ib = c.ia + 1;
-    c.up_a = c.ia >= prm.upd_lo_i && c.ia <= prm.upd_hi_i;
-    c.up_b = c.ib >= prm.upd_lo_i && c.ib <= prm.upd_hi_i;
-    const bool own_lane = lane >= T && lane < kLanes - T;
-    c.own_a = own_lane && c.ia <= ni;
-    c.own_b = own_lane && c.ib <= ni;
-    c.fix0_b = prm.ghost_left && c.ib == 0;
-    c.fixr_a = prm.ghost_right && c.ia == ni + 1;
-    c.fixr_b = prm.ghost_right && c.ib == ni + 1;
-    // columns this lane stores: owned interior + the physical ghost columns
-    c.st_a = c.own_a || c.fixr_a;
-    c.st_b = c.own_b || c.fix0_b || c.fixr_b;
-    c.lo_j = prm.upd_lo_j;
-    c.hi_j = prm.upd_hi_j;
-    c.j0 = j0;
-    c.j1 = j1;
-    c.wlo = by == 0 && prm.ghost_bottom;
-    c.whi = by == prm.nby - 1 && prm.ghost_top;
-    c.parity = prm.parity;
-    c.gb = prm.ghost_bottom;
-    c.gt = prm.ghost_top;
-    c.nj = nj;
-    c.idx2 = prm.idx2;
-    c.idy2 = prm.idy2;
-    c.coef = prm.coef;
-    c.bl = ((lane + 63) & 63) * 4;
-    c.br = ((lane + 1) & 63) * 4;
-
-    March<T, D> m;
-#pragma unroll
-    for (int t = 0; t < T; ++t) m.acc[t] = 0.0;
-    m.keep[0] = m.keep[1] = d2{0.0, 0.0};
-
-    // physical corners are never touched by solveRB; carry them into dst
-    if (L == 0 && threadIdx.x < 4) {
-        const int t = threadIdx.x;
-        const int ci = (t & 1) ? ni + 1 : 0, cj = (t & 2) ? nj + 1 : 0;
-        const bool phys = ((t & 1) ? prm.ghost_right : prm.ghost_left) &&
-                          ((t & 2) ? prm.ghost_top : prm.ghost_bottom);
-        if (phys) {
-            const long long k = (long long)(cj + kYOff) * pitch + (ci + kXOff);
-            dst[k] = src[k];
-        }
-    }
-
-    if (c_out <= ni) {  // wave-uniform
-        const long long base = (long long)kYOff * pitch + kXOff + c.ia;
-        Io io{src + base, rhs + base, dst + base, pitch};
-        const int rs = j0 - 2 * T;  // first streamed row
-        const int rend = j1 - 1 + 2 * T;
-#pragma unroll
-        for (int k = 0; k < D; ++k) {
-            m.Pq[k] = ldv(io.sp + (long long)(rs + k) * pitch);
-            m.Rq[k] = ldv(io.rp + (long long)(rs - 1 + k) * pitch);
-        }
-#pragma unroll
-        for (int t = 0; t < T; ++t) m.A[t] = m.M1[t] = m.M2[t] = d2{0.0, 0.0};
-#pragma unroll
-        for (int k = 0; k < 2 * T; ++k) m.R[k] = d2{0.0, 0.0};
-        // the colour of row rs: the same for every block of the launch (H even)
-        const bool q1 = ((c.parity + rs) & 1) != 0;
-
-        // columns interior: every column of the cone an updated cell (no lane
-        // masks, no ghost columns) and ownership uniform per lane -- the strip
-        // is whole, or it runs past column ni into a neighbour's halo (or the
-        // padding beyond it) with ni even, so ni | ni+1 falls between lanes;
-        // those lanes are neither stored nor counted.  Rows interior: no
-        // ghost rows in the cone, and a block height the static ring divides.
-        const bool cols_in = c_ld >= prm.upd_lo_i && c_ld + kStripCells - 1 <= prm.upd_hi_i &&
-                             (c_out + OW - 1 <= ni || (ni & 1) == 0);
-        const bool rows_in = rs >= prm.upd_lo_j && rend <= prm.upd_hi_j &&
-                             (j1 - j0) % S == 0 && j1 - j0 > 0;
-        if (!cols_in) {
-            if (q1) march_pairs<T, D, 1, kEdge>(m, c, io, rs, rend);
-            else    march_pairs<T, D, 0, kEdge>(m, c, io, rs, rend);
-        } else {
-            if (rows_in) {
-                // wave-uniform descriptors over the strip's 128 columns
-                auto rsrc = [&](const double* b, int row0, int rows) {
-                    const unsigned long long a = (unsigned long long)(
-                        b + (long long)(kYOff + row0) * pitch + kXOff + c_ld);
-                    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
-                    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
-                    return __builtin_amdgcn_make_buffer_rsrc(
-                        (void*)(((unsigned long long)hi << 32) | lo), (short)0,
-                        (int)((long long)rows * pitch * 8), 0x00020000);
-                };
-                Sio sio;
-                sio.p = rsrc(src, rs, rend - rs + 1 + D);
-                sio.r = rsrc(rhs, rs - 1, rend - rs + 1 + D);
-                sio.d = rsrc(dst, j0, j1 - j0);
-                sio.lane = (unsigned)lane * 16u;
-                sio.st_lane = c.own_a ? (unsigned)lane * 16u : 0x40000000u;
-                sio.row_bytes = (unsigned)(pitch * 8);
-                const int nchunks = (j1 - j0) / S;
-                if (q1) march_interior<T, D, 1, BP>(m, c, io, sio, rs, nchunks);
-                else    march_interior<T, D, 0, BP>(m, c, io, sio, rs, nchunks);
-            } else {
-                if (q1) march_pairs<T, D, 1, kRowEdge>(m, c, io, rs, rend);
-                else    march_pairs<T, D, 0, kRowEdge>(m, c, io, rs, rend);
-            }
-            if (!c.own_a) {
-#pragma unroll
-                for (int t = 0; t < T; ++t) m.acc[t] = 0.0;
-            }
-        }
-    }
-
-    // deterministic reduction per stage: lane tree, then waves in order
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-        const double s = wave_sum(m.acc[t]);
-        if (lane == 0) wsum[t][wave] = s;
-    }
-    __syncthreads();
-    if (threadIdx.x < T) {
-        const int t = threadIdx.x;
-        double s = 0.0;
-#pragma unroll
-        for (int w = 0; w < WAVES; ++w) s += wsum[t][w];
-        partials[(long long)t * prm.nblocks + L] = s;
-    }
-    __syncthreads();  // wsum is reused by the workgroup's next block
-}
-
-// occupancy target: 2 waves per SIMD (the register file of one wave is 256
-// VGPRs; below that the compiler would rather use AGPRs and run one wave).
-//
-// Two ways to hand out blocks:
-//  - one workgroup per block (queue == nullptr): block L of workgroup
-//    blockIdx.x, dealt to XCDs in contiguous runs (xcd_remap);
-//  - persistent (queue != nullptr): as many workgroups as fit on the GPU at
-//    once; workgroup w (on XCD w % 8, the hardware's round-robin) takes
-//    tickets from its XCD's queue -- a contiguous run of blocks, as above --
-//    and, once that is empty, from the other XCDs' queues.  The makespan then
-//    ends within one block of the last one started, instead of a last,
-//    partly filled round of workgroups (one rank's block at 8 GPUs runs
-//    3.5 rounds of 512 workgroups).  queue[0..7] are zeroed before the launch.
-template <int T, int WAVES, int D, bool BP>
-__global__ __launch_bounds__(kLanes* WAVES, 2) void rb_tb_kernel(
-    SweepParams prm, const double* __restrict__ src, double* __restrict__ dst,
-    const double* __restrict__ rhs, double* __restrict__ partials,
-    const DevState* __restrict__ st, int force, int* __restrict__ queue) {
-    __shared__ double wsum[T][WAVES];
-    __shared__ int ticket;
-    if (!force && st->done) return;
-    const int nwg = prm.nblocks, qq = nwg / 8, rr = nwg % 8;
-    auto run_start = [&](int x) { return x < rr ? x * (qq + 1) : rr * (qq + 1) + (x - rr) * qq; };
-    // Work order (persistent launches): the blocks on the grid's border first
-    // (the slower lane-masked / row-tested marches: strips at a physical
-    // left/right side, block rows at a physical bottom/top side, the last
-    // block row of non-uniform height), then the rest in row-major order (the
-    // short block rows last); the XCD queues hold contiguous runs of that
-    // order.  Slow blocks start early and the pass ends on short ones.
-    const int nbx = prm.nbx, nby = prm.nby;
-    auto order = [&](int k) -> int {  // k-th block of the work order -> L
-        if (nby <= 2 || nbx <= 2) return k;
-        if (k < nbx) return k;                                 // bottom row
-        k -= nbx;
-        if (k < nbx) return (nby - 1) * nbx + k;               // top row
-        k -= nbx;
-        if (k < nby - 2) return (1 + k) * nbx;                 // left column
-        k -= nby - 2;
-        if (k < nby - 2) return (1 + k) * nbx + nbx - 1;       // right column
-        k -= nby - 2;
-        const int w = nbx - 2;                                 // the rest
-        return (1 + k / w) * nbx + 1 + k % w;
-    };
-    const int home = blockIdx.x % 8;
-    bool first = true;
-    for (int probe = 0; probe < 8;) {
-        int L;
-        if (!queue) {  // one workgroup per block: one trip
-            if (!first) break;
-            L = blockIdx.x;
-            if (prm.xcd_remap) L = run_start(L % 8) + L / 8;
-        } else {
-            const int x = (home + probe) & 7;
-            if (threadIdx.x == 0) ticket = atomicAdd(&queue[x], 1);
-            __syncthreads();
-            const int b = ticket;
-            __syncthreads();
-            if (b >= (x < rr ? qq + 1 : qq)) {
-                ++probe;
-                continue;
-            }
-            L = order(run_start(x) + b);
-        }
-        first = false;
-        tb_block<T, WAVES, D, BP>(prm, src, dst, rhs, partials, L, wsum);
-    }
-}
-
-int tb_out_width(int T) { return kStripCells - 4 * T; }
+int tb_out_width(int T, int variant) { return kLanes * tb_cols(variant) - 4 * T; }
 
 int tb_waves(int variant) { return kTbVariants[variant].waves; }
 
@@ -683,105 +19,32 @@ int tb_ring_slots(int T, int variant) {
     return 2 * T + D + (D & 1);
 }
 
-int tb_nbx(int ni, int T, int waves) {
-    const int ow = tb_out_width(T);
+int tb_nbx(int ni, int T, int variant) {
+    const int ow = tb_out_width(T, variant);
     const int strips = (ni + ow - 1) / ow;
+    const int waves = tb_waves(variant);
     return (strips + waves - 1) / waves;
-}
-
-// workgroups of a persistent launch: as many as are resident at once
-template <int T, int W, int D, bool B>
-static int persistent_grid() {
-    static int n = 0;
-    if (n == 0) {
-        int per_cu = 0, dev = 0, cus = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rb_tb_kernel<T, W, D, B>,
-                                                           kLanes * W, 0);
-        n = std::max(8, per_cu * cus);
-    }
-    return n;
 }
 
 void launch_tb(hipStream_t s, int T, const SweepParams& prm, const double* src, double* dst,
                const double* rhs, double* partials, const DevState* st, int force, int* queue) {
-#define TBB(TT, W, DD, BB)                                                                    \
-    do {                                                                                     \
-        int grid_ = prm.nblocks;                                                             \
-        if (queue) {                                                                         \
-            (void)hipMemsetAsync(queue, 0, 8 * sizeof(int), s);                              \
-            grid_ = std::min(grid_, persistent_grid<TT, W, DD, BB>());                      \
-        }                                                                                    \
-        hipLaunchKernelGGL((rb_tb_kernel<TT, W, DD, BB>), dim3(grid_), dim3(kLanes * W), 0, s, \
-                           prm, src, dst, rhs, partials, st, force, queue);                  \
-    } while (0)
-#define TB(TT, W, DD) TBB(TT, W, DD, false)
-#define TB_T(TT)                       \
-    switch (prm.variant) {             \
-    case 1: TB(TT, 8, 2); break;       \
-    case 2: TB(TT, 2, 2); break;       \
-    case 3: TB(TT, 1, 2); break;       \
-    case 4: TB(TT, 4, 3); break;       \
-    default: TB(TT, 4, 2); break;      \
-    }
-    // must match kTbVariants (misor_internal.h)
-#ifdef MISOR_TB_QUICK  // experiment builds only: T = 7, default variant
-    TB(7, 4, 2);
-    (void)T;
-#else
     switch (T) {
-    case 1: TB_T(1); break;  // the last pass of a capped solve, or a recompute
-    case 2: TB_T(2); break;
-    case 3: TB_T(3); break;
-    case 4: TB_T(4); break;
-    case 5: TB_T(5); break;
-    case 6: TB_T(6); break;
-    case 7: TB_T(7); break;
-    case 8: TB_T(8); break;
-    case 9: TB_T(9); break;
-    case 10: TB_T(10); break;
-    case 11: TB_T(11); break;
-    default: TB_T(12); break;
+#define C(N)                                                                \
+    case N: launch_tb_t##N(s, prm, src, dst, rhs, partials, st, force, queue); break;
+    C(1) C(2) C(3) C(4) C(5) C(6) C(7) C(8) C(9) C(10) C(11)
+#undef C
+    default: launch_tb_t12(s, prm, src, dst, rhs, partials, st, force, queue); break;
     }
-#endif
-#undef TB_T
-#undef TB
-#undef TBB
 }
 
 int tb_resident(int T, int variant) {
-#define RES(TT, W, DD, BB) return persistent_grid<TT, W, DD, BB>()
-#define RES_T(TT)                                      \
-    switch (variant) {                                 \
-    case 1: RES(TT, 8, 2, false);                      \
-    case 2: RES(TT, 2, 2, false);                      \
-    case 3: RES(TT, 1, 2, false);                      \
-    case 4: RES(TT, 4, 3, false);                      \
-    default: RES(TT, 4, 2, false);                     \
-    }
-#ifdef MISOR_TB_QUICK
-    (void)T;
-    (void)variant;
-    RES(7, 4, 2, false);
-#else
     switch (T) {
-    case 1: RES_T(1);
-    case 2: RES_T(2);
-    case 3: RES_T(3);
-    case 4: RES_T(4);
-    case 5: RES_T(5);
-    case 6: RES_T(6);
-    case 7: RES_T(7);
-    case 8: RES_T(8);
-    case 9: RES_T(9);
-    case 10: RES_T(10);
-    case 11: RES_T(11);
-    default: RES_T(12);
+#define C(N) \
+    case N: return tb_resident_t##N(variant);
+    C(1) C(2) C(3) C(4) C(5) C(6) C(7) C(8) C(9) C(10) C(11)
+#undef C
+    default: return tb_resident_t12(variant);
     }
-#endif
-#undef RES_T
-#undef RES
 }
 
 }  // namespace misor

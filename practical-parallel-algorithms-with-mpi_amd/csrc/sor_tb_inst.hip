@@ -1,0 +1,102 @@
+// sor_tb_inst.hip -- the kernels of ONE pass length T = MISOR_TB_T (compiled
+// once per T by the Makefile: build/sor_tb_t<T>.o).  Device code: sor_tb.h.
+#include <algorithm>
+
+#include "sor_tb.h"
+
+#ifndef MISOR_TB_T
+#error "compile with -DMISOR_TB_T=<iterations per pass>"
+#endif
+#define MISOR_CAT2(a, b) a##b
+#define MISOR_CAT(a, b) MISOR_CAT2(a, b)
+
+namespace misor {
+
+// workgroups of a persistent launch: as many as are resident at once
+template <class K>
+static int persistent_grid(K kernel, int threads) {
+    int per_cu = 0, dev = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0);
+    return std::max(8, per_cu * cus);
+}
+
+template <int T, int W, int D, bool B>
+static int resident2() {
+    static int n = 0;
+    if (n == 0) n = persistent_grid(rb_tb_kernel<T, W, D, B>, kLanes * W);
+    return n;
+}
+
+template <int T, int W, int D, int SC>
+static int resident4() {
+    static int n = 0;
+    if (n == 0) n = persistent_grid(rb_tb4_kernel<T, W, D, SC>, kLanes * W);
+    return n;
+}
+
+constexpr int kT = MISOR_TB_T;
+// a quad variant exists for T <= its max_t (its LDS ring must fit); configure_tb
+// never selects it above
+template <int V>
+constexpr bool quad_ok() {
+    return kTbVariants[V].cols == 4 && kT <= kTbVariants[V].max_t;
+}
+
+void MISOR_CAT(launch_tb_t, MISOR_TB_T)(hipStream_t s, const SweepParams& prm,
+                                        const double* src, double* dst, const double* rhs,
+                                        double* partials, const DevState* st, int force,
+                                        int* queue) {
+    auto go = [&](auto kernel, int threads, int resident) {
+        int grid = prm.nblocks;
+        if (queue) {
+            (void)hipMemsetAsync(queue, 0, 8 * sizeof(int), s);
+            grid = std::min(grid, resident);
+        }
+        hipLaunchKernelGGL(kernel, dim3(grid), dim3(threads), 0, s, prm, src, dst, rhs, partials,
+                           st, force, queue);
+    };
+#define TB(W, DD) go(rb_tb_kernel<kT, W, DD, false>, kLanes * W, resident2<kT, W, DD, false>())
+    // must match kTbVariants (misor_internal.h)
+    switch (prm.variant) {
+    case 1: TB(8, 2); break;
+    case 2: TB(2, 2); break;
+    case 3: TB(1, 2); break;
+    case 4: TB(4, 3); break;
+#define Q4(V)                                                                               \
+    case V:                                                                                 \
+        if constexpr (quad_ok<V>()) {                                                       \
+            constexpr int D_ = kTbVariants[V].ahead, SC_ = kTbVariants[V].sched;            \
+            go(rb_tb4_kernel<kT, 4, D_, SC_>, kLanes * 4, resident4<kT, 4, D_, SC_>());     \
+            break;                                                                          \
+        }                                                                                   \
+        [[fallthrough]];
+    Q4(5)
+    default:
+        if (prm.pow2) go(rb_tb_kernel<kT, 4, 2, false, true>, kLanes * 4, resident2<kT, 4, 2, false>());
+        else TB(4, 2);
+        break;
+    }
+#undef Q4
+#undef TB
+}
+
+int MISOR_CAT(tb_resident_t, MISOR_TB_T)(int variant) {
+    switch (variant) {
+    case 1: return resident2<kT, 8, 2, false>();
+    case 2: return resident2<kT, 2, 2, false>();
+    case 3: return resident2<kT, 1, 2, false>();
+    case 4: return resident2<kT, 4, 3, false>();
+#define Q4(V)                                                                             \
+    case V:                                                                               \
+        if constexpr (quad_ok<V>())                                                       \
+            return resident4<kT, 4, kTbVariants[V].ahead, kTbVariants[V].sched>();        \
+        [[fallthrough]];
+    Q4(5)
+#undef Q4
+    default: return resident2<kT, 4, 2, false>();
+    }
+}
+
+}  // namespace misor

@@ -23,9 +23,11 @@ def set_mode(g, small):
     """small = 1: whole-solve LDS kernel where the grid fits; 0: the
     multi-block path with the default iterations per pass; "tN": the
     multi-block path with N iterations per pass (1: single-iteration sweep
-    kernel, 2..4: temporally blocked kernel).  All must match the reference."""
+    kernel, 2..: temporally blocked kernel); "qN": the same with 4 columns per
+    lane (TB variant 5).  All must match the reference."""
     if isinstance(small, str):
         g.set_tuning(M.TUNE_SMALL_SOLVE, 0)
+        g.set_tuning(M.TUNE_TB_VARIANT, QUAD if small[0] == "q" else 0)
         g.set_tuning(M.TUNE_TSTEPS, int(small[1:]))
     else:
         g.set_tuning(M.TUNE_SMALL_SOLVE, small)
@@ -38,7 +40,8 @@ def make_grid(ni, nj, xl=1.0, yl=1.0, omega=OMEGA, eps=EPS, itermax=1000000,
     return set_mode(g, small)
 
 
-TS = ["t%d" % t for t in range(1, 11)]
+QUAD = 5  # TB variant: 4 columns per lane (sor_tb.h, quad_interior)
+TS = ["t%d" % t for t in range(1, 11)] + ["q2", "q5", "q7", "q8"]
 PATHS = pytest.mark.parametrize("small", [1] + TS, ids=["lds"] + TS)
 
 
@@ -190,7 +193,7 @@ def test_large_grid_few_sweeps(k, finish2, monkeypatch):
 
 
 @pytest.mark.parametrize("T", range(2, 13))
-@pytest.mark.parametrize("variant", range(5))
+@pytest.mark.parametrize("variant", range(6))
 def test_tb_converges_mid_pass(T, variant):
     """convergence inside a temporally blocked pass: the pass is recomputed
     with fewer iterations, so the count and p equal solveRB's for every T"""
@@ -199,8 +202,17 @@ def test_tb_converges_mid_pass(T, variant):
     want = p.copy()
     eps = 3e-3
     it_ref, res_ref = orc.solve_rb(want, rhs, 1.0 / ni, 1.0 / nj, OMEGA, eps, 100000)
+    if variant == QUAD and T > 8:
+        with make_grid(ni, nj, small="t8") as g:
+            with pytest.raises(M.MisorError):
+                g.set_tuning(M.TUNE_TB_VARIANT, QUAD)
+                g.set_tuning(M.TUNE_TSTEPS, T)
+        return
     with make_grid(ni, nj, eps=eps, small="t%d" % T) as g:
+        if variant == QUAD:  # the quad variant first caps T at 8
+            g.set_tuning(M.TUNE_TSTEPS, 2)
         g.set_tuning(M.TUNE_TB_VARIANT, variant)  # strips per workgroup, rows in flight
+        g.set_tuning(M.TUNE_TSTEPS, T)
         g.poisson_init(1.0, 1.0, 2)
         it, res = g.solve_rb()
         got = g.download(M.P)
@@ -209,3 +221,91 @@ def test_tb_converges_mid_pass(T, variant):
     assert it == it_ref
     assert np.array_equal(got, want)
     assert abs(res - res_ref) <= 1e-12 * res_ref
+
+
+@pytest.mark.parametrize("T", [1, 2, 3, 5, 7, 8])
+@pytest.mark.parametrize("ni,nj", [(1201, 700), (2000, 1033), (1826, 600)])
+def test_quad_interior_vs_oracle(ni, nj, T):
+    """4 columns per lane: grids wide enough for interior 256-column strips
+    (the LDS-ring march) beside the 128-column strips of the border blocks;
+    k = one pass, two passes and a ragged remainder, random fields"""
+    rng = np.random.default_rng(ni * 31 + nj + T)
+    p = rng.standard_normal((nj + 2, ni + 2))
+    rhs = rng.standard_normal((nj + 2, ni + 2))
+    dx, dy = 1.1 / ni, 0.9 / nj
+    for k in (T, 2 * T + 1):
+        want = p.copy()
+        orc.solve_rb(want, rhs, dx, dy, 1.7, 1e-300, k)
+        with M.Grid(ni, nj, dx, dy, 1.7, 1e-300, k) as g:
+            set_mode(g, "q%d" % T)
+            g.set_tuning(M.TUNE_TB_ROWS, 48)  # several block rows
+            g.upload(M.P, p)
+            g.upload(M.RHS, rhs)
+            it, _ = g.solve_rb()
+            got = g.download(M.P)
+            assert g.get_tuning(M.TUNE_TB_VARIANT) == QUAD
+        assert it == k
+        assert np.array_equal(got, want), (k, np.argwhere(got != want)[:5])
+
+
+def test_quad_converges_mid_pass_interior():
+    """convergence inside a pass on a grid with interior quad strips: eps is
+    put between the residual of iteration k* and the smallest one before it
+    (the oracle's residual sequence), so solveRB stops at k*, inside a pass"""
+    ni, nj = 800, 300
+    rng = np.random.default_rng(3)
+    # scaled so every residual is < 1 (solveRB's loop starts from res = 1.0)
+    p0 = rng.standard_normal((nj + 2, ni + 2)) * 2.0 ** -30
+    rhs = np.zeros_like(p0)
+    res = {}
+    for k in range(1, 60):
+        q = p0.copy()
+        res[k] = orc.solve_rb(q, rhs, 1.0 / ni, 1.0 / nj, OMEGA, 1e-300, k)[1]
+    for ks in range(35, 60):
+        lo = min(res[k] for k in range(1, ks))
+        if res[ks] < lo * (1 - 1e-6) and ks % 7 and ks % 8:
+            break
+    else:
+        pytest.skip("no strictly decreasing residual step in range")
+    eps = ((res[ks] + lo) / 2) ** 0.5
+    want = p0.copy()
+    it_ref, res_ref = orc.solve_rb(want, rhs, 1.0 / ni, 1.0 / nj, OMEGA, eps, 100000)
+    assert it_ref == ks
+    for T in (7, 8):
+        with make_grid(ni, nj, eps=eps, small="q%d" % T) as g:
+            g.set_tuning(M.TUNE_TB_ROWS, 36)
+            g.upload(M.P, p0)
+            g.upload(M.RHS, rhs)
+            it, r = g.solve_rb()
+            got = g.download(M.P)
+        assert it == it_ref, (it, it_ref, T)
+        assert np.array_equal(got, want)
+        assert abs(r - res_ref) <= 1e-12 * res_ref
+
+
+@pytest.mark.parametrize("T", [2, 5, 8])
+@pytest.mark.parametrize("ni,nj", [(1024, 1024), (1000, 1537), (2050, 300)])
+def test_pow2_spacing_vs_oracle(ni, nj, T, monkeypatch):
+    """dx == dy == 2^-10: the TB kernel computes r with one fma in place of
+    two multiplies, an add and a subtract (sor_tb.h resid<true>); bit for bit
+    the reference's expression, on random fields of a wide dynamic range, and
+    identical to the general form (MISOR_NO_POW2=1)"""
+    rng = np.random.default_rng(ni + 7 * nj + T)
+    p = rng.standard_normal((nj + 2, ni + 2)) * np.exp(rng.uniform(-20, 20, (nj + 2, ni + 2)))
+    rhs = rng.standard_normal((nj + 2, ni + 2)) * 1e6
+    h = 2.0 ** -10
+    k = 2 * T + 1
+    want = p.copy()
+    orc.solve_rb(want, rhs, h, h, 1.7, 1e-300, k)
+    got = {}
+    for no in ("0", "1"):
+        monkeypatch.setenv("MISOR_NO_POW2", no)
+        with M.Grid(ni, nj, h, h, 1.7, 1e-300, k) as g:
+            set_mode(g, "t%d" % T)
+            g.upload(M.P, p)
+            g.upload(M.RHS, rhs)
+            it, _ = g.solve_rb()
+            got[no] = g.download(M.P)
+        assert it == k
+    assert np.array_equal(got["0"], want), np.argwhere(got["0"] != want)[:5]
+    assert np.array_equal(got["1"], want)

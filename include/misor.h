@@ -206,9 +206,17 @@ enum {
                                     * rows in flight */
     MISOR_TUNE_TB_ROWS = 8,        /* temporally blocked kernel: rows per block; <= 0: auto
                                     * (a multiple of the kernel's rhs ring) */
-    MISOR_TUNE_TB_PERSISTENT = 9   /* temporally blocked kernel: 1 (default) = as many
+    MISOR_TUNE_TB_PERSISTENT = 9,  /* temporally blocked kernel: 1 (default) = as many
                                     * workgroups as are resident, taking blocks from per-XCD
                                     * work queues; 0 = one workgroup per block */
+    MISOR_TUNE_NS_FUSE = 10,       /* 1 (default): misor_compute_fg also computes RHS in the
+                                    * same pass over u, v (computeRHS then only completes the
+                                    * cells next to a neighbour rank); 0 = separate kernels */
+    MISOR_TUNE_FINISH2 = 11,       /* single rank: 1 (default) = two-level loop test
+                                    * (partial sums, then the test); 0 = one kernel */
+    MISOR_TUNE_TB_RESERVE = 12     /* decomposed, overlapped: workgroup slots the persistent
+                                    * interior launch leaves to the exchange / all-reduce /
+                                    * edge-block streams (default 16) */
 };
 int misor_set_tuning(misor_grid* g, int key, int value);
 int misor_get_tuning(const misor_grid* g, int key, int* value);

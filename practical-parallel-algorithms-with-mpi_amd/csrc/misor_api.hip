@@ -117,6 +117,13 @@ struct misor_grid {
     // adaptUV leaves max |u|, |v| partials in max_partials (max_ver = uv_ver)
     unsigned uv_ver = 1, max_ver = 0;
     double* max_partials = nullptr;
+    // f, g, rhs versions: every write of f, g or rhs from outside bumps fgr_ver;
+    // the fused computeFG (ns_fuse) leaves rhs computed from its f, g with dt
+    // fused_dt (fused_ver = fgr_ver), so computeRHS only completes the cells
+    // next to a neighbour rank
+    bool ns_fuse = true;
+    unsigned fgr_ver = 1, fused_ver = 0;
+    double fused_dt = 0.0;
 
     // sweep
     SweepParams sp{};
@@ -134,6 +141,8 @@ struct misor_grid {
     int tb_nparts = 0;
     int tb_rows_req = 0;          // MISOR_TUNE_TB_ROWS (0: automatic)
     bool tb_persistent = true;    // MISOR_TUNE_TB_PERSISTENT: work-queue launches
+    int tb_reserve = kTbReserve;  // MISOR_TUNE_TB_RESERVE: slots a pipelined interior launch
+                                  // leaves to the communication / edge-block streams
     int* tb_queue = nullptr;      // 8 per-XCD block counters of a persistent launch
 
     // reductions
@@ -835,6 +844,8 @@ int misor_create(misor_grid** out, const misor_desc* d) {
     {
         const char* e = getenv("MISOR_FINISH2");
         g->finish2 = !(e && e[0] == '0');
+        e = getenv("MISOR_NS_FUSE");  // A/B switch (bench.py --workload ns)
+        g->ns_fuse = !(e && e[0] == '0');
     }
     const int T0 = (long long)g->loc.ni * g->loc.nj >= kTsteps8Cells ? kDefaultTsteps
                                                                       : kSmallBlockTsteps;
@@ -901,6 +912,7 @@ int misor_upload(misor_grid* g, int field, const double* host) {
     const size_t h = (size_t)(g->loc.nj + 2);
     if (field == MISOR_RHS) g->rhs_halo = 0;
     if (field == MISOR_U || field == MISOR_V) ++g->uv_ver;
+    if (field == MISOR_F || field == MISOR_G || field == MISOR_RHS) ++g->fgr_ver;
     if (field == MISOR_P) {  // every pressure buffer: corners and ghosts must agree
         g->cur = 0;
         for (int b = 0; b < g->np; ++b)
@@ -1069,6 +1081,7 @@ int misor_fill(misor_grid* g, int field, double value) {
     // whole padded array: ghosts included, pads too (pads never feed results)
     if (field == MISOR_RHS) g->rhs_halo = 0;
     if (field == MISOR_U || field == MISOR_V) ++g->uv_ver;
+    if (field == MISOR_F || field == MISOR_G || field == MISOR_RHS) ++g->fgr_ver;
     if (field == MISOR_P) {
         g->cur = 0;
         for (int b = 0; b < g->np; ++b) launch_fill(g->stream, pbuf(g, b), g->elems, value);
@@ -1104,6 +1117,7 @@ int misor_poisson_init(misor_grid* g, double xlength, double ylength, int proble
                           hipMemcpyHostToDevice, g->stream));
     g->cur = 0;
     g->rhs_halo = 0;
+    ++g->fgr_ver;
     for (int b = 0; b < g->np; ++b)
         launch_poisson_init(g->stream, pbuf(g, b), g->fld[kRhs], tab, tab + 2 * (ni + 2),
                             tab + (ni + 2), ni, nj, g->pitch, problem);
@@ -1194,6 +1208,12 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
         } else {
             SweepParams tp = g->tp;
             tp.part = part;
+            // the interior blocks of an overlapped pass leave workgroup slots to the
+            // halo exchange, the residual all-reduce + loop test and the edge blocks
+            // on the other streams: a persistent launch holds every slot it gets
+            // until the pass is over, so without them the exchange would only start
+            // at the end of the interior blocks
+            tp.reserve = part == 1 ? g->tb_reserve : 0;
             if (Tp != T) tb_geometry(g, Tp, tp);  // narrower cone: wider strips
             // persistent work-queue launch on the grid stream (whole passes and
             // interior blocks); the boundary blocks of a split pass are few
@@ -1557,18 +1577,39 @@ int misor_compute_fg(misor_grid* g) {
     int rc = exchange(g, g->fld[kU], 1);  // 9-point stencil incl. diagonals: corners too
     if (!rc) rc = exchange(g, g->fld[kV], 1);
     if (rc) return rc;
-    launch_compute_fg(g->nl, g->fld[kU], g->fld[kV], g->fld[kF], g->fld[kG]);
+    ++g->fgr_ver;
+    if (g->ns_fuse) {  // computeRHS of the same f, g in the same pass (ns_kernels.hip)
+        launch_compute_fg_rhs(g->nl, g->fld[kU], g->fld[kV], g->fld[kF], g->fld[kG],
+                              g->fld[kRhs]);
+        g->rhs_halo = 0;
+        g->fused_ver = g->fgr_ver;
+        g->fused_dt = g->nl.prm.dt;
+    } else {
+        launch_compute_fg(g->nl, g->fld[kU], g->fld[kV], g->fld[kF], g->fld[kG]);
+    }
     HIPCHK(hipGetLastError());
     return MISOR_OK;
 }
 
 int misor_compute_rhs(misor_grid* g) {
     NEED_NS(g);
+    // the fused computeFG already wrote rhs from these f, g and this dt: only
+    // the cells that read a neighbour's F(0, j) / G(i, 0) are left
+    // (decomposed: the exchange is collective, so every rank takes part, also
+    // one with walls on its left and bottom whose rhs is complete already)
+    const bool fused = g->fused_ver == g->fgr_ver && g->fused_dt == g->nl.prm.dt;
+    ++g->fgr_ver;
+    g->rhs_halo = 0;
+    if (fused && !g->dist) return MISOR_OK;
     int rc = exchange(g, g->fld[kF], 1);  // F(i-1,j), G(i,j-1): the skeleton's shift()
     if (!rc) rc = exchange(g, g->fld[kG], 1);
     if (rc) return rc;
-    launch_compute_rhs(g->nl, g->fld[kF], g->fld[kG], g->fld[kRhs]);
-    g->rhs_halo = 0;
+    if (fused) {
+        if (!(g->nl.wall_left && g->nl.wall_bottom))
+            launch_rhs_edges(g->nl, g->fld[kF], g->fld[kG], g->fld[kRhs]);
+    } else {
+        launch_compute_rhs(g->nl, g->fld[kF], g->fld[kG], g->fld[kRhs]);
+    }
     HIPCHK(hipGetLastError());
     return MISOR_OK;
 }
@@ -1655,6 +1696,12 @@ int misor_set_tuning(misor_grid* g, int key, int value) {
     case MISOR_TUNE_TB_VARIANT: return configure_tb(g, g->tsteps, value, g->tb_rows_req);
     case MISOR_TUNE_TB_ROWS: return configure_tb(g, g->tsteps, g->tp.variant, value);
     case MISOR_TUNE_TB_PERSISTENT: g->tb_persistent = value != 0; return MISOR_OK;
+    case MISOR_TUNE_NS_FUSE: g->ns_fuse = value != 0; return MISOR_OK;
+    case MISOR_TUNE_FINISH2: g->finish2 = value != 0; return MISOR_OK;
+    case MISOR_TUNE_TB_RESERVE:
+        if (value < 0) return fail(MISOR_EINVAL, "reserve must be >= 0");
+        g->tb_reserve = value;
+        return MISOR_OK;
     default: return fail(MISOR_EINVAL, "unknown tuning key %d", key);
     }
 }
@@ -1671,6 +1718,9 @@ int misor_get_tuning(const misor_grid* g, int key, int* value) {
     case MISOR_TUNE_TB_VARIANT: *value = g->tp.variant; return MISOR_OK;
     case MISOR_TUNE_TB_ROWS: *value = g->tp.rows_per_block; return MISOR_OK;
     case MISOR_TUNE_TB_PERSISTENT: *value = g->tb_persistent; return MISOR_OK;
+    case MISOR_TUNE_NS_FUSE: *value = g->ns_fuse; return MISOR_OK;
+    case MISOR_TUNE_FINISH2: *value = g->finish2; return MISOR_OK;
+    case MISOR_TUNE_TB_RESERVE: *value = g->tb_reserve; return MISOR_OK;
     default: return fail(MISOR_EINVAL, "unknown tuning key %d", key);
     }
 }

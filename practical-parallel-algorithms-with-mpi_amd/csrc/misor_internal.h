@@ -85,6 +85,7 @@ constexpr int kTbRowLadder[] = {576, 384, 288, 192};
 constexpr int kTbRowLadderLen = 4;
 constexpr int kTbSmallRows = 32;       // short block rows the work order takes last ...
 constexpr int kTbSmallRounds = 2;      // ... about this many resident rounds of them
+constexpr int kTbReserve = 16;         // slots a pipelined interior launch leaves free
 int tb_waves(int variant);
 // rhs ring slots of the steady march: interior block heights are multiples of it
 int tb_ring_slots(int T, int variant);
@@ -128,6 +129,8 @@ struct SweepParams {
                                                  // neighbour sides)
     double idx2, idy2, coef;  // 1/dx^2, 1/dy^2, factor (RB) or omega*factor (RBA)
     int pow2;                 // idx2 == idy2 == 2^m, m >= 0: the default TB kernel's P2 form
+    int reserve;              // persistent launch: leave this many workgroup slots free
+                              // (host only; the comm / edge streams' kernels run there)
 };
 
 struct NsParams {
@@ -216,6 +219,11 @@ void launch_special_bc(const NsLaunch& L, double* u);
 void launch_compute_fg(const NsLaunch& L, const double* u, const double* v, double* f,
                        double* g);
 void launch_compute_rhs(const NsLaunch& L, const double* f, const double* g, double* rhs);
+// computeFG + computeRHS in one column march (RHS of column 1 / row 1 next to a
+// neighbour rank left to launch_rhs_edges after the f, g exchange)
+void launch_compute_fg_rhs(const NsLaunch& L, const double* u, const double* v, double* f,
+                           double* g, double* rhs);
+void launch_rhs_edges(const NsLaunch& L, const double* f, const double* g, double* rhs);
 void launch_adapt_uv(const NsLaunch& L, const double* f, const double* g, const double* p,
                      double* u, double* v);
 // reductions over ALL (ni+2)(nj+2) cells: partial per block, then a finish

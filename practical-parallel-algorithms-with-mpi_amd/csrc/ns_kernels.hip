@@ -195,6 +195,153 @@ void launch_compute_fg(const NsLaunch& L, const double* u, const double* v, doub
                        L.wall_right, L.wall_bottom, L.wall_top);
 }
 
+// ---- computeFG fused with computeRHS (:122-138).  The reference's main loop
+// (main.c:43-60) calls computeRHS right after computeFG, and RHS needs only
+// F(i-1..i, j) and G(i, j-1..j): the column march has both at hand.  The lanes
+// keep fg_kernel's aligned columns (lane = column i, a wave's row segment on
+// whole 128-B lines); F(i-1, j) is recomputed in the lane from the same
+// registers plus u(i-2, j) (the kernel is bound by HBM, not by its FP64 work,
+// so the second F costs no time), and G(i, j-1) is carried in a register (the
+// band's first row gets it from one extra row of the march).  One pass reads
+// u, v and writes f, g, rhs: 40 B per cell instead of 32 + 24.  Every value is
+// the same expression on the same operands as fg_kernel / rhs_kernel, so the
+// bits are identical.  RHS cells whose F(0, j) / G(i, 0) belong to a neighbour
+// rank (column 1 with a left neighbour, row 1 with a bottom one) are left to
+// rhs_edge_kernel after the f, g exchange (the skeleton's shift()).
+struct FgArgs {
+    double dt, inverseRe, inverseDx, inverseDy, gamma, gx, gy, idx, idy, idt;
+};
+
+// F of one cell (:384-398, :415-416), operands named as in fg_kernel
+__device__ __forceinline__ double f_val(const FgArgs& a, double uc, double ue, double uw,
+                                        double un, double us, double vc, double ve, double vs,
+                                        double vse) {
+    const double inverseDx = a.inverseDx, inverseDy = a.inverseDy, gamma = a.gamma;
+    const double du2dx = inverseDx * 0.25 * ((uc + ue) * (uc + ue) - (uc + uw) * (uc + uw)) +
+                         gamma * inverseDx * 0.25 *
+                             (fabs(uc + ue) * (uc - ue) + fabs(uc + uw) * (uc - uw));
+    const double duvdy = inverseDy * 0.25 * ((vc + ve) * (uc + un) - (vs + vse) * (uc + us)) +
+                         gamma * inverseDy * 0.25 *
+                             (fabs(vc + ve) * (uc - un) + fabs(vs + vse) * (uc - us));
+    const double du2dx2 = inverseDx * inverseDx * (ue - 2.0 * uc + uw);
+    const double du2dy2 = inverseDy * inverseDy * (un - 2.0 * uc + us);
+    return uc + a.dt * (a.inverseRe * (du2dx2 + du2dy2) - du2dx - duvdy + a.gx);
+}
+
+// G of one cell (:400-413, :417-418)
+__device__ __forceinline__ double g_val(const FgArgs& a, const Uv3& S, const Uv3& C,
+                                        const Uv3& N) {
+    const double uc = C.uc, uw = C.um, un = N.uc, unw = N.um;
+    const double vc = C.vc, ve = C.vp, vw = C.vm, vn = N.vc, vs = S.vc;
+    const double inverseDx = a.inverseDx, inverseDy = a.inverseDy, gamma = a.gamma;
+    const double duvdx = inverseDx * 0.25 * ((uc + un) * (vc + ve) - (uw + unw) * (vc + vw)) +
+                         gamma * inverseDx * 0.25 *
+                             (fabs(uc + un) * (vc - ve) + fabs(uw + unw) * (vc - vw));
+    const double dv2dy = inverseDy * 0.25 * ((vc + vn) * (vc + vn) - (vc + vs) * (vc + vs)) +
+                         gamma * inverseDy * 0.25 *
+                             (fabs(vc + vn) * (vc - vn) + fabs(vc + vs) * (vc - vs));
+    const double dv2dx2 = inverseDx * inverseDx * (ve - 2.0 * vc + vw);
+    const double dv2dy2 = inverseDy * inverseDy * (vn - 2.0 * vc + vs);
+    return vc + a.dt * (a.inverseRe * (dv2dx2 + dv2dy2) - duvdx - dv2dy + a.gy);
+}
+
+__global__ __launch_bounds__(kTx* kTy) void fg_rhs_kernel(CLay u, CLay v, Lay f, Lay g, Lay rhs,
+                                                          int ni, int nj, FgArgs a, int wl,
+                                                          int wr, int wb, int wt) {
+    const int i = 1 + blockIdx.x * kTx + threadIdx.x;
+    const int j0 = 1 + (blockIdx.y * kTy + threadIdx.y) * kFgBand;
+    if (i > ni || j0 > nj) return;
+    const int j1 = min(nj, j0 + kFgBand - 1);
+    const bool has_fl = i > 1 || wl;  // F(i-1, j) is local (F(0, j) = U(0, j) on a left wall)
+    Uv3 S, C, N;
+    double gprev;
+    bool has_gp;
+    if (j0 > 1) {  // G(i, j0-1) from one extra row of the march
+        S = load_uv3(u, v, i, j0 - 2);
+        C = load_uv3(u, v, i, j0 - 1);
+        N = load_uv3(u, v, i, j0);
+        gprev = g_val(a, S, C, N);
+        has_gp = true;
+        S = C;
+        C = N;
+        N = load_uv3(u, v, i, j0 + 1);
+    } else {
+        S = load_uv3(u, v, i, 0);
+        C = load_uv3(u, v, i, 1);
+        N = load_uv3(u, v, i, 2);
+        gprev = S.vc;  // G(i, 0) = V(i, 0) on a bottom wall (:434)
+        has_gp = wb != 0;
+    }
+    double uww = i >= 2 ? u(i - 2, j0) : 0.0;  // u(i-2, j) of the current row
+    for (int j = j0; j <= j1; ++j) {
+        Uv3 NN;
+        if (j + 2 <= nj + 1) NN = load_uv3(u, v, i, j + 2);
+        const double uww_n = (i >= 2 && j < j1) ? u(i - 2, j + 1) : 0.0;
+        double fv = f_val(a, C.uc, C.up, C.um, N.uc, S.uc, C.vc, C.vp, S.vc, S.vp);
+        double gv = g_val(a, S, C, N);
+        // boundary of F / G (:426-435) overrides the interior value
+        if (wr && i == ni) fv = C.uc;
+        if (wt && j == nj) gv = C.vc;
+        f(i, j) = fv;
+        g(i, j) = gv;
+        if (wl && i == 1) f(0, j) = C.um;
+        if (wb && j == 1) g(i, 0) = S.vc;
+        if (has_fl && has_gp) {
+            // F(i-1, j): the same expression lane i-1 evaluates (F(0, j) = U(0, j))
+            const double fl = i == 1 ? C.um
+                                     : f_val(a, C.um, C.uc, uww, N.um, S.um, C.vm, C.vc, S.vm,
+                                             S.vc);
+            rhs(i, j) = a.idt * ((fv - fl) * a.idx + (gv - gprev) * a.idy);  // :131-133
+        }
+        gprev = gv;
+        has_gp = true;
+        uww = uww_n;
+        S = C;
+        C = N;
+        N = NN;
+    }
+}
+
+void launch_compute_fg_rhs(const NsLaunch& L, const double* u, const double* v, double* f,
+                           double* g, double* rhs) {
+    const int bands = (L.nj + kFgBand - 1) / kFgBand;
+    dim3 grid((L.ni + kTx - 1) / kTx, (bands + kTy - 1) / kTy);
+    const NsParams& P = L.prm;
+    FgArgs a{P.dt, 1.0 / P.re, 1.0 / P.dx, 1.0 / P.dy, P.gamma, P.gx, P.gy,
+             1.0 / P.dx, 1.0 / P.dy, 1.0 / P.dt};
+    hipLaunchKernelGGL(fg_rhs_kernel, grid, dim3(kTx, kTy), 0, L.s, CLay{u, L.pitch},
+                       CLay{v, L.pitch}, Lay{f, L.pitch}, Lay{g, L.pitch}, Lay{rhs, L.pitch},
+                       L.ni, L.nj, a, L.wall_left, L.wall_right, L.wall_bottom, L.wall_top);
+}
+
+// the RHS cells fg_rhs_kernel leaves to after the f, g exchange: column 1
+// (left neighbour) and row 1 (bottom neighbour); same expression as rhs_kernel
+__global__ void rhs_edge_kernel(CLay f, CLay g, Lay rhs, int ni, int nj, double idx, double idy,
+                                double idt, int wl, int wb) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    int i, j;
+    if (k < nj) {
+        if (wl) return;
+        i = 1;
+        j = 1 + k;
+    } else if (k < nj + ni) {
+        if (wb) return;
+        i = 1 + (k - nj);
+        j = 1;
+    } else {
+        return;
+    }
+    rhs(i, j) = idt * ((f(i, j) - f(i - 1, j)) * idx + (g(i, j) - g(i, j - 1)) * idy);
+}
+
+void launch_rhs_edges(const NsLaunch& L, const double* f, const double* g, double* rhs) {
+    const int n = L.ni + L.nj;
+    hipLaunchKernelGGL(rhs_edge_kernel, dim3((n + 255) / 256), dim3(256), 0, L.s,
+                       CLay{f, L.pitch}, CLay{g, L.pitch}, Lay{rhs, L.pitch}, L.ni, L.nj,
+                       1.0 / L.prm.dx, 1.0 / L.prm.dy, 1.0 / L.prm.dt, L.wall_left,
+                       L.wall_bottom);
+}
+
 // ---- computeRHS, :122-138
 __global__ void rhs_kernel(CLay f, CLay g, Lay rhs, int ni, int nj, double idx, double idy,
                            double idt) {
@@ -317,26 +464,48 @@ __global__ __launch_bounds__(kRedThreads) void adapt_absmax_kernel(CLay f, CLay 
                                                                    double* partials) {
     __shared__ double su[kRedThreads / 64], sv[kRedThreads / 64];
     double mu = 2.2250738585072014e-308, mv = 2.2250738585072014e-308;  // DBL_MIN
+    // kAU columns per thread per trip, their loads issued together (the
+    // stores of one trip would otherwise order the next trip's loads behind
+    // them: one row segment in flight per wave, ~4 TB/s)
+    constexpr int kAU = 4;
     for (int jj = blockIdx.x; jj < R.h; jj += gridDim.x) {
         const int j = R.jlo + jj;
         const bool jin = j >= 1 && j <= nj;
-        for (int ii = threadIdx.x; ii < R.w; ii += kRedThreads) {
-            const int i = R.ilo + ii;
-            double a, b;
-            if (jin && i >= 1 && i <= ni) {
-                const double pc = p(i, j);
-                a = f(i, j) - (p(i + 1, j) - pc) * fx;
-                b = g(i, j) - (p(i, j + 1) - pc) * fy;
-                u(i, j) = a;
-                v(i, j) = b;
-            } else {
-                a = u(i, j);
-                b = v(i, j);
+        for (int i0 = threadIdx.x; i0 < R.w; i0 += kAU * kRedThreads) {
+            double pc[kAU], pe[kAU], pn[kAU], fv[kAU], gv[kAU];
+            bool upd[kAU], inr[kAU];
+#pragma unroll
+            for (int q = 0; q < kAU; ++q) {
+                const int ii = i0 + q * kRedThreads, i = R.ilo + ii;
+                inr[q] = ii < R.w;
+                upd[q] = inr[q] && jin && i >= 1 && i <= ni;
+                if (upd[q]) {
+                    pc[q] = p(i, j);
+                    pe[q] = p(i + 1, j);
+                    pn[q] = p(i, j + 1);
+                    fv[q] = f(i, j);
+                    gv[q] = g(i, j);
+                } else if (inr[q]) {  // physical ghost cell: its unchanged value
+                    fv[q] = u(i, j);
+                    gv[q] = v(i, j);
+                }
             }
-            a = fabs(a);
-            b = fabs(b);
-            mu = (mu > a) ? mu : a;
-            mv = (mv > b) ? mv : b;
+#pragma unroll
+            for (int q = 0; q < kAU; ++q) {
+                if (!inr[q]) continue;
+                const int i = R.ilo + i0 + q * kRedThreads;
+                double a = fv[q], b = gv[q];
+                if (upd[q]) {
+                    a = fv[q] - (pe[q] - pc[q]) * fx;
+                    b = gv[q] - (pn[q] - pc[q]) * fy;
+                    u(i, j) = a;
+                    v(i, j) = b;
+                }
+                a = fabs(a);
+                b = fabs(b);
+                mu = (mu > a) ? mu : a;
+                mv = (mv > b) ? mv : b;
+            }
         }
     }
     mu = wmax(mu);

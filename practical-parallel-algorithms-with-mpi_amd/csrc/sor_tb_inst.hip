@@ -52,7 +52,7 @@ void MISOR_CAT(launch_tb_t, MISOR_TB_T)(hipStream_t s, const SweepParams& prm,
         int grid = prm.nblocks;
         if (queue) {
             (void)hipMemsetAsync(queue, 0, 8 * sizeof(int), s);
-            grid = std::min(grid, resident);
+            grid = std::min(grid, std::max(8, resident - prm.reserve));
         }
         hipLaunchKernelGGL(kernel, dim3(grid), dim3(threads), 0, s, prm, src, dst, rhs, partials,
                            st, force, queue);

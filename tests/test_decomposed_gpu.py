@@ -69,7 +69,7 @@ def assemble(parts, shape):
                                         (4, (1, 4)), (6, (0, 0)), (8, (0, 0))])
 @pytest.mark.parametrize("ni,nj,k", [(61, 43, 5), (300, 257, 3), (2100, 90, 2)])
 @pytest.mark.parametrize("overlap", [1, 0], ids=["overlap", "serial"])
-@pytest.mark.parametrize("T", [1, 2, 4, 6, 7], ids=["t1", "t2", "t4", "t6", "t7"])
+@pytest.mark.parametrize("T", [1, 2, 4, 6, 7, 8], ids=["t1", "t2", "t4", "t6", "t7", "t8"])
 def test_fixed_sweeps_partition_independent(world, dims, ni, nj, k, overlap, T):
     rng = np.random.default_rng(ni + 31 * nj + world)
     p = rng.standard_normal((nj + 2, ni + 2))
@@ -245,3 +245,34 @@ def test_rccl_single_rank_pipelined_fixed_sweeps():
             assert it == k == it_ref
             assert abs(res - res_ref) <= 1e-12 * res_ref
             assert np.array_equal(g.download(M.P), want)
+
+
+@pytest.mark.parametrize("reserve", [0, 16, 500, 1 << 20])
+def test_pipelined_reserve(reserve):
+    """the pipelined loop's persistent interior launch leaves `reserve` of its
+    workgroup slots to the other streams (misor_api.hip, SweepParams.reserve;
+    at least 8 workgroups remain, so 2^20 runs the whole pass on 8 queue
+    workers): p stays bit-identical over several passes and a remainder pass"""
+    world, ni, nj, k, T = 4, 900, 700, 19, 4
+    rng = np.random.default_rng(reserve % 1000 + 5)
+    p = rng.standard_normal((nj + 2, ni + 2))
+    rhs = rng.standard_normal((nj + 2, ni + 2)) * 20
+    dx, dy = 1.0 / ni, 1.0 / nj
+    want = p.copy()
+    orc.solve_rb(want, rhs, dx, dy, 1.7, 1e-300, k)
+
+    def rank_fn(r, cid, dims):
+        with M.Grid(ni, nj, dx, dy, 1.7, 1e-300, k, device=0, nranks=world, rank=r,
+                    dims=dims, comm_id=cid) as g:
+            g.set_tuning(M.TUNE_TSTEPS, T)
+            g.set_tuning(M.TUNE_TB_RESERVE, reserve)
+            assert g.get_tuning(M.TUNE_TB_RESERVE) == reserve
+            g.upload(M.P, local_window(p, g.loc))
+            g.upload(M.RHS, local_window(rhs, g.loc))
+            it, _ = g.solve_rb()
+            return g.loc, g.download(M.P), it
+
+    outs = run_ranks(world, rank_fn)
+    assert all(o[2] == k for o in outs)
+    got = assemble([(o[0], o[1]) for o in outs], p.shape)
+    assert np.array_equal(got, want), np.argwhere(got != want)[:5]

@@ -78,10 +78,15 @@ def test_boundary_conditions_bitwise(golden, name, lr, bt):
     g.close()
 
 
-@pytest.mark.parametrize("ni,nj", [(37, 23), (128, 128), (200, 50), (513, 70)])
-def test_fg_rhs_adapt_bitwise(golden, ni, nj):
+@pytest.mark.parametrize("fuse", [1, 0])
+@pytest.mark.parametrize("ni,nj", [(37, 23), (128, 128), (200, 50), (513, 70), (126, 65)])
+def test_fg_rhs_adapt_bitwise(golden, ni, nj, fuse):
+    """fuse=1: computeFG's column march also writes RHS (ns_kernels.hip
+    fg_rhs_kernel; 126 = 2 x 63 columns: the waves' shifted column ranges end
+    exactly on ni); fuse=0: the separate computeRHS kernel"""
     prm = par(golden, "a6_canal.par", imax=ni, jmax=nj)
     ns, g = load_both(prm, random_state(prm, ni + nj), 0.0137)
+    g.set_tuning(M.TUNE_NS_FUSE, fuse)
     ns.call("compute_fg")
     g.call("compute_fg")
     assert_fields(ns, g, ("f", "g", "u", "v"))
@@ -92,6 +97,74 @@ def test_fg_rhs_adapt_bitwise(golden, ni, nj):
     g.call("adapt_uv")
     assert_fields(ns, g, ("u", "v"))
     g.close()
+
+
+@pytest.mark.parametrize("change", ["dt", "upload_f", "upload_rhs", "none"])
+def test_fused_rhs_invalidated(golden, change):
+    """the RHS the fused computeFG left behind is used by computeRHS only when
+    f, g, rhs and dt are unchanged since; otherwise computeRHS recomputes it"""
+    prm = par(golden, "a6_dcavity.par", imax=70, jmax=45)
+    st = random_state(prm, 11)
+    ns, g = load_both(prm, st, 0.011)
+    ns.call("compute_fg")
+    g.call("compute_fg")
+    rng = np.random.default_rng(5)
+    if change == "dt":
+        ns.s.dt = 0.017
+        g.set_dt(0.017)
+    elif change == "upload_f":
+        ns.f[...] = rng.standard_normal(ns.f.shape)
+        g.upload(M.F, ns.f)
+    elif change == "upload_rhs":
+        ns.rhs[...] = rng.standard_normal(ns.rhs.shape)
+        g.upload(M.RHS, ns.rhs)
+    ns.call("compute_rhs")
+    g.call("compute_rhs")
+    assert_fields(ns, g, ("rhs", "f", "g"))
+    g.close()
+
+
+@pytest.mark.parametrize("nranks", [2, 3, 4])
+def test_fg_rhs_decomposed_bitwise(golden, nranks):
+    """one computeFG + computeRHS on N ranks (LOCAL transport): the fused march
+    leaves column 1 / row 1 next to a neighbour to computeRHS after the f, g
+    exchange; the assembled f, g, rhs equal the oracle's bit for bit"""
+    prm = par(golden, "a6_canal.par", imax=131, jmax=77)
+    st = random_state(prm, 21)
+    ns = orc.NS(prm)
+    for k, _ in FIELDS:
+        getattr(ns, k)[...] = st[k]
+    ns.s.dt = 0.0123
+    ns.call("compute_fg")
+    ns.call("compute_rhs")
+    out, errs = [None] * nranks, []
+    cid = ("LOCAL:fgrhs%d" % nranks).encode()
+
+    def body(r):
+        try:
+            g = D.ns_grid(prm, nranks=nranks, rank=r, comm_id=cid)
+            loc = g.loc
+            for k, fid in FIELDS:
+                g.upload(fid, st[k][loc.joff:loc.joff + loc.nj + 2, loc.ioff:loc.ioff + loc.ni + 2])
+            g.set_dt(0.0123)
+            g.call("compute_fg")
+            g.call("compute_rhs")
+            out[r] = (loc, {k: g.download(fid) for k, fid in FIELDS if k in ("f", "g", "rhs")})
+            g.close()
+        except BaseException as e:
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(nranks)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(300)
+    assert not errs, errs
+    for loc, f in out:
+        sl = np.s_[loc.joff + 1:loc.joff + loc.nj + 1, loc.ioff + 1:loc.ioff + loc.ni + 1]
+        for k in ("f", "g", "rhs"):
+            got = f[k][1:loc.nj + 1, 1:loc.ni + 1]
+            assert np.array_equal(got, getattr(ns, k)[sl]), (k, loc.ioff, loc.joff)
 
 
 def test_timestep_and_normalize(golden):

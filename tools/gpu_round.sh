@@ -4,7 +4,7 @@ set -e
 export TMPDIR=/tmp
 tag=$1; shift
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread \
+timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 170 --timeout-method thread \
     > gpurun_out/gpu_tests_$tag.log 2>&1
 bash tools/profile_bench.sh $tag
 timeout -k 10 300 python tools/scale_proxy.py --comm --tsteps 7,8 --rows 0 --rounds 2 --sweeps 48 \

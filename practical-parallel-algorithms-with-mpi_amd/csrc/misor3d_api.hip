@@ -87,12 +87,14 @@ struct misor_grid3 {
     int sweep = 1;             // MISOR3_TUNE_SWEEP
     int rows = 8;              // MISOR3_TUNE_ROWS
     int kchunk = 0;            // MISOR3_TUNE_KCHUNK (0: automatic)
+    int fold = 0;              // MISOR3_TUNE_FOLD: single rank, loop test inside the sweep
     double dx = 0, dy = 0, dz = 0, dt = 0, dt_bound = 0;
     double* partials = nullptr;  // per-block partial sums / maxima
     long long partials_cap = 0;
     double* out = nullptr;      // 4 doubles on the device (maxima / sum)
     double* out_host = nullptr; // pinned
     DevState* st = nullptr;
+    DevState* st2 = nullptr;  // the folded loop test's second state buffer
     DevState* st_host = nullptr;
     int last_iters = 0;
     bool timing = false;          // misor3_enable_timing
@@ -219,6 +221,7 @@ void misor3_destroy(misor_grid3* g) {
     (void)hipFree(g->out);
     (void)hipHostFree(g->out_host);
     (void)hipFree(g->st);
+    (void)hipFree(g->st2);
     (void)hipHostFree(g->st_host);
     (void)hipFree(g->gstage);
     for (auto& e : g->ev)
@@ -307,11 +310,14 @@ int misor3_create(misor_grid3** out, const misor3_desc* d) {
     g->partials_cap = 2LL * ns3_partials(g->g);
     if (g->partials_cap < 3LL * absmax3_blocks()) g->partials_cap = 3LL * absmax3_blocks();
     // the fused sweep's partials: the smallest rows / kchunk settings
-    if (g->partials_cap < sweep3_blocks(g->g, 4, 4)) g->partials_cap = sweep3_blocks(g->g, 4, 4);
+    // (two sets: the folded loop test reads the previous sweep's partials)
+    if (g->partials_cap < 2LL * sweep3_blocks(g->g, 4, 4))
+        g->partials_cap = 2LL * sweep3_blocks(g->g, 4, 4);
     if (hipMalloc(&g->partials, sizeof(double) * (size_t)g->partials_cap) != hipSuccess ||
         hipMalloc(&g->out, sizeof(double) * 4) != hipSuccess ||
         hipHostMalloc(&g->out_host, sizeof(double) * 4, hipHostMallocDefault) != hipSuccess ||
         hipMalloc(&g->st, sizeof(DevState)) != hipSuccess ||
+        hipMalloc(&g->st2, sizeof(DevState)) != hipSuccess ||
         hipHostMalloc(&g->st_host, sizeof(DevState), hipHostMallocDefault) != hipSuccess)
         CF(MISOR_ENOMEM, "allocation failed");
     if (nranks > 1) {
@@ -632,6 +638,14 @@ int misor3_solve(misor_grid3* g, int* iters, double* res) {
     const bool fused = g->sweep != 0;
     if (!fused && dist(g)) return fail3(MISOR_ESTATE, "the two-pass solve is single-rank only");
     const int kc = g->kchunk > 0 ? g->kchunk : auto_kchunk(g->g, g->rows);
+    // single rank: the loop test of sweep m runs inside sweep m+1 (k3_sweep,
+    // Fold3); the state alternates between st and st2, the partials between
+    // the two halves of g->partials
+    const bool fold = fused && !dist(g) && g->fold;
+    DevState* const stb[2] = {g->st, g->st2};
+    const long long half = g->partials_cap / 2;
+    double* const part[2] = {g->partials, g->partials + half};
+    int sx = 0;  // the state buffer that holds the current state
     *g->st_host = s0;
     if (g->timing) HIPCHK3(hipEventRecord(g->ev[0], g->stream));
     HIPCHK3(hipMemcpyAsync(g->st, g->st_host, sizeof(DevState), hipMemcpyHostToDevice,
@@ -656,6 +670,14 @@ int misor3_solve(misor_grid3* g, int* iters, double* res) {
         if (batch < 1) batch = 1;
         for (int b = 0; b < batch; ++b) {
             const long long m = launched + b;
+            if (fold) {
+                launch3_sweep_folded(g->stream, g->g, buf[m & 1], buf[(m + 1) & 1],
+                                     g->fld[MISOR3_RHS], 1.0 / dx2, 1.0 / dy2, 1.0 / dz2, factor,
+                                     g->rows, kc, part[m & 1], b == 0 ? nullptr : part[(m - 1) & 1],
+                                     stb[sx], stb[sx ^ 1], cells);
+                sx ^= 1;
+                continue;
+            }
             if (!fused) {
                 launch3_rb_iteration(g->stream, g->g, g->fld[MISOR3_P], g->fld[MISOR3_RHS],
                                      1.0 / dx2, 1.0 / dy2, 1.0 / dz2, factor, g->partials,
@@ -674,10 +696,15 @@ int misor3_solve(misor_grid3* g, int* iters, double* res) {
                 if ((rc = exchange3(g, nb, kHalo)) != MISOR_OK) return rc;
             }
         }
+        if (fold) {  // the loop test of the batch's last sweep
+            launch3_fold_decide(g->stream, g->g, g->rows, kc, part[(launched + batch - 1) & 1],
+                                stb[sx], stb[sx ^ 1], cells);
+            sx ^= 1;
+        }
         HIPCHK3(hipGetLastError());
         launched += batch;
         if (g->timing) HIPCHK3(hipEventRecord(g->ev[1], g->stream));
-        HIPCHK3(hipMemcpyAsync(g->st_host, g->st, sizeof(DevState), hipMemcpyDeviceToHost,
+        HIPCHK3(hipMemcpyAsync(g->st_host, stb[sx], sizeof(DevState), hipMemcpyDeviceToHost,
                                g->stream));
         HIPCHK3(hipStreamSynchronize(g->stream));
         if (g->st_host->done || launched >= d.itermax) break;
@@ -718,6 +745,7 @@ int misor3_set_tuning(misor_grid3* g, int key, int value) {
         if (value != 0 && value < 4) return fail3(MISOR_EINVAL, "kchunk must be 0 or >= 4");
         g->kchunk = value;
         return MISOR_OK;
+    case MISOR3_TUNE_FOLD: g->fold = value != 0; return MISOR_OK;
     }
     return fail3(MISOR_EINVAL, "unknown tuning key %d", key);
 }
@@ -730,6 +758,7 @@ int misor3_get_tuning(const misor_grid3* g, int key, int* value) {
     case MISOR3_TUNE_KCHUNK:
         *value = g->kchunk > 0 ? g->kchunk : auto_kchunk(g->g, g->rows);
         return MISOR_OK;
+    case MISOR3_TUNE_FOLD: *value = g->fold; return MISOR_OK;
     }
     return fail3(MISOR_EINVAL, "unknown tuning key %d", key);
 }

@@ -590,39 +590,42 @@ static int pick_tb_rows(int ni, int nj, int T, int variant) {
     return on_ring(h);
 }
 
-// geometry of the temporally blocked pass with T iterations into `tp`: the
-// block height of that T (an explicit MISOR_TUNE_TB_ROWS request for every T),
-// block rows, block columns
+// geometry of the temporally blocked pass with T iterations into `tp`: block
+// columns and block rows.  Automatic geometry (no MISOR_TUNE_TB_ROWS request):
+// blocks of pick_tb_rows' height H, then about two resident rounds of short
+// ones (~32 rows) -- the work order takes them last, so the pass ends on
+// blocks a sixth as long (the makespan of a persistent pass runs ~half a
+// block past its average), at the cost of their extra halo rows -- and a last
+// block row of one to two short-block heights (the rest; round 1 left up to H
+// rows there, a long row-tested block at the very end of the order).
+// (tools/scale_proxy.py, profiles/r02_small_rows.txt: the short band took one
+// rank's 8192 x 16384 at 8 GPUs from 0.149 to 0.118 ms per iteration.)  A
+// three-level form -- the bulk in 576-row blocks, one round of H, then the
+// short band -- ran up to 1.7x slower on the small grids (the tall blocks
+// hold their slots for a whole pass; profiles/r02_tb_levels.txt) and was
+// dropped.  An explicit request gives uniform blocks of that height, the last
+// row taking the rest.
 static void tb_geometry(const misor_grid* g, int T, SweepParams& tp) {
     const int nj = g->loc.nj, req = g->tb_rows_req;
+    tp.nbx = tb_nbx(g->loc.ni, T, tp.variant);
+    const int S = tb_ring_slots(T, tp.variant);
     int h = req > 0 ? req : pick_tb_rows(g->loc.ni, nj, T, tp.variant);
     if (h > nj) h = nj;
-    tp.rows_per_block = h;
-    tp.nbx = tb_nbx(g->loc.ni, T, tp.variant);
-    // block rows: H tall, then (automatic geometry) about one resident round of
-    // short ones -- the work order takes them last, so the pass ends on blocks
-    // about a quarter as long (the makespan of a pass runs ~half a block past
-    // its average), at the cost of their extra halo rows -- and the last row
-    // takes the rest (at most H rows)
-    // (tools/scale_proxy.py, profiles/r02_small_rows.txt: 32-row blocks for two
-    // resident rounds; one rank's 8192 x 16384 at 8 GPUs 0.149 -> 0.118 ms per
-    // iteration, 32768^2 unchanged)
-    const int S = tb_ring_slots(T, tp.variant);
     const int hs = S * std::max(1, (kTbSmallRows + S / 2) / S);
-    int nsmall = 0;
-    if (req <= 0 && hs < h) {
-        const int round_rows =
-            (kTbSmallRounds * tb_resident(T, tp.variant) + tp.nbx - 1) / tp.nbx;
-        nsmall = std::min(round_rows, nj / 4 / hs);
+    int nbig = 0, ns = 0;
+    if (req > 0 || hs >= h || nj < 4 * hs) {  // uniform blocks, the last takes the rest
+        nbig = nj / h;
+        if (nbig * h == nj && nbig > 0) --nbig;
+    } else {
+        const int band = std::min(
+            (kTbSmallRounds * tb_resident(T, tp.variant) + tp.nbx - 1) / tp.nbx, nj / 4 / hs);
+        nbig = std::max(0, (nj - band * hs - hs) / h);
+        ns = std::max(0, (nj - nbig * h) / hs - 1);  // the last row: [hs, 2 hs)
     }
-    const int big_rows = nj - nsmall * hs;
-    int nbig = big_rows / h;
-    if (nbig * h == big_rows && nbig > 0) --nbig;  // the last row keeps >= 1 row
-    if (nsmall > 0 && nbig * h + nsmall * hs >= nj) --nsmall;
-    if (nsmall < 0) nsmall = 0;
+    tp.rows_per_block = h;
     tp.nby_big = nbig;
     tp.h_small = hs;
-    tp.nby = nbig + nsmall + 1;
+    tp.nby = nbig + ns + 1;
     tp.nblocks = tp.nbx * tp.nby;
 }
 

@@ -114,7 +114,7 @@ struct SweepParams {
     int ni, nj;          // local interior size
     int rows_per_block;  // H (temporally blocked: block rows 0 .. nby_big-1 are H tall)
     int nby;             // temporally blocked: block rows; rows nby_big .. nby-2 are
-                         // h_small tall, the last one takes the rest
+                         // h_small tall, the last one takes the rest (tb_geometry)
     int nby_big, h_small;
     int parity;          // (ioff + joff) & 1 : global colour of local cell (0,0)
     int ghost_left, ghost_right, ghost_bottom, ghost_top;  // physical boundary -> Neumann copy
@@ -295,5 +295,17 @@ void launch3_sub_mean(hipStream_t s, const G3& g, double* p, const double* sum, 
 // the loop test of a decomposed solve: st->sum[0] holds the all-reduced sum
 // of r^2 of the iteration (written by launch3_sweep with sum_only)
 void launch3_decide(hipStream_t s, DevState* st, double cells);
+// single rank, the loop test folded into the sweep: the sweep first applies
+// the test of the previous sweep (prev_partials; nullptr: none) to st_in,
+// workgroup 0 writes the result to st_out, and the launch is a no-op once the
+// loop is over; launch3_fold_decide applies the test of a batch's last sweep
+void launch3_sweep_folded(hipStream_t s, const G3& g, const double* src, double* dst,
+                          const double* rhs, double idx2, double idy2, double idz2,
+                          double factor, int rows, int kc, double* partials,
+                          const double* prev_partials, const DevState* st_in, DevState* st_out,
+                          double cells);
+void launch3_fold_decide(hipStream_t s, const G3& g, int rows, int kc,
+                         const double* prev_partials, const DevState* st_in, DevState* st_out,
+                         double cells);
 
 }  // namespace misor

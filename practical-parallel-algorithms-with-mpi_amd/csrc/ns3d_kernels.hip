@@ -165,6 +165,66 @@ __global__ void k3_decide(DevState* st, double cells) {
     st->done = !((res >= st->epssq) && (it < st->itermax));
 }
 
+// Folded loop test (single rank).  Instead of a k3_finish launch after every
+// sweep, sweep launch b of a batch first completes the loop test of sweep
+// b-1 from its per-workgroup partials -- every workgroup redundantly, in
+// k3_finish's exact order (1024 strided sums, then the same tree), so all
+// agree bit for bit -- and returns at once if the loop is over.  The state is
+// double-buffered (launch b reads in, workgroup 0 writes out; the next launch
+// swaps them) so no workgroup reads a state another one of the same launch is
+// writing.  k3_fold_decide applies the last test of a batch.  One launch per
+// iteration instead of two.
+struct Fold3 {
+    const double* prev;   // partials of the previous sweep (nullptr: no test, copy the state)
+    int prev_nb;
+    const DevState* in;
+    DevState* out;
+    double cells;
+};
+
+// the loop test of one sweep; scratch: 1024 doubles of LDS; every thread of
+// the (256-thread) workgroup returns the new state's done flag
+__device__ __forceinline__ int fold_test(const Fold3& F, double* scratch, DevState& s) {
+    const int t = threadIdx.y * blockDim.x + threadIdx.x;
+    s = *F.in;
+    if (!s.done && F.prev) {
+        // k3_finish's order with 1024 virtual threads v = t + 256 m
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const int vt = t + 256 * m;
+            double x = 0.0;
+            for (int q = vt; q < F.prev_nb; q += 1024) x += F.prev[q];
+            scratch[vt] = x;
+        }
+        __syncthreads();
+        scratch[t] += scratch[t + 512];  // w = 512: virtual threads t and t + 256
+        scratch[t + 256] += scratch[t + 768];
+        __syncthreads();
+        for (int w = 256; w >= 64; w >>= 1) {
+            if (t < w) scratch[t] += scratch[t + w];
+            __syncthreads();
+        }
+        if (t < 64) {
+            const double v = wave_sum(scratch[t]);
+            if (t == 0) scratch[1024] = v;
+        }
+        __syncthreads();
+        const double res = (s.res + scratch[1024]) / F.cells;
+        const int it = s.it + 1;
+        s.res = res;
+        s.it = it;
+        s.done = !((res >= s.epssq) && (it < s.itermax));
+    }
+    if (blockIdx.x == 0 && t == 0) *F.out = s;
+    return s.done;
+}
+
+__global__ __launch_bounds__(256) void k3_fold_decide(Fold3 F) {
+    __shared__ double scratch[1025];
+    DevState s;
+    (void)fold_test(F, scratch, s);
+}
+
 // ------------------------------------------------- fused red-black sweep
 // One launch = one whole solve iteration (red of every cell, then black),
 // read from `src`, written to `dst` (ping-pong: blocks never see another
@@ -247,15 +307,16 @@ __global__ __launch_bounds__(256) void k3_sweep(G3 g, const double* __restrict__
                                                 double idy2, double idz2, double factor,
                                                 int nstrips, int nrowb, int kc,
                                                 double* __restrict__ partials,
-                                                const DevState* __restrict__ st) {
+                                                const DevState* __restrict__ st, Fold3 F) {
     constexpr int NR = R + 4;  // rows per plane in LDS
     static_assert(R % 4 == 0, "R must be a multiple of 4");
     constexpr int LR = NR / 4;           // rows each wave loads
     constexpr int RR = (R + 2 + 3) / 4;  // update rows per wave (LDS rows 1..R+2)
     constexpr int PL = NR * kSwRow;      // doubles per LDS plane
+    static_assert(kSwSlots * PL >= 1025, "the folded loop test uses the plane ring as scratch");
     __shared__ double L[kSwSlots * PL];
     __shared__ double sh[4];
-    if (st->done) return;
+    if (!F.in && st->done) return;
 
     // XCD-aware order: the hardware deals workgroups round-robin to the 8 XCDs
     // (each with its own L2); give XCD x a contiguous run of tiles so that
@@ -427,19 +488,32 @@ __global__ __launch_bounds__(256) void k3_sweep(G3 g, const double* __restrict__
         store_plane(k + 2, pl_out);
     };
 
-    // preload planes k0-2 .. k0 into LDS, plane k0+1 into registers
-    {
-        D2 v[LR];
-        for (int kk = k0 - 2; kk <= k0; ++kk) {
-            load_plane(kk, v);
-            store_plane(kk, v);
-        }
-    }
+    // preload planes k0-2 .. k0 (into LDS) and k0+1 (registers) and the first
+    // rhs pairs: all loads issued together, so the march starts after one
+    // memory latency instead of three
+    D2 v0[LR], v1[LR], v2[LR];
+    // (loads one step ahead of use; a variant with p three and rhs two steps
+    // ahead -- 4 + 4 register sets -- ran 1.6-1.7x slower at 128^3 and 384^3,
+    // profiles/r02_tune3d_depth.txt)
     D2 pl[2][LR];
     D2 rs[3][RR];  // rhs pairs of three consecutive planes, rotating
+    load_plane(k0 - 2, v0);
+    load_plane(k0 - 1, v1);
+    load_plane(k0, v2);
     load_plane(k0 + 1, pl[0]);
     load_rhs(k0 - 2, rs[2]);
     load_rhs(k0 - 1, rs[0]);
+    if (F.in) {
+        // folded loop test (single rank): its partial-sum loads queue behind
+        // the preloads, so it costs the LDS tree, not another memory latency;
+        // L is free until the planes are stored
+        DevState s;
+        if (fold_test(F, L, s)) return;  // uniform: every thread reads the same state
+        __syncthreads();                 // scratch reads done before the planes land
+    }
+    store_plane(k0 - 2, v0);
+    store_plane(k0 - 1, v1);
+    store_plane(k0, v2);
     // step k uses the pairs of planes k (red) and k-1 (black) and loads k+1;
     // with k = k0-1+3n+u the three sets rotate with period 3, the planes with
     // period 2: unroll by 6
@@ -718,28 +792,50 @@ int sweep3_blocks(const G3& g, int rows, int kc) {
     return (int)(nstr * nrb * nkc);
 }
 
+static void sweep3_kernel(hipStream_t s, const G3& g, const double* src, double* dst,
+                          const double* rhs, double idx2, double idy2, double idz2,
+                          double factor, int rows, int kc, double* partials,
+                          const DevState* st, const Fold3& F) {
+    const int nstr = (g.I + kSwOwn - 1) / kSwOwn, nrb = (g.J + rows - 1) / rows;
+    const int nb = sweep3_blocks(g, rows, kc);
+#define K3SW(RR_)                                                                           \
+    hipLaunchKernelGGL(k3_sweep<RR_>, dim3(nb), dim3(256), 0, s, g, src, dst, rhs, idx2, idy2, \
+                       idz2, factor, nstr, nrb, kc, partials, st, F)
+    switch (rows) {
+    case 4: K3SW(4); break;
+    case 12: K3SW(12); break;
+    default: K3SW(8); break;
+    }
+#undef K3SW
+}
+
 int launch3_sweep(hipStream_t s, const G3& g, const double* src, double* dst, const double* rhs,
                   double idx2, double idy2, double idz2, double factor, int rows, int kc,
                   double* partials, DevState* st, double cells, bool sum_only) {
-    const int nstr = (g.I + kSwOwn - 1) / kSwOwn, nrb = (g.J + rows - 1) / rows;
     const int nb = sweep3_blocks(g, rows, kc);
-    switch (rows) {
-    case 4:
-        hipLaunchKernelGGL(k3_sweep<4>, dim3(nb), dim3(256), 0, s, g, src, dst, rhs, idx2, idy2,
-                           idz2, factor, nstr, nrb, kc, partials, st);
-        break;
-    case 12:
-        hipLaunchKernelGGL(k3_sweep<12>, dim3(nb), dim3(256), 0, s, g, src, dst, rhs, idx2, idy2,
-                           idz2, factor, nstr, nrb, kc, partials, st);
-        break;
-    default:
-        hipLaunchKernelGGL(k3_sweep<8>, dim3(nb), dim3(256), 0, s, g, src, dst, rhs, idx2, idy2,
-                           idz2, factor, nstr, nrb, kc, partials, st);
-        break;
-    }
+    sweep3_kernel(s, g, src, dst, rhs, idx2, idy2, idz2, factor, rows, kc, partials, st,
+                  Fold3{nullptr, 0, nullptr, nullptr, cells});
     hipLaunchKernelGGL(k3_finish, dim3(1), dim3(1024), 0, s, partials, nb, 1, st, cells,
                        sum_only ? 1 : 0);
     return nb;
+}
+
+void launch3_sweep_folded(hipStream_t s, const G3& g, const double* src, double* dst,
+                          const double* rhs, double idx2, double idy2, double idz2,
+                          double factor, int rows, int kc, double* partials,
+                          const double* prev_partials, const DevState* st_in, DevState* st_out,
+                          double cells) {
+    const int nb = sweep3_blocks(g, rows, kc);
+    sweep3_kernel(s, g, src, dst, rhs, idx2, idy2, idz2, factor, rows, kc, partials, st_in,
+                  Fold3{prev_partials, nb, st_in, st_out, cells});
+}
+
+void launch3_fold_decide(hipStream_t s, const G3& g, int rows, int kc,
+                         const double* prev_partials, const DevState* st_in, DevState* st_out,
+                         double cells) {
+    const int nb = sweep3_blocks(g, rows, kc);
+    hipLaunchKernelGGL(k3_fold_decide, dim3(1), dim3(256), 0, s,
+                       Fold3{prev_partials, nb, st_in, st_out, cells});
 }
 
 void launch3_decide(hipStream_t s, DevState* st, double cells) {

@@ -452,60 +452,70 @@ void launch_absmax2(const NsLaunch& L, const double* u, const double* v, double*
 // adaptUV (:438-455) fused with the maxElement partials of the NEXT step's
 // computeTimestep (:193-234): the reference's main loop changes no u, v
 // between adaptUV and computeTimestep (main.c:43-60), so the maxima of the
-// fields adaptUV leaves are the ones computeTimestep needs.  The walk is
-// absmax2_kernel's (rows over blocks, columns over threads, over the cells
-// the reduction visits); cells inside [1, ni] x [1, nj] get adaptUV's update
-// and contribute their new value, the physical ghost cells their unchanged
-// one.  One pass over f, g, p -> u, v instead of that pass plus a 16-B/cell
-// re-read of u, v (misor_api.hip misor_adapt_uv / misor_max_uv).
+// fields adaptUV leaves are the ones computeTimestep needs.  One pass over
+// f, g, p -> u, v instead of that pass plus a 16-B/cell re-read of u, v
+// (misor_api.hip misor_adapt_uv / misor_max_uv).
+//
+// Walk: tiles of kRedThreads columns x kAH rows in row-major order, a
+// workgroup takes every gridDim-th tile, so the workgroups running at any time
+// cover one compact stretch of rows (like a one-thread-per-cell launch; the
+// row-strided walk of absmax2_kernel writes 1024 scattered rows at once and
+// ran adaptUV at ~4 TB/s).  A thread loads its column's kAH rows of f, g,
+// p(i+1) and kAH+1 rows of p at once, then updates and stores them.  Cells
+// inside [1, ni] x [1, nj] get adaptUV's update and contribute their new
+// value, the physical ghost cells of the reduction region their unchanged
+// one.  One partial per workgroup (max: order-free, exact).
+constexpr int kAH = 8;
+
 __global__ __launch_bounds__(kRedThreads) void adapt_absmax_kernel(CLay f, CLay g, CLay p, Lay u,
                                                                    Lay v, int ni, int nj,
                                                                    double fx, double fy, Region R,
                                                                    double* partials) {
     __shared__ double su[kRedThreads / 64], sv[kRedThreads / 64];
     double mu = 2.2250738585072014e-308, mv = 2.2250738585072014e-308;  // DBL_MIN
-    // kAU columns per thread per trip, their loads issued together (the
-    // stores of one trip would otherwise order the next trip's loads behind
-    // them: one row segment in flight per wave, ~4 TB/s)
-    constexpr int kAU = 4;
-    for (int jj = blockIdx.x; jj < R.h; jj += gridDim.x) {
-        const int j = R.jlo + jj;
-        const bool jin = j >= 1 && j <= nj;
-        for (int i0 = threadIdx.x; i0 < R.w; i0 += kAU * kRedThreads) {
-            double pc[kAU], pe[kAU], pn[kAU], fv[kAU], gv[kAU];
-            bool upd[kAU], inr[kAU];
+    const int ntx = (R.w + kRedThreads - 1) / kRedThreads, nty = (R.h + kAH - 1) / kAH;
+    for (int t = blockIdx.x; t < ntx * nty; t += gridDim.x) {
+        const int ii = (t % ntx) * kRedThreads + (int)threadIdx.x, jj0 = (t / ntx) * kAH;
+        if (ii >= R.w) continue;
+        const int i = R.ilo + ii;
+        const bool icol = i >= 1 && i <= ni;
+        double pc[kAH + 1], pe[kAH], fv[kAH], gv[kAH];
 #pragma unroll
-            for (int q = 0; q < kAU; ++q) {
-                const int ii = i0 + q * kRedThreads, i = R.ilo + ii;
-                inr[q] = ii < R.w;
-                upd[q] = inr[q] && jin && i >= 1 && i <= ni;
-                if (upd[q]) {
+        for (int q = 0; q < kAH; ++q) {
+            const int j = R.jlo + jj0 + q;
+            if (jj0 + q < R.h) {
+                if (icol && j >= 1 && j <= nj) {
                     pc[q] = p(i, j);
                     pe[q] = p(i + 1, j);
-                    pn[q] = p(i, j + 1);
                     fv[q] = f(i, j);
                     gv[q] = g(i, j);
-                } else if (inr[q]) {  // physical ghost cell: its unchanged value
+                } else {  // a physical ghost cell: its unchanged value
                     fv[q] = u(i, j);
                     gv[q] = v(i, j);
                 }
             }
+        }
+        {
+            const int j = R.jlo + jj0 + kAH;  // p(i, j+1) of the tile's last row
+            if (icol && jj0 + kAH - 1 < R.h && j - 1 >= 1 && j - 1 <= nj) pc[kAH] = p(i, j);
+        }
 #pragma unroll
-            for (int q = 0; q < kAU; ++q) {
-                if (!inr[q]) continue;
-                const int i = R.ilo + i0 + q * kRedThreads;
-                double a = fv[q], b = gv[q];
-                if (upd[q]) {
-                    a = fv[q] - (pe[q] - pc[q]) * fx;
-                    b = gv[q] - (pn[q] - pc[q]) * fy;
-                    u(i, j) = a;
-                    v(i, j) = b;
-                }
-                a = fabs(a);
-                b = fabs(b);
-                mu = (mu > a) ? mu : a;
-                mv = (mv > b) ? mv : b;
+        for (int q = 0; q < kAH; ++q) {
+            const int j = R.jlo + jj0 + q;
+            if (jj0 + q >= R.h) break;
+            double a = fv[q], b = gv[q];
+            if (icol && j >= 1 && j <= nj) {
+                const double pn = q + 1 < kAH ? ((j + 1 <= nj) ? pc[q + 1] : p(i, j + 1))
+                                              : pc[kAH];
+                a = fv[q] - (pe[q] - pc[q]) * fx;  // :447-452
+                b = gv[q] - (pn - pc[q]) * fy;
+                u(i, j) = a;
+                v(i, j) = b;
             }
+            a = fabs(a);
+            b = fabs(b);
+            mu = (mu > a) ? mu : a;
+            mv = (mv > b) ? mv : b;
         }
     }
     mu = wmax(mu);

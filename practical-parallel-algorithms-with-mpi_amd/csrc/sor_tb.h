@@ -581,6 +581,7 @@ __device__ __forceinline__ void tb_strip2(const SweepParams& prm, const double* 
 
 // block rows: nby_big of H = rows_per_block rows, then h_small-row ones
 // (short blocks, which the work order takes last), the last takes the rest
+// (misor_api.hip tb_geometry)
 __device__ __forceinline__ void block_rows(const SweepParams& prm, int by, int& j0, int& j1) {
     const int H = prm.rows_per_block;
     j0 = by < prm.nby_big ? 1 + by * H : 1 + prm.nby_big * H + (by - prm.nby_big) * prm.h_small;

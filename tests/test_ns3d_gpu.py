@@ -47,10 +47,20 @@ def random_state(shape, seed):
     return st
 
 
-# 3D solve variants (sweep, rows, kchunk): the fused k-march sweep with the
-# default and odd geometries (chunk boundaries inside the grid), and the
-# two colour-pass form
-SOLVE_TUNES = [(1, 8, 0), (1, 4, 4), (1, 12, 5), (1, 8, 3 + 4), (0, 8, 0)]
+# 3D solve variants (sweep, rows, kchunk[, fold]): the fused k-march sweep with
+# the default and odd geometries (chunk boundaries inside the grid), the loop
+# test as a finish kernel after every sweep (default) or folded into the next
+# sweep, and the two colour-pass form
+SOLVE_TUNES = [(1, 8, 0), (1, 4, 4), (1, 12, 5), (1, 8, 3 + 4), (1, 8, 0, 1), (1, 4, 4, 1),
+               (1, 12, 5, 1), (0, 8, 0)]
+
+
+def set_tune(g, tune):
+    g.set_tuning(M.TUNE3_SWEEP, tune[0])
+    g.set_tuning(M.TUNE3_ROWS, tune[1])
+    g.set_tuning(M.TUNE3_KCHUNK, tune[2])
+    if len(tune) > 3:
+        g.set_tuning(M.TUNE3_FOLD, tune[3])
 
 
 def pair(prm, st, dt, tune=None):
@@ -61,9 +71,7 @@ def pair(prm, st, dt, tune=None):
     ns.s.dt = dt
     g = M.Grid3(prm)
     if tune is not None:
-        g.set_tuning(M.TUNE3_SWEEP, tune[0])
-        g.set_tuning(M.TUNE3_ROWS, tune[1])
-        g.set_tuning(M.TUNE3_KCHUNK, tune[2])
+        set_tune(g, tune)
     for n in orc3.FIELDS:
         g.upload(GPU_FIELD[n], st[n])
     g.set_dt(dt)
@@ -200,9 +208,7 @@ def run_gpu(prm, steps, tune=None):
     """assignment-6/src/main.c:45-60 through the C ABI (no normalizePressure)"""
     g = M.Grid3(prm)
     if tune is not None:
-        g.set_tuning(M.TUNE3_SWEEP, tune[0])
-        g.set_tuning(M.TUNE3_ROWS, tune[1])
-        g.set_tuning(M.TUNE3_KCHUNK, tune[2])
+        set_tune(g, tune)
     g.fill(M.U3, prm["u_init"])
     g.fill(M.V3, prm["v_init"])
     g.fill(M.W3, prm["w_init"])
@@ -220,7 +226,7 @@ def run_gpu(prm, steps, tune=None):
     return g, np.array(iters), t
 
 
-@pytest.mark.parametrize("tune", [(1, 8, 0), (0, 8, 0), (1, 4, 4)])
+@pytest.mark.parametrize("tune", [(1, 8, 0), (0, 8, 0), (1, 4, 4), (1, 8, 0, 1)])
 @pytest.mark.parametrize("fixture,par", [("ns3d_dcavity_short.npz", "a6_dcavity.par"),
                                          ("ns3d_canal_short.npz", "a6_canal.par")])
 def test_short_run_matches_reference_fixture(golden, fixture, par, tune):
@@ -254,6 +260,7 @@ def test_tuning_keys(golden):
     with M.Grid3(prm) as g:
         assert g.get_tuning(M.TUNE3_SWEEP) == 1 and g.get_tuning(M.TUNE3_ROWS) == 8
         assert g.get_tuning(M.TUNE3_KCHUNK) >= 8
+        assert g.get_tuning(M.TUNE3_FOLD) == 0
         for key, bad in ((M.TUNE3_SWEEP, 2), (M.TUNE3_ROWS, 5), (M.TUNE3_KCHUNK, 2), (99, 0)):
             with pytest.raises(M.MisorError):
                 g.set_tuning(key, bad)

@@ -3,6 +3,7 @@ iteration counts from a random state, device time from the library's HIP
 events, p checked bit-identical across variants.
 
     python tools/tune3d.py --size 384 --iters 60 [--configs 1,8,0 1,4,0 0,8,0 ...]
+    (a config is sweep,rows,kchunk[,fold]; MISOR3_TUNE_*)
 """
 import argparse
 import os
@@ -34,11 +35,14 @@ def main():
         rhs = rng.standard_normal((n + 2, n + 2, n + 2))
         ref = None
         for cfg in a.configs:
-            sw, rows, kc = (int(x) for x in cfg.split(","))
+            v = [int(x) for x in cfg.split(",")]
+            sw, rows, kc = v[:3]
+            fold = v[3] if len(v) > 3 else 0
             with M.Grid3(prm) as g:
                 g.set_tuning(M.TUNE3_SWEEP, sw)
                 g.set_tuning(M.TUNE3_ROWS, rows)
                 g.set_tuning(M.TUNE3_KCHUNK, kc)
+                g.set_tuning(M.TUNE3_FOLD, fold)
                 g.upload(M.RHS3, rhs)
                 best = None
                 for r in range(a.reps + 1):
@@ -54,9 +58,9 @@ def main():
                     ref = p
                 kc_eff = g.get_tuning(M.TUNE3_KCHUNK)
             mlups = n ** 3 / (best / 1e3) / 1e6
-            print("n=%d sweep=%d rows=%d kc=%d: %.4f ms/iter  %.0f MLUP/s  %.3f of 8 TB/s "
-                  "(24 B/LUP)  %s" % (n, sw, rows, kc_eff, best, mlups, mlups * 24e-6 / 8.0,
-                                      same), flush=True)
+            print("n=%d sweep=%d rows=%d kc=%d fold=%d: %.4f ms/iter  %.0f MLUP/s  "
+                  "%.3f of 8 TB/s (24 B/LUP)  %s" % (n, sw, rows, kc_eff, fold, best, mlups,
+                                                     mlups * 24e-6 / 8.0, same), flush=True)
 
 
 if __name__ == "__main__":

@@ -119,3 +119,75 @@ def test_ns_dcavity_16384_two_steps(golden):
             assert np.abs(got - want).max() <= 1e-12 * scale, name
     finally:
         g.close()
+
+
+def test_decomposed_8_ranks_32768_windows():
+    """BASELINE config 4 at 8 GPUs: the 4 x 2 split of 32768^2 that bench.py
+    --gpus 8 runs (one rank's block 8192 x 16384: T = 7, its automatic block
+    geometry, pipelined passes with the slot reserve, 2T-deep exchanges), as 8
+    in-process ranks on the one GPU of the test box; windows at the physical
+    corners and where two and four rank blocks meet, bit for bit against the
+    oracle run on the window (see test_full_size_32768_windows)"""
+    import threading
+    n, k, world = 32768, 20, 8
+    m = 2 * k + 2
+    C, W = 812, 768 + 2 * m
+    N2 = n + 2
+    dx = 1.0 / n
+    cid = b"LOCAL:bench8"
+    outs, errs = [None] * world, []
+
+    def body(r):
+        try:
+            with M.Grid(n, n, dx, dx, OMEGA, 1e-300, k, device=0, nranks=world, rank=r,
+                        comm_id=cid) as g:
+                g.poisson_init(1.0, 1.0, 2)
+                p0, rhs = g.download(M.P), g.download(M.RHS)
+                it, _ = g.solve_rb()
+                outs[r] = (g.loc, p0, rhs, g.download(M.P), it, g.stats()["iters_per_pass"])
+        except BaseException as e:
+            errs.append((r, repr(e)))
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(600)
+        assert not t.is_alive(), "rank thread hung"
+    assert not errs, errs
+    assert all(o[4] == k for o in outs)
+    assert all(o[5] == 7 for o in outs)  # T of a 2^27-cell block (misor_api.hip)
+    assert tuple(outs[0][0].dims) == (4, 2) and (outs[0][0].ni, outs[0][0].nj) == (8192, 16384)
+
+    def assemble(idx):
+        glob = np.empty((N2, N2))
+        for o in outs:
+            loc, a = o[0], o[idx]
+            nb = list(loc.neighbours)
+            i0, j0 = (0 if nb[0] < 0 else 1), (0 if nb[2] < 0 else 1)
+            i1 = loc.ni + 1 if nb[1] < 0 else loc.ni
+            j1 = loc.nj + 1 if nb[3] < 0 else loc.nj
+            glob[loc.joff + j0:loc.joff + j1 + 1, loc.ioff + i0:loc.ioff + i1 + 1] = \
+                a[j0:j1 + 1, i0:i1 + 1]
+        return glob
+
+    p0, rhs = assemble(1), assemble(2)
+    h = W // 2
+    # (j0, i0, h, w), j0 + i0 even: four physical corners; the junction of four
+    # blocks (j = 16384, i = 8192); a vertical boundary (i = 16384) inside a
+    # block row; the horizontal boundary (j = 16384) at the physical left side
+    wins = [(0, 0, C, C), (0, N2 - C, C, C), (N2 - C, 0, C, C), (N2 - C, N2 - C, C, C),
+            (16384 - h, 8192 - h, W, W), (8000 - h, 16384 - h, W, W), (16384 - h, 0, W, C)]
+    ref = [window_oracle(p0, rhs, j0, i0, hh, w, k, dx, dx) for (j0, i0, hh, w) in wins]
+    del p0, rhs
+    got = assemble(3)
+    outs.clear()
+    for (j0, i0, hh, w), pw in zip(wins, ref):
+        jl = 0 if j0 == 0 else m
+        jh = hh if j0 + hh == N2 else hh - m
+        il = 0 if i0 == 0 else m
+        ih = w if i0 + w == N2 else w - m
+        a = got[j0 + jl:j0 + jh, i0 + il:i0 + ih]
+        b = pw[jl:jh, il:ih]
+        assert min(a.shape) >= 768, (a.shape, j0, i0)
+        assert np.array_equal(a, b), ((j0, i0), np.argwhere(a != b)[:5])

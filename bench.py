@@ -389,6 +389,10 @@ def main():
                          "assignment-6's 3D dcavity (--size cells^3, default 128)")
     ap.add_argument("--itermax", type=int, default=0,
                     help="ns: pressure-solve cap (default 100); ns3d: default 1000 (.par)")
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
+                    help="poisson: strong (default: the --size^2 grid split over the GPUs, "
+                         "BASELINE config 4) or weak (--size^2 cells per GPU: the global grid "
+                         "is the process grid times --size^2, same spacing 1/--size)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -424,16 +428,22 @@ def main():
     import pymisor as M
 
     n = args.size
+    # strong: n^2 over all GPUs; weak: n^2 per GPU, the process grid's extent
+    # in cells, on a domain of dims[0] x dims[1] unit squares (spacing 1/n
+    # either way, so the power-of-two form of the sweep applies to both)
+    pdims = list(M.decompose(world, 0, 1 << 20, 1 << 20).dims) if args.scaling == "weak" \
+        else [1, 1]
+    imax, jmax = n * pdims[0], n * pdims[1]
     comm_id = None
     if world > 1:
         obj = [M.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         comm_id = obj[0]
-    g = M.Grid(n, n, 1.0 / n, 1.0 / n, 1.9, 1e-300, args.steps, device=local_rank,
+    g = M.Grid(imax, jmax, 1.0 / n, 1.0 / n, 1.9, 1e-300, args.steps, device=local_rank,
                nranks=world, rank=rank, comm_id=comm_id)
     if args.tsteps > 0:
         g.set_tuning(M.TUNE_TSTEPS, args.tsteps)
-    g.poisson_init(1.0, 1.0, 2)
+    g.poisson_init(float(pdims[0]), float(pdims[1]), 2)
     local_cells = g.loc.ni * g.loc.nj
 
     def barrier():
@@ -471,7 +481,7 @@ def main():
     else:
         kern_ms = st["sweep_ms"] / passes
 
-    total_lup = float(n) * float(n) * args.steps
+    total_lup = float(imax) * float(jmax) * args.steps
     mlups = total_lup / elapsed / 1e6
     # one pass moves at least p in, rhs in, p out: 24 B per local cell
     hbm_min = BYTES_PER_LUP * local_cells
@@ -490,14 +500,14 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (assignment-4 problem-2 fields, generated on device)",
         "config": {"workload": "2D Poisson red-black SOR (solveRB), %dx%d interior cells, "
                                "fixed %d iterations per timed region, 1 iteration = 1 step, "
-                               "%d iterations per kernel launch" % (n, n, args.steps, T),
-                   "imax": n, "jmax": n, "omega": 1.9, "problem": 2,
+                               "%d iterations per kernel launch" % (imax, jmax, args.steps, T),
+                   "imax": imax, "jmax": jmax, "omega": 1.9, "problem": 2,
                    "decomposition": dims, "baseline_config": 4},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / PEAK_GBS, 4),

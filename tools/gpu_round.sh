@@ -14,3 +14,5 @@ timeout -k 10 300 python tools/scale_proxy.py --tsteps 7,8 --rows 0 --rounds 2 -
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
     --master-port 29611 bench.py --gpus 1 --steps 24 --warmup 8 --no-cpu-baseline \
     > gpurun_out/bench_torchrun_$tag.json 2> gpurun_out/bench_torchrun_$tag.err
+timeout -k 10 300 python bench.py --scaling weak --steps 24 --warmup 8 --no-cpu-baseline \
+    > gpurun_out/bench_weak_$tag.json 2> gpurun_out/bench_weak_$tag.err

@@ -148,6 +148,14 @@ int misor_download(misor_grid* g, int field, double* host);
  * every rank contributes its interior plus the ghost layer on its physical
  * sides; other ranks pass NULL.  With one rank it is misor_download. */
 int misor_gather(misor_grid* g, int field, double* host_global);
+/* exchange (assignment-5/skeleton/src/solver.c:137-165): collective over the
+ * ranks of a decomposed grid.  The `depth`-deep halo of `field` (1 <= depth <=
+ * the deepest halo the grid supports, >= 2) receives the neighbours' owned
+ * cells, edges and corners, from all 8 neighbours; ghost cells on physical
+ * sides are not touched.  MISOR_P is the current pressure buffer.  With one
+ * rank it does nothing.  The solve and the NS steps exchange internally;
+ * this entry point is the skeleton's own call (and its printExchange check). */
+int misor_exchange(misor_grid* g, int field, int depth);
 /* number of visible GPUs (host programs map rank -> device) */
 int misor_device_count(int* n);
 /* fill a field (incl. ghosts) with a constant; initSolver of NS (solver.c:92-99) */

@@ -1072,6 +1072,18 @@ int misor_gather(misor_grid* g, int field, double* host) {
     return MISOR_OK;
 }
 
+int misor_exchange(misor_grid* g, int field, int depth) {
+    if (!g || !field_ptr(g, field)) return fail(MISOR_EINVAL, "bad exchange");
+    if (!g->dist) return MISOR_OK;
+    if (depth < 1 || depth > g->max_depth)
+        return fail(MISOR_EINVAL, "exchange depth %d outside 1..%d", depth, g->max_depth);
+    HIPCHK(hipSetDevice(g->device));
+    int rc = exchange(g, field_ptr(g, field), depth);
+    if (rc) return rc;
+    if (field == MISOR_RHS) g->rhs_halo = std::max(g->rhs_halo, depth);  // now fresh to depth
+    return wait_stream(g, g->stream);
+}
+
 int misor_device_count(int* n) {
     if (!n) return fail(MISOR_EINVAL, "null argument");
     HIPCHK(hipGetDeviceCount(n));

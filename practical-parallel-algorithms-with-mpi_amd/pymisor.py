@@ -91,6 +91,7 @@ SIGNATURES = {
     "misor_download": (C.c_int, [C.c_void_p, C.c_int, _dp]),
     "misor_fill": (C.c_int, [C.c_void_p, C.c_int, C.c_double]),
     "misor_gather": (C.c_int, [C.c_void_p, C.c_int, _dp]),
+    "misor_exchange": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     "misor_device_count": (C.c_int, [C.POINTER(C.c_int)]),
     "misor_poisson_init": (C.c_int, [C.c_void_p, C.c_double, C.c_double, C.c_int]),
     "misor_solve_rb": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), _dp]),
@@ -238,6 +239,11 @@ class Grid:
             return out
         _check(lib().misor_gather(self.h, field, C.cast(None, _dp)))
         return None
+
+    def exchange(self, field, depth=1):
+        """exchange (skeleton/src/solver.c:137-165): the depth-deep halo of
+        `field` from the 8 neighbours (collective)"""
+        _check(lib().misor_exchange(self.h, field, depth))
 
     def fill(self, field, value):
         _check(lib().misor_fill(self.h, field, value))

@@ -276,3 +276,49 @@ def test_pipelined_reserve(reserve):
     assert all(o[2] == k for o in outs)
     got = assemble([(o[0], o[1]) for o in outs], p.shape)
     assert np.array_equal(got, want), np.argwhere(got != want)[:5]
+
+
+@pytest.mark.parametrize("world,dims", [(2, (0, 0)), (4, (0, 0)), (6, (3, 2)), (8, (0, 0))])
+@pytest.mark.parametrize("depth", [1, 2, 7])
+def test_exchange_rank_fill(world, dims, depth):
+    """the skeleton's printExchange check (assignment-5/skeleton/src/solver.c:38-66):
+    every rank fills the cells it owns -- its interior plus the ghost cells on
+    its physical sides -- with a code of (rank, global i, global j) and the
+    rest of its array with -1; after misor_exchange at any depth every cell of
+    every rank's (ni+2) x (nj+2) array holds the code its owner wrote for that
+    global cell: own cells untouched, halo edges and corners from the 8
+    neighbours (corner ghosts of a physical side from the neighbour that owns
+    them)"""
+    ni, nj = 61, 47
+
+    def code(r, gi, gj):
+        return r * 1e6 + gj * 1000.0 + gi
+
+    def extent(loc):  # global cells a rank owns, (i0, i1, j0, j1) inclusive
+        nb = list(loc.neighbours)
+        return (loc.ioff + (0 if nb[0] < 0 else 1), loc.ioff + loc.ni + (1 if nb[1] < 0 else 0),
+                loc.joff + (0 if nb[2] < 0 else 1), loc.joff + loc.nj + (1 if nb[3] < 0 else 0))
+
+    def rank_fn(r, cid, dims):
+        with M.Grid(ni, nj, 1.0 / ni, 1.0 / nj, 1.7, 1e-6, 10, device=0, nranks=world, rank=r,
+                    dims=dims, comm_id=cid) as g:
+            loc = g.loc
+            i0, i1, j0, j1 = extent(loc)
+            jj, ii = np.mgrid[0:loc.nj + 2, 0:loc.ni + 2]
+            gi, gj = loc.ioff + ii, loc.joff + jj
+            mine = (gi >= i0) & (gi <= i1) & (gj >= j0) & (gj <= j1)
+            a = np.where(mine, code(r, gi, gj), -1.0)
+            g.upload(M.U, a)
+            g.exchange(M.U, depth)
+            return loc, g.download(M.U)
+
+    outs = run_ranks(world, rank_fn, dims)
+    ext = [extent(o[0]) for o in outs]
+    for r, (loc, got) in enumerate(outs):
+        for j in range(loc.nj + 2):
+            for i in range(loc.ni + 2):
+                gi, gj = loc.ioff + i, loc.joff + j
+                own = [q for q, (a0, a1, b0, b1) in enumerate(ext)
+                       if a0 <= gi <= a1 and b0 <= gj <= b1]
+                assert len(own) == 1, (gi, gj, own)
+                assert got[j, i] == code(own[0], gi, gj), (r, i, j, got[j, i], own[0])

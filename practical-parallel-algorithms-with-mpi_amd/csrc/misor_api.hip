@@ -611,14 +611,19 @@ static void tb_geometry(const misor_grid* g, int T, SweepParams& tp) {
     const int S = tb_ring_slots(T, tp.variant);
     int h = req > 0 ? req : pick_tb_rows(g->loc.ni, nj, T, tp.variant);
     if (h > nj) h = nj;
-    const int hs = S * std::max(1, (kTbSmallRows + S / 2) / S);
+    // MISOR_TB_SMALL_ROWS / MISOR_TB_BAND_ROUNDS: tuning experiments (tools/geom_sweep.py)
+    const char* es = getenv("MISOR_TB_SMALL_ROWS");
+    const char* eb = getenv("MISOR_TB_BAND_ROUNDS");
+    const int small_rows = es && atoi(es) > 0 ? atoi(es) : kTbSmallRows;
+    const double band_rounds = eb && atof(eb) >= 0 ? atof(eb) : kTbSmallRounds;
+    const int hs = S * std::max(1, (small_rows + S / 2) / S);
     int nbig = 0, ns = 0;
     if (req > 0 || hs >= h || nj < 4 * hs) {  // uniform blocks, the last takes the rest
         nbig = nj / h;
         if (nbig * h == nj && nbig > 0) --nbig;
     } else {
         const int band = std::min(
-            (kTbSmallRounds * tb_resident(T, tp.variant) + tp.nbx - 1) / tp.nbx, nj / 4 / hs);
+            (int)((band_rounds * tb_resident(T, tp.variant) + tp.nbx - 1) / tp.nbx), nj / 4 / hs);
         nbig = std::max(0, (nj - band * hs - hs) / h);
         ns = std::max(0, (nj - nbig * h) / hs - 1);  // the last row: [hs, 2 hs)
     }

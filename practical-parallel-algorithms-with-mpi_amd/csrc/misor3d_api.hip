@@ -88,6 +88,8 @@ struct misor_grid3 {
     int rows = 8;              // MISOR3_TUNE_ROWS
     int kchunk = 0;            // MISOR3_TUNE_KCHUNK (0: automatic)
     int fold = 0;              // MISOR3_TUNE_FOLD: single rank, loop test inside the sweep
+    int rhs_ahead = 0;         // MISOR3_TUNE_RHS_AHEAD: fused sweep's rhs loads 1 or 2 steps
+                               // ahead; 0: 2 on marches of >= 16 planes, else 1
     double dx = 0, dy = 0, dz = 0, dt = 0, dt_bound = 0;
     double* partials = nullptr;  // per-block partial sums / maxima
     long long partials_cap = 0;
@@ -638,6 +640,10 @@ int misor3_solve(misor_grid3* g, int* iters, double* res) {
     const bool fused = g->sweep != 0;
     if (!fused && dist(g)) return fail3(MISOR_ESTATE, "the two-pass solve is single-rank only");
     const int kc = g->kchunk > 0 ? g->kchunk : auto_kchunk(g->g, g->rows);
+    // rhs two plane steps ahead pays on long marches (384^3, 32 planes: 0.384 ->
+    // 0.376 ms per iteration) and costs on short ones (128^3, 8 planes: 27.4 ->
+    // 28.1 us; profiles/r02_tune3d_ra2.txt)
+    const bool ra2 = g->rhs_ahead ? g->rhs_ahead == 2 : kc >= 16;
     // single rank: the loop test of sweep m runs inside sweep m+1 (k3_sweep,
     // Fold3); the state alternates between st and st2, the partials between
     // the two halves of g->partials
@@ -674,7 +680,7 @@ int misor3_solve(misor_grid3* g, int* iters, double* res) {
                 launch3_sweep_folded(g->stream, g->g, buf[m & 1], buf[(m + 1) & 1],
                                      g->fld[MISOR3_RHS], 1.0 / dx2, 1.0 / dy2, 1.0 / dz2, factor,
                                      g->rows, kc, part[m & 1], b == 0 ? nullptr : part[(m - 1) & 1],
-                                     stb[sx], stb[sx ^ 1], cells);
+                                     stb[sx], stb[sx ^ 1], cells, ra2);
                 sx ^= 1;
                 continue;
             }
@@ -686,7 +692,7 @@ int misor3_solve(misor_grid3* g, int* iters, double* res) {
             }
             launch3_sweep(g->stream, g->g, buf[m & 1], buf[(m + 1) & 1], g->fld[MISOR3_RHS],
                           1.0 / dx2, 1.0 / dy2, 1.0 / dz2, factor, g->rows, kc, g->partials,
-                          g->st, cells, dist(g));
+                          g->st, cells, dist(g), ra2);
             if (dist(g)) {
                 if ((rc = allreduce3(g, &g->st->sum[0], 1, false)) != MISOR_OK) return rc;
                 launch3_decide(g->stream, g->st, cells);
@@ -746,6 +752,10 @@ int misor3_set_tuning(misor_grid3* g, int key, int value) {
         g->kchunk = value;
         return MISOR_OK;
     case MISOR3_TUNE_FOLD: g->fold = value != 0; return MISOR_OK;
+    case MISOR3_TUNE_RHS_AHEAD:
+        if (value < 0 || value > 2) return fail3(MISOR_EINVAL, "rhs_ahead must be 0, 1 or 2");
+        g->rhs_ahead = value;
+        return MISOR_OK;
     }
     return fail3(MISOR_EINVAL, "unknown tuning key %d", key);
 }
@@ -759,6 +769,7 @@ int misor3_get_tuning(const misor_grid3* g, int key, int* value) {
         *value = g->kchunk > 0 ? g->kchunk : auto_kchunk(g->g, g->rows);
         return MISOR_OK;
     case MISOR3_TUNE_FOLD: *value = g->fold; return MISOR_OK;
+    case MISOR3_TUNE_RHS_AHEAD: *value = g->rhs_ahead; return MISOR_OK;
     }
     return fail3(MISOR_EINVAL, "unknown tuning key %d", key);
 }

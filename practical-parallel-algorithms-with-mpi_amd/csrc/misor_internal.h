@@ -274,7 +274,8 @@ int launch3_rb_iteration(hipStream_t s, const G3& g, double* p, const double* rh
 int sweep3_blocks(const G3& g, int rows, int kc);
 int launch3_sweep(hipStream_t s, const G3& g, const double* src, double* dst, const double* rhs,
                   double idx2, double idy2, double idz2, double factor, int rows, int kc,
-                  double* partials, DevState* st, double cells, bool sum_only = false);
+                  double* partials, DevState* st, double cells, bool sum_only = false,
+                  bool ra2 = false);
 void launch3_fg(hipStream_t s, const G3& g, const double* u, const double* v, const double* w,
                 double* f, double* gg, double* h, const Fg3& c);
 void launch3_adapt(hipStream_t s, const G3& g, const double* f, const double* gg,
@@ -303,7 +304,7 @@ void launch3_sweep_folded(hipStream_t s, const G3& g, const double* src, double*
                           const double* rhs, double idx2, double idy2, double idz2,
                           double factor, int rows, int kc, double* partials,
                           const double* prev_partials, const DevState* st_in, DevState* st_out,
-                          double cells);
+                          double cells, bool ra2 = false);
 void launch3_fold_decide(hipStream_t s, const G3& g, int rows, int kc,
                          const double* prev_partials, const DevState* st_in, DevState* st_out,
                          double cells);

@@ -182,12 +182,14 @@ struct Fold3 {
     double cells;
 };
 
-// the loop test of one sweep; scratch: 1024 doubles of LDS; every thread of
-// the (256-thread) workgroup returns the new state's done flag
-__device__ __forceinline__ int fold_test(const Fold3& F, double* scratch, DevState& s) {
+// the loop test of one sweep; scratch: 1025 doubles of LDS; every thread of
+// the (256-thread) workgroup returns the new state's done flag.  The state is
+// handled field by field (a whole-struct copy lands in scratch memory).
+__device__ __forceinline__ int fold_test(const Fold3& F, double* scratch) {
     const int t = threadIdx.y * blockDim.x + threadIdx.x;
-    s = *F.in;
-    if (!s.done && F.prev) {
+    int it = F.in->it, done = F.in->done;
+    double res = F.in->res;
+    if (!done && F.prev) {
         // k3_finish's order with 1024 virtual threads v = t + 256 m
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
@@ -209,20 +211,23 @@ __device__ __forceinline__ int fold_test(const Fold3& F, double* scratch, DevSta
             if (t == 0) scratch[1024] = v;
         }
         __syncthreads();
-        const double res = (s.res + scratch[1024]) / F.cells;
-        const int it = s.it + 1;
-        s.res = res;
-        s.it = it;
-        s.done = !((res >= s.epssq) && (it < s.itermax));
+        res = (res + scratch[1024]) / F.cells;
+        it = it + 1;
+        done = !((res >= F.in->epssq) && (it < F.in->itermax));
     }
-    if (blockIdx.x == 0 && t == 0) *F.out = s;
-    return s.done;
+    if (blockIdx.x == 0 && t == 0) {
+        F.out->it = it;
+        F.out->done = done;
+        F.out->res = res;
+        F.out->itermax = F.in->itermax;
+        F.out->epssq = F.in->epssq;
+    }
+    return done;
 }
 
 __global__ __launch_bounds__(256) void k3_fold_decide(Fold3 F) {
     __shared__ double scratch[1025];
-    DevState s;
-    (void)fold_test(F, scratch, s);
+    (void)fold_test(F, scratch);
 }
 
 // ------------------------------------------------- fused red-black sweep
@@ -300,7 +305,7 @@ struct alignas(8) D2 {
 };
 }  // namespace
 
-template <int R>
+template <int R, bool RA2 = false>
 __global__ __launch_bounds__(256) void k3_sweep(G3 g, const double* __restrict__ src,
                                                 double* __restrict__ dst,
                                                 const double* __restrict__ rhs, double idx2,
@@ -445,7 +450,7 @@ __global__ __launch_bounds__(256) void k3_sweep(G3 g, const double* __restrict__
                     const SwCell (&cp)[RR], const D2 (&rk)[RR], const D2 (&rkm)[RR],
                     D2 (&rk_n)[RR]) {
         load_plane(k + 3, pl_in);
-        load_rhs(k + 1, rk_n);
+        load_rhs(k + (RA2 ? 2 : 1), rk_n);
         __syncthreads();  // plane k+1 in LDS, plane k-2 final; the slot reused below is free
         if (k - 2 >= k0 && k - 2 <= kend) store_final(k - 2);
         if (k >= kr_lo && k <= kr_hi) {
@@ -496,19 +501,27 @@ __global__ __launch_bounds__(256) void k3_sweep(G3 g, const double* __restrict__
     // ahead -- 4 + 4 register sets -- ran 1.6-1.7x slower at 128^3 and 384^3,
     // profiles/r02_tune3d_depth.txt)
     D2 pl[2][LR];
-    D2 rs[3][RR];  // rhs pairs of three consecutive planes, rotating
+    // rhs pairs of consecutive planes, rotating: 3 sets, loaded one step
+    // ahead; RA2: 4 sets (set of plane x = (x - k0 + 1) & 3), two steps ahead
+    constexpr int NRS = RA2 ? 4 : 3;
+    D2 rs[NRS][RR];
     load_plane(k0 - 2, v0);
     load_plane(k0 - 1, v1);
     load_plane(k0, v2);
     load_plane(k0 + 1, pl[0]);
-    load_rhs(k0 - 2, rs[2]);
-    load_rhs(k0 - 1, rs[0]);
+    if constexpr (RA2) {
+        load_rhs(k0 - 2, rs[NRS - 1]);
+        load_rhs(k0 - 1, rs[0]);
+        load_rhs(k0, rs[1]);
+    } else {
+        load_rhs(k0 - 2, rs[2]);
+        load_rhs(k0 - 1, rs[0]);
+    }
     if (F.in) {
         // folded loop test (single rank): its partial-sum loads queue behind
         // the preloads, so it costs the LDS tree, not another memory latency;
         // L is free until the planes are stored
-        DevState s;
-        if (fold_test(F, L, s)) return;  // uniform: every thread reads the same state
+        if (fold_test(F, L)) return;  // uniform: every thread reads the same state
         __syncthreads();                 // scratch reads done before the planes land
     }
     store_plane(k0 - 2, v0);
@@ -517,6 +530,19 @@ __global__ __launch_bounds__(256) void k3_sweep(G3 g, const double* __restrict__
     // step k uses the pairs of planes k (red) and k-1 (black) and loads k+1;
     // with k = k0-1+3n+u the three sets rotate with period 3, the planes with
     // period 2: unroll by 6
+    if constexpr (RA2) {
+        // step k = k0-1+u (mod 4): red uses rhs set u, black set u+3, loads
+        // rhs k+2 into set u+2; p planes alternate as below
+        for (int k = k0 - 1; k <= kend + 1; k += 4) {
+            step(k, pl[1], pl[0], cA, cB, rs[0], rs[NRS - 1], rs[2]);
+            if (k + 1 > kend + 1) break;
+            step(k + 1, pl[0], pl[1], cB, cA, rs[1], rs[0], rs[NRS - 1]);
+            if (k + 2 > kend + 1) break;
+            step(k + 2, pl[1], pl[0], cA, cB, rs[2], rs[1], rs[0]);
+            if (k + 3 > kend + 1) break;
+            step(k + 3, pl[0], pl[1], cB, cA, rs[NRS - 1], rs[2], rs[1]);
+        }
+    } else
     for (int k = k0 - 1; k <= kend + 1; k += 6) {
         step(k, pl[1], pl[0], cA, cB, rs[0], rs[2], rs[1]);
         if (k + 1 > kend + 1) break;
@@ -795,26 +821,26 @@ int sweep3_blocks(const G3& g, int rows, int kc) {
 static void sweep3_kernel(hipStream_t s, const G3& g, const double* src, double* dst,
                           const double* rhs, double idx2, double idy2, double idz2,
                           double factor, int rows, int kc, double* partials,
-                          const DevState* st, const Fold3& F) {
+                          const DevState* st, const Fold3& F, bool ra2) {
     const int nstr = (g.I + kSwOwn - 1) / kSwOwn, nrb = (g.J + rows - 1) / rows;
     const int nb = sweep3_blocks(g, rows, kc);
-#define K3SW(RR_)                                                                           \
-    hipLaunchKernelGGL(k3_sweep<RR_>, dim3(nb), dim3(256), 0, s, g, src, dst, rhs, idx2, idy2, \
-                       idz2, factor, nstr, nrb, kc, partials, st, F)
+#define K3SW(RR_, A_)                                                                       \
+    hipLaunchKernelGGL((k3_sweep<RR_, A_>), dim3(nb), dim3(256), 0, s, g, src, dst, rhs, idx2,  \
+                       idy2, idz2, factor, nstr, nrb, kc, partials, st, F)
     switch (rows) {
-    case 4: K3SW(4); break;
-    case 12: K3SW(12); break;
-    default: K3SW(8); break;
+    case 4: if (ra2) K3SW(4, true); else K3SW(4, false); break;
+    case 12: if (ra2) K3SW(12, true); else K3SW(12, false); break;
+    default: if (ra2) K3SW(8, true); else K3SW(8, false); break;
     }
 #undef K3SW
 }
 
 int launch3_sweep(hipStream_t s, const G3& g, const double* src, double* dst, const double* rhs,
                   double idx2, double idy2, double idz2, double factor, int rows, int kc,
-                  double* partials, DevState* st, double cells, bool sum_only) {
+                  double* partials, DevState* st, double cells, bool sum_only, bool ra2) {
     const int nb = sweep3_blocks(g, rows, kc);
     sweep3_kernel(s, g, src, dst, rhs, idx2, idy2, idz2, factor, rows, kc, partials, st,
-                  Fold3{nullptr, 0, nullptr, nullptr, cells});
+                  Fold3{nullptr, 0, nullptr, nullptr, cells}, ra2);
     hipLaunchKernelGGL(k3_finish, dim3(1), dim3(1024), 0, s, partials, nb, 1, st, cells,
                        sum_only ? 1 : 0);
     return nb;
@@ -824,10 +850,10 @@ void launch3_sweep_folded(hipStream_t s, const G3& g, const double* src, double*
                           const double* rhs, double idx2, double idy2, double idz2,
                           double factor, int rows, int kc, double* partials,
                           const double* prev_partials, const DevState* st_in, DevState* st_out,
-                          double cells) {
+                          double cells, bool ra2) {
     const int nb = sweep3_blocks(g, rows, kc);
     sweep3_kernel(s, g, src, dst, rhs, idx2, idy2, idz2, factor, rows, kc, partials, st_in,
-                  Fold3{prev_partials, nb, st_in, st_out, cells});
+                  Fold3{prev_partials, nb, st_in, st_out, cells}, ra2);
 }
 
 void launch3_fold_decide(hipStream_t s, const G3& g, int rows, int kc,

@@ -29,7 +29,7 @@ LEX_A4, LEX_SEQ = 0, 1
 COMM_ID_BYTES = 128
 # 3D field ids (misor3_*)
 P3, RHS3, U3, V3, W3, F3, G3, H3 = range(8)
-TUNE3_SWEEP, TUNE3_ROWS, TUNE3_KCHUNK, TUNE3_FOLD = 1, 2, 3, 4
+TUNE3_SWEEP, TUNE3_ROWS, TUNE3_KCHUNK, TUNE3_FOLD, TUNE3_RHS_AHEAD = 1, 2, 3, 4, 5
 
 _dp = C.POINTER(C.c_double)
 

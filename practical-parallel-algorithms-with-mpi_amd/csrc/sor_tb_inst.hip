@@ -61,7 +61,10 @@ void MISOR_CAT(launch_tb_t, MISOR_TB_T)(hipStream_t s, const SweepParams& prm,
     // must match kTbVariants (misor_internal.h)
     switch (prm.variant) {
     case 1: TB(8, 2); break;
-    case 2: TB(2, 2); break;
+    case 2:  // 2 strips per workgroup (finer slots for small rank blocks)
+        if (prm.pow2) go(rb_tb_kernel<kT, 2, 2, false, true>, kLanes * 2, resident2<kT, 2, 2, false>());
+        else TB(2, 2);
+        break;
     case 3: TB(1, 2); break;
     case 4: TB(4, 3); break;
 #define Q4(V)                                                                               \

@@ -283,13 +283,15 @@ def test_quad_converges_mid_pass_interior():
         assert abs(r - res_ref) <= 1e-12 * res_ref
 
 
+@pytest.mark.parametrize("variant", [-1, 2], ids=["v0", "v2"])
 @pytest.mark.parametrize("T", [2, 5, 8])
 @pytest.mark.parametrize("ni,nj", [(1024, 1024), (1000, 1537), (2050, 300)])
-def test_pow2_spacing_vs_oracle(ni, nj, T, monkeypatch):
+def test_pow2_spacing_vs_oracle(ni, nj, T, variant, monkeypatch):
     """dx == dy == 2^-10: the TB kernel computes r with one fma in place of
     two multiplies, an add and a subtract (sor_tb.h resid<true>); bit for bit
     the reference's expression, on random fields of a wide dynamic range, and
-    identical to the general form (MISOR_NO_POW2=1)"""
+    identical to the general form (MISOR_NO_POW2=1); the default kernel and
+    the 2-strip workgroup variant"""
     rng = np.random.default_rng(ni + 7 * nj + T)
     p = rng.standard_normal((nj + 2, ni + 2)) * np.exp(rng.uniform(-20, 20, (nj + 2, ni + 2)))
     rhs = rng.standard_normal((nj + 2, ni + 2)) * 1e6
@@ -302,6 +304,8 @@ def test_pow2_spacing_vs_oracle(ni, nj, T, monkeypatch):
         monkeypatch.setenv("MISOR_NO_POW2", no)
         with M.Grid(ni, nj, h, h, 1.7, 1e-300, k) as g:
             set_mode(g, "t%d" % T)
+            if variant >= 0:
+                g.set_tuning(M.TUNE_TB_VARIANT, variant)
             g.upload(M.P, p)
             g.upload(M.RHS, rhs)
             it, _ = g.solve_rb()

@@ -452,11 +452,11 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    # warm-up: --warmup iterations, then every instantiation the timed solve
-    # launches (full passes of T and the last pass of steps % T)
+    # warm-up: --warmup iterations, then a solve of the timed length, so every
+    # kernel instantiation the timed solve launches has run once (the library
+    # splits a capped solve into passes of as even a length as it can)
     g.solve_rb(itermax=max(args.warmup, 1))
-    T_eff = g.stats()["iters_per_pass"] or 1
-    g.solve_rb(itermax=T_eff + args.steps % T_eff)
+    g.solve_rb(itermax=args.steps)
     g.enable_timing(True)
     g.reset_stats()
     barrier()

@@ -310,9 +310,9 @@ enum {
                              * launches, in place */
     MISOR3_TUNE_ROWS = 2,   /* fused sweep: rows per workgroup tile, 4 / 8 / 12 */
     MISOR3_TUNE_KCHUNK = 3, /* fused sweep: planes per workgroup (>= 4; 0: automatic) */
-    MISOR3_TUNE_FOLD = 4,   /* single rank, fused sweep: 1 = each sweep launch first applies
-                             * the previous sweep's loop test (one launch per iteration);
-                             * 0 (default) = a finish kernel after every sweep */
+    MISOR3_TUNE_FOLD = 4,   /* single rank, fused sweep: 1 (default) = each sweep launch first
+                             * applies the previous sweep's loop test (one launch per
+                             * iteration); 0 = a finish kernel after every sweep */
     MISOR3_TUNE_RHS_AHEAD = 5 /* fused sweep: plane steps between an rhs load and its first
                                * use, 1 or 2; 0 (default) = 2 on marches of >= 16 planes */
 };

@@ -87,7 +87,7 @@ struct misor_grid3 {
     int sweep = 1;             // MISOR3_TUNE_SWEEP
     int rows = 8;              // MISOR3_TUNE_ROWS
     int kchunk = 0;            // MISOR3_TUNE_KCHUNK (0: automatic)
-    int fold = 0;              // MISOR3_TUNE_FOLD: single rank, loop test inside the sweep
+    int fold = 1;              // MISOR3_TUNE_FOLD: single rank, loop test inside the sweep
     int rhs_ahead = 0;         // MISOR3_TUNE_RHS_AHEAD: fused sweep's rhs loads 1 or 2 steps
                                // ahead; 0: 2 on marches of >= 16 planes, else 1
     double dx = 0, dy = 0, dz = 0, dt = 0, dt_bound = 0;

@@ -49,11 +49,11 @@ def random_state(shape, seed):
 
 # 3D solve variants (sweep, rows, kchunk[, fold[, rhs_ahead]]): the fused
 # k-march sweep with the default and odd geometries (chunk boundaries inside
-# the grid), the loop test as a finish kernel after every sweep (default) or
-# folded into the next sweep, rhs loaded one (default) or two plane steps
-# ahead, and the two colour-pass form
-SOLVE_TUNES = [(1, 8, 0), (1, 4, 4), (1, 12, 5), (1, 8, 3 + 4), (1, 8, 0, 1), (1, 4, 4, 1),
-               (1, 12, 5, 1), (1, 8, 0, 0, 2), (1, 4, 4, 1, 2), (1, 12, 5, 0, 2), (1, 8, 3 + 4, 0, 2), (1, 8, 16, 0, 1),
+# the grid), the loop test folded into the next sweep (default, single rank)
+# or a finish kernel after every sweep, rhs loaded one or two plane steps
+# ahead (default: by march length), and the two colour-pass form
+SOLVE_TUNES = [(1, 8, 0), (1, 4, 4), (1, 12, 5), (1, 8, 3 + 4), (1, 8, 0, 0), (1, 4, 4, 0),
+               (1, 12, 5, 0), (1, 8, 0, 0, 2), (1, 4, 4, 1, 2), (1, 12, 5, 0, 2), (1, 8, 3 + 4, 0, 2), (1, 8, 16, 0, 1),
                (0, 8, 0)]
 
 
@@ -230,7 +230,7 @@ def run_gpu(prm, steps, tune=None):
     return g, np.array(iters), t
 
 
-@pytest.mark.parametrize("tune", [(1, 8, 0), (0, 8, 0), (1, 4, 4), (1, 8, 0, 1), (1, 8, 0, 0, 2)])
+@pytest.mark.parametrize("tune", [(1, 8, 0), (0, 8, 0), (1, 4, 4), (1, 8, 0, 0), (1, 8, 0, 0, 2)])
 @pytest.mark.parametrize("fixture,par", [("ns3d_dcavity_short.npz", "a6_dcavity.par"),
                                          ("ns3d_canal_short.npz", "a6_canal.par")])
 def test_short_run_matches_reference_fixture(golden, fixture, par, tune):
@@ -264,7 +264,7 @@ def test_tuning_keys(golden):
     with M.Grid3(prm) as g:
         assert g.get_tuning(M.TUNE3_SWEEP) == 1 and g.get_tuning(M.TUNE3_ROWS) == 8
         assert g.get_tuning(M.TUNE3_KCHUNK) >= 8
-        assert g.get_tuning(M.TUNE3_FOLD) == 0 and g.get_tuning(M.TUNE3_RHS_AHEAD) == 0
+        assert g.get_tuning(M.TUNE3_FOLD) == 1 and g.get_tuning(M.TUNE3_RHS_AHEAD) == 0
         for key, bad in ((M.TUNE3_SWEEP, 2), (M.TUNE3_ROWS, 5), (M.TUNE3_KCHUNK, 2), (99, 0)):
             with pytest.raises(M.MisorError):
                 g.set_tuning(key, bad)

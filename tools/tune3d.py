@@ -37,7 +37,7 @@ def main():
         for cfg in a.configs:
             v = [int(x) for x in cfg.split(",")]
             sw, rows, kc = v[:3]
-            fold = v[3] if len(v) > 3 else 0
+            fold = v[3] if len(v) > 3 else 1
             ahead = v[4] if len(v) > 4 else 0
             with M.Grid3(prm) as g:
                 g.set_tuning(M.TUNE3_SWEEP, sw)

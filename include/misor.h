@@ -222,9 +222,13 @@ enum {
                                     * cells next to a neighbour rank); 0 = separate kernels */
     MISOR_TUNE_FINISH2 = 11,       /* single rank: 1 (default) = two-level loop test
                                     * (partial sums, then the test); 0 = one kernel */
-    MISOR_TUNE_TB_RESERVE = 12     /* decomposed, overlapped: workgroup slots the persistent
+    MISOR_TUNE_TB_RESERVE = 12,    /* decomposed, overlapped: workgroup slots the persistent
                                     * interior launch leaves to the exchange / all-reduce /
                                     * edge-block streams (default 16) */
+    MISOR_TUNE_TB_CHAIN = 13       /* temporally blocked kernel, persistent, default variant:
+                                    * 1 (default) = chained vertical runs of short blocks
+                                    * with work stealing (no warm-up rows between the blocks
+                                    * of a run); 0 = one block per work item */
 };
 int misor_set_tuning(misor_grid* g, int key, int value);
 int misor_get_tuning(const misor_grid* g, int key, int* value);

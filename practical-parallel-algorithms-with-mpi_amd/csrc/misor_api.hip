@@ -144,6 +144,16 @@ struct misor_grid {
     int tb_reserve = kTbReserve;  // MISOR_TUNE_TB_RESERVE: slots a pipelined interior launch
                                   // leaves to the communication / edge-block streams
     int* tb_queue = nullptr;      // 8 per-XCD block counters of a persistent launch
+    // chained passes (sor_tb.h rb_tbc_kernel; MISOR_TUNE_TB_CHAIN): the initial
+    // segment list of every pass length and part (0: whole pass, 1: interior
+    // blocks, 2: edge blocks of a pipelined decomposed pass), and two work
+    // areas (parts 0 / 1, part 2: they run concurrently on two streams)
+    bool tb_chain = true;
+    struct ChainPlan {
+        unsigned long long* tmpl = nullptr;
+        int nseg0 = 0, blocks = 0;
+    } chain_plan[kMaxT + 1][3];
+    int* tb_work[2] = {nullptr, nullptr};
 
     // reductions
     double* red_partials = nullptr;
@@ -257,6 +267,9 @@ void misor_destroy(misor_grid* g) {
         if (f) (void)hipFree(f);
     (void)hipFree(g->partials);
     (void)hipFree(g->tb_queue);
+    for (auto& row : g->chain_plan)
+        for (auto& pl : row) (void)hipFree(pl.tmpl);
+    for (int* w : g->tb_work) (void)hipFree(w);
     (void)hipFree(g->st);
     (void)hipHostFree(g->st_host);
     (void)hipFree(g->red_partials);
@@ -605,10 +618,30 @@ static int pick_tb_rows(int ni, int nj, int T, int variant) {
 // hold their slots for a whole pass; profiles/r02_tb_levels.txt) and was
 // dropped.  An explicit request gives uniform blocks of that height, the last
 // row taking the rest.
+static bool chain_on(const misor_grid* g, int variant) {
+    return g->tb_chain && g->tb_persistent && variant == kDefaultTbVariant;
+}
+
 static void tb_geometry(const misor_grid* g, int T, SweepParams& tp) {
     const int nj = g->loc.nj, req = g->tb_rows_req;
     tp.nbx = tb_nbx(g->loc.ni, T, tp.variant);
     const int S = tb_ring_slots(T, tp.variant);
+    tp.chain = chain_on(g, tp.variant);
+    if (tp.chain) {
+        // chained passes: short blocks (the unit of residual partials and of
+        // work stealing), long runs; every block row but the last a multiple
+        // of the ring (MISOR_TB_CHAIN_RINGS: tuning experiments)
+        const char* er = getenv("MISOR_TB_CHAIN_RINGS");
+        const int rings = er && atoi(er) > 0 ? atoi(er) : kChainRingsPerBlock;
+        int h = req > 0 ? S * std::max(1, (req + S / 2) / S) : rings * S;
+        if (h > nj) h = nj;
+        tp.rows_per_block = h;
+        tp.nby = (nj + h - 1) / h;
+        tp.nby_big = tp.nby - 1;
+        tp.h_small = h;
+        tp.nblocks = tp.nbx * tp.nby;
+        return;
+    }
     int h = req > 0 ? req : pick_tb_rows(g->loc.ni, nj, T, tp.variant);
     if (h > nj) h = nj;
     // MISOR_TB_SMALL_ROWS / MISOR_TB_BAND_ROUNDS: tuning experiments (tools/geom_sweep.py)
@@ -632,6 +665,111 @@ static void tb_geometry(const misor_grid* g, int T, SweepParams& tp) {
     tp.h_small = hs;
     tp.nby = nbig + ns + 1;
     tp.nblocks = tp.nbx * tp.nby;
+}
+
+// The initial segment lists of the chained passes (sor_tb.h rb_tbc_kernel),
+// for every pass length 1..Te and part.  Blocks in a part: all (0), those whose
+// cone stays clear of the halo (1, sor_tb.h tb_block's test), the rest (2).
+// Along a column, blocks of steady-able rows (chain_rows_ok) form runs, each
+// split into segments of about B / G blocks (B: blocks of the part, G:
+// workgroups resident at once), so that the initial list gives every
+// resident workgroup about one segment; every other block (cone at a
+// physical bottom / top side, a last block off the ring) is a segment of its
+// own.  The list is column-interleaved (segment s of every column, then s + 1
+// ...): the XCD queues deal contiguous runs of it, so neighbouring columns --
+// whose strips share 4T columns -- march side by side on one XCD.
+static int build_chain_plans(misor_grid* g, int Te) {
+    for (auto& row : g->chain_plan)
+        for (auto& pl : row) {
+            (void)hipFree(pl.tmpl);
+            pl = misor_grid::ChainPlan{};
+        }
+    if (!chain_on(g, g->tp.variant)) return MISOR_OK;
+    long long most = 0;
+    for (int Tp = 1; Tp <= std::max(2, Te); ++Tp) {
+        SweepParams tp = g->tp;
+        tb_geometry(g, Tp, tp);
+        const int W = tb_waves(tp.variant), OW = tb_out_width(Tp, tp.variant);
+        const int S = tb_ring_slots(Tp, tp.variant);
+        const int nbx = tp.nbx, nby = tp.nby;
+        auto rows = [&](int by, int& j0, int& j1) {
+            j0 = 1 + by * tp.rows_per_block;
+            j1 = by == nby - 1 ? tp.nj + 1 : j0 + tp.rows_per_block;
+        };
+        auto interior = [&](int bx, int by) {
+            int j0, j1;
+            rows(by, j0, j1);
+            const int lo = 1 + bx * W * OW - 2 * Tp;
+            const int hi = 1 + (bx * W + W - 1) * OW - 2 * Tp + kStripCells - 1;
+            return lo >= tp.int_lo_i && hi <= tp.int_hi_i && j0 - 2 * Tp >= tp.int_lo_j &&
+                   j1 - 1 + 2 * Tp <= tp.int_hi_j;
+        };
+        auto steady = [&](int by) {  // sor_tb.h chain_rows_ok
+            int j0, j1;
+            rows(by, j0, j1);
+            return j0 - 2 * Tp >= tp.upd_lo_j && j1 - 1 + 2 * Tp <= tp.upd_hi_j &&
+                   (j1 - j0) % S == 0 && j1 > j0;
+        };
+        const int G = std::max(8, tb_resident(Tp, tp.variant));
+        for (int part = 0; part < (g->dist ? 3 : 1); ++part) {
+            auto in_part = [&](int bx, int by) {
+                return part == 0 || interior(bx, by) == (part == 1);
+            };
+            long long B = 0;
+            for (int bx = 0; bx < nbx; ++bx)
+                for (int by = 0; by < nby; ++by) B += in_part(bx, by);
+            const double per = std::max(1.0, (double)B / G);  // blocks per segment
+            std::vector<std::vector<unsigned long long>> col(nbx);
+            for (int bx = 0; bx < nbx; ++bx) {
+                for (int by = 0; by < nby;) {
+                    if (!in_part(bx, by)) {
+                        ++by;
+                        continue;
+                    }
+                    if (!steady(by)) {
+                        col[bx].push_back(chain_word(bx, by, by + 1));
+                        ++by;
+                        continue;
+                    }
+                    int e = by;
+                    while (e < nby && in_part(bx, e) && steady(e)) ++e;
+                    const int n = e - by;
+                    const int k = std::min(n, std::max(1, (int)llround(n / per)));
+                    for (int q = 0; q < k; ++q)
+                        col[bx].push_back(chain_word(bx, by + (int)((long long)n * q / k),
+                                                     by + (int)((long long)n * (q + 1) / k)));
+                    by = e;
+                }
+            }
+            std::vector<unsigned long long> list;
+            for (size_t q = 0;; ++q) {
+                bool any = false;
+                for (int bx = 0; bx < nbx; ++bx)
+                    if (q < col[bx].size()) {
+                        list.push_back(col[bx][q]);
+                        any = true;
+                    }
+                if (!any) break;
+            }
+            auto& pl = g->chain_plan[Tp][part];
+            pl.nseg0 = (int)list.size();
+            pl.blocks = (int)B;
+            most = std::max(most, (long long)list.size());
+            if (list.empty()) continue;
+            if (hipMalloc(&pl.tmpl, list.size() * sizeof(unsigned long long)) != hipSuccess ||
+                hipMemcpy(pl.tmpl, list.data(), list.size() * sizeof(unsigned long long),
+                          hipMemcpyHostToDevice) != hipSuccess)
+                return fail(MISOR_ENOMEM, "chain plan allocation failed");
+        }
+    }
+    const size_t bytes = kChainHead * sizeof(int) + (most + kChainSegCap) * sizeof(unsigned long long);
+    for (int k = 0; k < (g->dist ? 2 : 1); ++k) {
+        (void)hipFree(g->tb_work[k]);
+        g->tb_work[k] = nullptr;
+        if (hipMalloc(&g->tb_work[k], bytes) != hipSuccess)
+            return fail(MISOR_ENOMEM, "chain work area allocation failed");
+    }
+    return MISOR_OK;
 }
 
 static int configure_tb(misor_grid* g, int T, int variant, int rows) {
@@ -663,7 +801,9 @@ static int configure_tb(misor_grid* g, int T, int variant, int rows) {
     }
     tb_geometry(g, std::max(2, Te), tp);
     g->tb_nparts = tp.nblocks;
-    return ensure_partials(g, (int)need);
+    int rc = ensure_partials(g, (int)need);
+    if (rc) return rc;
+    return build_chain_plans(g, Te);
 }
 
 int misor_create(misor_grid** out, const misor_desc* d) {
@@ -1235,6 +1375,17 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
             // at the end of the interior blocks
             tp.reserve = part == 1 ? g->tb_reserve : 0;
             if (Tp != T) tb_geometry(g, Tp, tp);  // narrower cone: wider strips
+            if (tp.chain) {  // chained runs, work stealing (parts 0 / 1 and 2 concurrently)
+                const auto& pl = g->chain_plan[Tp][part];
+                if (pl.blocks == 0) return;
+                tp.seg_tmpl = pl.tmpl;
+                tp.nseg0 = pl.nseg0;
+                tp.seg_cap = kChainSegCap;
+                tp.chain_blocks = pl.blocks;
+                launch_tb(s, Tp, tp, src, dst, rhs, partials, g->st, force,
+                          g->tb_work[part == 2 ? 1 : 0]);
+                return;
+            }
             // persistent work-queue launch on the grid stream (whole passes and
             // interior blocks); the boundary blocks of a split pass are few
             int* q = (g->tb_persistent && part != 2 && s == g->stream) ? g->tb_queue : nullptr;
@@ -1736,7 +1887,12 @@ int misor_set_tuning(misor_grid* g, int key, int value) {
     case MISOR_TUNE_TSTEPS: return configure_tb(g, value, g->tp.variant, g->tb_rows_req);
     case MISOR_TUNE_TB_VARIANT: return configure_tb(g, g->tsteps, value, g->tb_rows_req);
     case MISOR_TUNE_TB_ROWS: return configure_tb(g, g->tsteps, g->tp.variant, value);
-    case MISOR_TUNE_TB_PERSISTENT: g->tb_persistent = value != 0; return MISOR_OK;
+    case MISOR_TUNE_TB_PERSISTENT:
+        g->tb_persistent = value != 0;
+        return configure_tb(g, g->tsteps, g->tp.variant, g->tb_rows_req);
+    case MISOR_TUNE_TB_CHAIN:
+        g->tb_chain = value != 0;
+        return configure_tb(g, g->tsteps, g->tp.variant, g->tb_rows_req);
     case MISOR_TUNE_NS_FUSE: g->ns_fuse = value != 0; return MISOR_OK;
     case MISOR_TUNE_FINISH2: g->finish2 = value != 0; return MISOR_OK;
     case MISOR_TUNE_TB_RESERVE:
@@ -1759,6 +1915,7 @@ int misor_get_tuning(const misor_grid* g, int key, int* value) {
     case MISOR_TUNE_TB_VARIANT: *value = g->tp.variant; return MISOR_OK;
     case MISOR_TUNE_TB_ROWS: *value = g->tp.rows_per_block; return MISOR_OK;
     case MISOR_TUNE_TB_PERSISTENT: *value = g->tb_persistent; return MISOR_OK;
+    case MISOR_TUNE_TB_CHAIN: *value = g->tb_chain; return MISOR_OK;
     case MISOR_TUNE_NS_FUSE: *value = g->ns_fuse; return MISOR_OK;
     case MISOR_TUNE_FINISH2: *value = g->finish2; return MISOR_OK;
     case MISOR_TUNE_TB_RESERVE: *value = g->tb_reserve; return MISOR_OK;

@@ -131,7 +131,31 @@ struct SweepParams {
     int pow2;                 // idx2 == idy2 == 2^m, m >= 0: the default TB kernel's P2 form
     int reserve;              // persistent launch: leave this many workgroup slots free
                               // (host only; the comm / edge streams' kernels run there)
+    // chained passes (sor_tb.h rb_tbc_kernel): vertical runs of blocks taken
+    // from the launch's segment list, with work stealing
+    int chain;                // 1: blocks are 4 ring lengths tall, runs chain them
+    int nseg0;                // segments of the launch's initial list
+    int seg_cap;              // dynamic segment slots (created by steals)
+    int chain_blocks;         // blocks in the launch (its part)
+    const unsigned long long* seg_tmpl;  // the initial list (device; copied per launch)
 };
+
+// Chained passes: a segment word holds the next unclaimed block row (bits
+// 0..25), the end block row, exclusive (26..51), and the column (52..63).
+// Work area of a chained launch: int head[kChainHead] (0..7: per-XCD tickets
+// of the initial segments, 8: dynamic segments created), then the words.
+constexpr int kChainBits = 26;
+constexpr unsigned long long kChainMask = (1ull << kChainBits) - 1;
+constexpr int kChainHead = 16;
+constexpr int kChainSegCap = 4096;       // dynamic slots per launch
+constexpr int kChainRingsPerBlock = 4;   // block height of a chained pass, in ring lengths
+__host__ __device__ inline unsigned long long chain_word(int col, int next, int end) {
+    return ((unsigned long long)col << (2 * kChainBits)) |
+           ((unsigned long long)end << kChainBits) | (unsigned long long)next;
+}
+// zero the head, copy the initial list, empty the dynamic slots
+void launch_chain_init(hipStream_t s, int* work, const unsigned long long* tmpl, int nseg0,
+                       int cap);
 
 struct NsParams {
     double dx, dy, dt;

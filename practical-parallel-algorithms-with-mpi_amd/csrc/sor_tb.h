@@ -467,7 +467,9 @@ __device__ __forceinline__ void march_interior(March<T, D>& m, const Lane& c, co
 // at a physical side as several of these, clipped to its own columns; ni +
 // anything for the 2-column kernel).  The wave's residual of every stage is
 // added to acc[].
-template <int T, int D, bool BP, bool P2 = false>
+// STEADY = false: no static-ring path (the caller knows the block's rows are
+// not steady-able; the chained kernel's edge blocks)
+template <int T, int D, bool BP, bool P2 = false, bool STEADY = true>
 __device__ __forceinline__ void tb_strip2(const SweepParams& prm, const double* __restrict__ src,
                                           double* __restrict__ dst,
                                           const double* __restrict__ rhs, const int c_out,
@@ -545,7 +547,7 @@ __device__ __forceinline__ void tb_strip2(const SweepParams& prm, const double* 
         if (q1) march_pairs<T, D, 1, kEdge, false, P2>(m, c, io, rs, rend);
         else    march_pairs<T, D, 0, kEdge, false, P2>(m, c, io, rs, rend);
     } else {
-        if (rows_in) {
+        if (STEADY && rows_in) {
             // wave-uniform descriptors over the strip's 128 columns
             auto rsrc = [&](const double* b, int row0, int rows) {
                 const unsigned long long a = (unsigned long long)(
@@ -1020,6 +1022,405 @@ __device__ __forceinline__ void for_each_block(const SweepParams& prm, int* __re
         }
         first = false;
         block(L);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Chained passes: vertical runs of blocks (SweepParams::chain)
+//
+// A block of H rows streams H + 4T rows (4T warm-up rows re-read from the
+// block below), so short blocks waste HBM traffic and issue slots in their
+// warm-up.  Here a workgroup that finishes block (bx, by) goes on with
+// (bx, by + 1) with its stage registers live: the march continues, no
+// warm-up, no re-read.  Blocks stay short (4 ring lengths, ~72 rows) -- they
+// are the unit of residual partials (fixed slots: the sum order does not
+// depend on who ran a block) and of work stealing -- while the runs are long.
+//
+// Work: segments = ranges of block rows of one column, one 64-bit word each
+// (chain_word): the next unclaimed block row N, the end E (exclusive), the
+// column.  A launch starts from a host-built list of segments (about one per
+// resident workgroup), dealt to the XCDs in contiguous runs (neighbouring
+// columns share an XCD's L2: the strips' overlapping columns).  A workgroup
+// takes a segment by ticket and claims its blocks one by one
+// (atomicAdd(word, 1): block N is its if N < E).  Once the tickets are gone it
+// steals: it scans the segments for the most unclaimed blocks r = E - N, and
+// takes the top r/2 with a compare-and-swap of (N, E) -> (N, E - r/2) (the
+// owner, which only ever increments N, keeps the block it claims next); the
+// stolen range becomes a new segment so it can be split again.  A workgroup
+// exits when no segment has 2 or more unclaimed blocks; every block is
+// claimed exactly once, by a workgroup that runs it.
+//
+// Modes along a run (the colour of each row is the same as in tb_strip2):
+// strips at a physical left / right side march in pairs (kEdge) throughout;
+// the others keep the static ring at every block boundary -- a block whose
+// cone touches a physical bottom / top side (or the column's last block, of
+// any height) is marched in pairs (kRowEdge) between two ring conversions,
+// the rest run steady chunks.  Every block height but the column's last is a
+// multiple of the ring's S slots, so every block boundary is at slot phase
+// 4T mod S.
+// ---------------------------------------------------------------------------
+// a block row [j0, j1) that can be part of a run: its cone clear of the
+// physical bottom / top sides and a height the static ring divides
+// (tb_strip2's rows_in); misor_api.hip chain_plan uses the same test
+template <int T, int D>
+__host__ __device__ inline bool chain_rows_ok(const SweepParams& prm, int j0, int j1) {
+    constexpr int S = ring_slots<T, D>();
+    return j0 - 2 * T >= prm.upd_lo_j && j1 - 1 + 2 * T <= prm.upd_hi_j && (j1 - j0) % S == 0 &&
+           j1 > j0;
+}
+
+__device__ __forceinline__ int chain_next(unsigned long long w) { return (int)(w & kChainMask); }
+__device__ __forceinline__ int chain_end(unsigned long long w) {
+    return (int)((w >> kChainBits) & kChainMask);
+}
+__device__ __forceinline__ int chain_col(unsigned long long w) { return (int)(w >> (2 * kChainBits)); }
+
+__device__ __forceinline__ unsigned long long chain_load(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The run a workgroup takes next, into sh[0..3] = column, block row, segment
+// slot (-1: a private range), end of a private range; sh[0] = -1: no work
+// left.  Wave 0 only.
+__device__ void chain_acquire(const SweepParams& prm, int* head, unsigned long long* seg,
+                              int* sh) {
+    const int lane = threadIdx.x & 63;
+    const int n0 = prm.nseg0, qq = n0 / 8, rr = n0 % 8;
+    auto run_start = [&](int x) { return x < rr ? x * (qq + 1) : rr * (qq + 1) + (x - rr) * qq; };
+    // 1. the initial segments, by ticket: the home XCD's run first
+    int got = 0;
+    if (lane == 0) {
+        const int home = blockIdx.x % 8;
+        for (int probe = 0; probe < 8;) {
+            const int x = (home + probe) & 7;
+            const int cnt = x < rr ? qq + 1 : qq;
+            const int b = atomicAdd(&head[x], 1);
+            if (b >= cnt) {
+                ++probe;
+                continue;
+            }
+            const int k = run_start(x) + b;
+            const unsigned long long old = atomicAdd(&seg[k], 1ull);
+            if (chain_next(old) < chain_end(old)) {  // else stolen empty before its owner came
+                sh[0] = chain_col(old);
+                sh[1] = chain_next(old);
+                sh[2] = k;
+                sh[3] = 0;
+                got = 1;
+                break;
+            }
+        }
+    }
+    if (__shfl(got, 0, 64)) return;
+    // 2. steal the top half of the segment with the most unclaimed blocks
+    for (;;) {
+        const int ndyn = min(__hip_atomic_load(&head[8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                             prm.seg_cap);
+        const int n = n0 + ndyn;
+        int best_r = 1, best_k = -1;
+        constexpr int U = 8;  // loads in flight per lane
+        for (int k0 = 0; k0 < n; k0 += 64 * U) {
+            unsigned long long w[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int k = k0 + u * 64 + lane;
+                w[u] = k < n ? chain_load(seg + k) : 0ull;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int r = chain_end(w[u]) - chain_next(w[u]);
+                if (r > best_r) {
+                    best_r = r;
+                    best_k = k0 + u * 64 + lane;
+                }
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const int r = __shfl_xor(best_r, o, 64), k = __shfl_xor(best_k, o, 64);
+            if (r > best_r || (r == best_r && k > best_k)) {
+                best_r = r;
+                best_k = k;
+            }
+        }
+        best_k = __shfl(best_k, 0, 64);
+        if (best_k < 0) {  // nothing left to split: the owners finish the rest
+            if (lane == 0) sh[0] = -1;
+            return;
+        }
+        int ok = 0;
+        if (lane == 0) {
+            unsigned long long w = chain_load(seg + best_k);
+            for (;;) {
+                const int N = chain_next(w), E = chain_end(w), r = E - N;
+                if (r < 2) break;
+                const int m = E - r / 2;  // the owner keeps [N, m)
+                const unsigned long long nw =
+                    chain_word(chain_col(w), N, m);
+                const unsigned long long prev = atomicCAS(seg + best_k, w, nw);
+                if (prev == w) {
+                    sh[0] = chain_col(w);
+                    sh[1] = m;
+                    sh[2] = -1;
+                    sh[3] = E;
+                    if (E - m >= 2) {  // the rest of the stolen range becomes stealable
+                        const int d = atomicAdd(&head[8], 1);
+                        if (d < prm.seg_cap) {
+                            atomicExch(seg + n0 + d, chain_word(chain_col(w), m + 1, E));
+                            sh[2] = n0 + d;
+                        }
+                    }
+                    ok = 1;
+                    break;
+                }
+                w = prev;
+            }
+        }
+        if (__shfl(ok, 0, 64)) return;
+    }
+}
+
+// End of block L of a run: the block's residual partials (as block_partials),
+// then the claim of the run's next block.  Returns its block row, or -1.
+template <int T, int WAVES>
+__device__ __forceinline__ int chain_block_end(const SweepParams& prm, double (&acc)[T],
+                                               double* partials, int L, double (*wsum)[WAVES],
+                                               int* sh, unsigned long long* seg, int slot,
+                                               int pend, int by) {
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const double s = wave_sum(acc[t]);
+        if (lane == 0) wsum[t][wave] = s;
+        acc[t] = 0.0;
+    }
+    if (threadIdx.x == 0) {
+        int nb = -1;
+        if (slot >= 0) {
+            const unsigned long long old = atomicAdd(seg + slot, 1ull);
+            if (chain_next(old) < chain_end(old)) nb = chain_next(old);
+        } else if (by + 1 < pend) {
+            nb = by + 1;
+        }
+        sh[1] = nb;
+    }
+    __syncthreads();
+    if (threadIdx.x < T) {
+        const int t = threadIdx.x;
+        double s = 0.0;
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w) s += wsum[t][w];
+        partials[(long long)t * prm.nblocks + L] = s;
+    }
+    // wave-uniform (the buffer descriptors and row offsets of the next block
+    // derive from it: they must be scalars)
+    const int nb = __builtin_amdgcn_readfirstlane(sh[1]);
+    __syncthreads();  // wsum and sh are rewritten at the next block end
+    return nb;
+}
+
+// One wave's chained run over its strip of column bx, from block row by
+// (the colour of the first streamed row: Q0): steady chunks (cols_in: every
+// block of the run is steady-able) or the general march (kEdge).  Every wave
+// of the workgroup calls chain_block_end at the same block ends.
+template <int T, int WAVES, int D, int Q0, bool P2>
+__device__ __forceinline__ void chain_strip(const SweepParams& prm, const double* __restrict__ src,
+                                            double* __restrict__ dst,
+                                            const double* __restrict__ rhs,
+                                            double* __restrict__ partials, double (*wsum)[WAVES],
+                                            int* sh, unsigned long long* seg, Lane& c,
+                                            const Io& io, bool cols_in, int c_ld, int bx, int by,
+                                            int slot, int pend, int lane) {
+    constexpr int S = ring_slots<T, D>();
+    const long long pitch = prm.pitch;
+    int j0, j1;
+    block_rows(prm, by, j0, j1);
+    auto set_block = [&](int b, int a0, int a1) {
+        c.j0 = a0;
+        c.j1 = a1;
+        c.wlo = b == 0 && prm.ghost_bottom;
+        c.whi = b == prm.nby - 1 && prm.ghost_top;
+    };
+    set_block(by, j0, j1);
+    March<T, D> m;
+#pragma unroll
+    for (int t = 0; t < T; ++t) m.acc[t] = 0.0;
+    m.keep[0] = m.keep[1] = d2{0.0, 0.0};
+    const int rs = j0 - 2 * T;
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        m.Pq[k] = ldv(io.sp + (long long)(rs + k) * pitch);
+        m.Rq[k] = ldv(io.rp + (long long)(rs - 1 + k) * pitch);
+    }
+#pragma unroll
+    for (int t = 0; t < T; ++t) m.A[t] = m.M1[t] = m.M2[t] = d2{0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < 2 * T; ++k) m.R[k] = d2{0.0, 0.0};
+
+    if (!cols_in) {  // a strip at a physical left / right side: pairs throughout
+        march_pairs<T, D, Q0, kEdge, false, P2>(m, c, io, rs, j1 - 1 + 2 * T);
+        for (;;) {
+            const int nb = chain_block_end<T, WAVES>(prm, m.acc, partials, by * prm.nbx + bx, wsum,
+                                                     sh, seg, slot, pend, by);
+            if (nb < 0) return;
+            by = nb;
+            block_rows(prm, by, j0, j1);
+            set_block(by, j0, j1);
+            march_pairs<T, D, Q0, kEdge, false, P2>(m, c, io, j0 + 2 * T, j1 - 1 + 2 * T);
+        }
+    }
+    auto rsrc = [&](const double* b, int row0, int rows) {
+        const unsigned long long a =
+            (unsigned long long)(b + (long long)(kYOff + row0) * pitch + kXOff + c_ld);
+        const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+        const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+        return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo),
+                                                 (short)0, (int)((long long)rows * pitch * 8),
+                                                 0x00020000);
+    };
+    // 4T warm-up steps, then the static ring: rhs row rs - 1 + j in slot j mod S
+    march_pairs<T, D, Q0, kPre, false, P2>(m, c, io, rs, rs + 4 * T - 1);
+    d2 R[S];
+#pragma unroll
+    for (int k = 0; k < S; ++k) R[k] = d2{0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < 2 * T; ++k) R[(4 * T - 1 - k) % S] = m.R[k];
+#pragma unroll
+    for (int k = 0; k < D; ++k) R[(4 * T + k) % S] = m.Rq[k];
+    for (;;) {
+        // the steady chunks of block [j0, j1): descriptors from its virtual
+        // start j0 - 2T (the ring phase is the same at every block start:
+        // the heights are multiples of S)
+        {
+            const int vrs = j0 - 2 * T, vrend = j1 - 1 + 2 * T;
+            Sio sio;
+            sio.p = rsrc(src, vrs, vrend - vrs + 1 + D);
+            sio.r = rsrc(rhs, vrs - 1, vrend - vrs + 1 + D);
+            sio.d = rsrc(dst, j0, j1 - j0);
+            sio.lane = (unsigned)lane * 16u;
+            sio.st_lane = c.own_a ? (unsigned)lane * 16u : 0x40000000u;
+            sio.row_bytes = (unsigned)(pitch * 8);
+            constexpr int P0 = (4 * T) % S;
+            int r0 = vrs + 4 * T;
+            unsigned off = 4u * T * sio.row_bytes;
+            for (int k = 0; k < (j1 - j0) / S; ++k) {
+                steady_chunk<T, D, Q0, P0, false, P2>(m, R, c, sio, r0, off,
+                                                     std::make_integer_sequence<int, S>{});
+                r0 += S;
+                off += (unsigned)S * sio.row_bytes;
+            }
+        }
+        if (!c.own_a) {  // lanes that do not own their columns tallied garbage
+#pragma unroll
+            for (int t = 0; t < T; ++t) m.acc[t] = 0.0;
+        }
+        const int nb = chain_block_end<T, WAVES>(prm, m.acc, partials, by * prm.nbx + bx, wsum,
+                                                 sh, seg, slot, pend, by);
+        if (nb < 0) return;
+        by = nb;
+        block_rows(prm, by, j0, j1);
+        set_block(by, j0, j1);
+    }
+}
+
+// one run of a chained pass: column bx from block row by (all waves)
+template <int T, int WAVES, int D, bool P2>
+__device__ __forceinline__ void chain_run(const SweepParams& prm, const double* __restrict__ src,
+                                          double* __restrict__ dst, const double* __restrict__ rhs,
+                                          double* __restrict__ partials, double (*wsum)[WAVES],
+                                          int* sh, unsigned long long* seg, int bx, int by,
+                                          int slot, int pend) {
+    constexpr int OW = kStripCells - 4 * T;
+    const int lane = threadIdx.x & 63;
+    // wave-uniform (as known to the compiler: the strip's descriptors and
+    // branches derive from it)
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int ni = prm.ni;
+    const int c_out = 1 + (bx * WAVES + wave) * OW;
+    if (bx == 0 && by == 0) copy_corners(prm, src, dst);
+    if (c_out > ni) {  // no strip for this wave: only the block ends
+        double acc[T];
+#pragma unroll
+        for (int t = 0; t < T; ++t) acc[t] = 0.0;
+        for (;;) {
+            by = chain_block_end<T, WAVES>(prm, acc, partials, by * prm.nbx + bx, wsum, sh, seg,
+                                           slot, pend, by);
+            if (by < 0) return;
+        }
+    }
+    const int c_ld = c_out - 2 * T;
+    const long long pitch = prm.pitch;
+    Lane c;
+    c.ia = c_ld + 2 * lane;
+    c.ib = c.ia + 1;
+    c.up_a = c.ia >= prm.upd_lo_i && c.ia <= prm.upd_hi_i;
+    c.up_b = c.ib >= prm.upd_lo_i && c.ib <= prm.upd_hi_i;
+    const bool own_lane = lane >= T && lane < kLanes - T;
+    c.own_a = own_lane && c.ia <= ni;
+    c.own_b = own_lane && c.ib <= ni;
+    c.fix0_b = prm.ghost_left && c.ib == 0;
+    c.fixr_a = prm.ghost_right && c.ia == ni + 1;
+    c.fixr_b = prm.ghost_right && c.ib == ni + 1;
+    c.st_a = c.own_a || c.fixr_a;
+    c.st_b = c.own_b || c.fix0_b || c.fixr_b;
+    c.lo_j = prm.upd_lo_j;
+    c.hi_j = prm.upd_hi_j;
+    c.parity = prm.parity;
+    c.gb = prm.ghost_bottom;
+    c.gt = prm.ghost_top;
+    c.nj = prm.nj;
+    c.idx2 = prm.idx2;
+    c.idy2 = prm.idy2;
+    c.coef = prm.coef;
+    c.bl = ((lane + 63) & 63) * 4;
+    c.br = ((lane + 1) & 63) * 4;
+    const long long base = (long long)kYOff * pitch + kXOff + c.ia;
+    Io io{src + base, rhs + base, dst + base, pitch};
+    int j0, j1;
+    block_rows(prm, by, j0, j1);
+    // steady chunks for strips clear of the physical left / right sides, in
+    // runs of steady-able block rows; the general lane-masked, row-tested
+    // march (kEdge) for the rest: strips at a physical side, and the few
+    // block rows whose cone reaches a physical bottom / top side (or a
+    // column's last block of a height the ring does not divide) -- the host
+    // keeps those in segments of their own.  (A row-tested-only march for
+    // the latter, kRowEdge, in the same kernel as the steady runs makes the
+    // register allocator spill the runs' ring.)
+    const bool cols_in = c_ld >= prm.upd_lo_i && c_ld + kStripCells - 1 <= prm.upd_hi_i &&
+                         (c_out + OW - 1 <= ni || (ni & 1) == 0) &&
+                         chain_rows_ok<T, D>(prm, j0, j1);
+    // the colour of the run's first streamed row: every block but a column's
+    // last is an even number of rows tall, so the same at every block start
+    if (((prm.parity + j0 - 2 * T) & 1) != 0)
+        chain_strip<T, WAVES, D, 1, P2>(prm, src, dst, rhs, partials, wsum, sh, seg, c, io, cols_in,
+                                        c_ld, bx, by, slot, pend, lane);
+    else
+        chain_strip<T, WAVES, D, 0, P2>(prm, src, dst, rhs, partials, wsum, sh, seg, c, io, cols_in,
+                                        c_ld, bx, by, slot, pend, lane);
+}
+
+// chained persistent pass (2-column strips); work = the launch's work area
+// (int head[kChainHead], then the segment words; misor_api.hip chain plans)
+template <int T, int WAVES, int D, bool P2>
+__global__ __launch_bounds__(kLanes* WAVES, 2) void rb_tbc_kernel(
+    SweepParams prm, const double* __restrict__ src, double* __restrict__ dst,
+    const double* __restrict__ rhs, double* __restrict__ partials,
+    const DevState* __restrict__ st, int force, int* __restrict__ work) {
+    __shared__ double wsum[T][WAVES];
+    __shared__ int sh[4];
+    if (!force && st->done) return;
+    unsigned long long* seg = reinterpret_cast<unsigned long long*>(work + kChainHead);
+    for (;;) {
+        if (threadIdx.x < kLanes) chain_acquire(prm, work, seg, sh);
+        __syncthreads();
+        const int bx = __builtin_amdgcn_readfirstlane(sh[0]);
+        const int by = __builtin_amdgcn_readfirstlane(sh[1]);
+        const int slot = __builtin_amdgcn_readfirstlane(sh[2]);
+        const int pend = __builtin_amdgcn_readfirstlane(sh[3]);
+        __syncthreads();  // sh is rewritten by the run's block ends
+        if (bx < 0) break;
+        chain_run<T, WAVES, D, P2>(prm, src, dst, rhs, partials, wsum, sh, seg, bx, by, slot, pend);
     }
 }
 

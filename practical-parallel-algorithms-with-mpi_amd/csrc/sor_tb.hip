@@ -2,6 +2,8 @@
 // the launch dispatch over T (each T's kernels are instantiated in its own
 // unit, sor_tb_inst.hip compiled with MISOR_TB_T = T, so the build runs in
 // parallel).  Device code: sor_tb.h.
+#include <algorithm>
+
 #include "misor_internal.h"
 
 namespace misor {
@@ -24,6 +26,22 @@ int tb_nbx(int ni, int T, int variant) {
     const int strips = (ni + ow - 1) / ow;
     const int waves = tb_waves(variant);
     return (strips + waves - 1) / waves;
+}
+
+__global__ void chain_init_kernel(int* work, const unsigned long long* tmpl, int nseg0,
+                                  int cap) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned long long* seg = reinterpret_cast<unsigned long long*>(work + kChainHead);
+    if (k < kChainHead) work[k] = 0;
+    if (k < nseg0) seg[k] = tmpl[k];
+    else if (k < nseg0 + cap) seg[k] = 0ull;
+}
+
+void launch_chain_init(hipStream_t s, int* work, const unsigned long long* tmpl, int nseg0,
+                       int cap) {
+    const int n = std::max(kChainHead, nseg0 + cap);
+    hipLaunchKernelGGL(chain_init_kernel, dim3((n + 255) / 256), dim3(256), 0, s, work, tmpl,
+                       nseg0, cap);
 }
 
 void launch_tb(hipStream_t s, int T, const SweepParams& prm, const double* src, double* dst,

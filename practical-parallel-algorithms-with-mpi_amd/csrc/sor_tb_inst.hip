@@ -29,6 +29,13 @@ static int resident2() {
     return n;
 }
 
+template <int T, int W, int D, bool P2>
+static int resident_chain() {
+    static int n = 0;
+    if (n == 0) n = persistent_grid(rb_tbc_kernel<T, W, D, P2>, kLanes * W);
+    return n;
+}
+
 template <int T, int W, int D, int SC>
 static int resident4() {
     static int n = 0;
@@ -48,6 +55,20 @@ void MISOR_CAT(launch_tb_t, MISOR_TB_T)(hipStream_t s, const SweepParams& prm,
                                         const double* src, double* dst, const double* rhs,
                                         double* partials, const DevState* st, int force,
                                         int* queue) {
+    if (prm.chain && queue && prm.variant == 0) {
+        // chained pass (sor_tb.h rb_tbc_kernel): the work area gets the launch's
+        // initial segment list; as many workgroups as are resident (less the
+        // reserve), at most one per block
+        launch_chain_init(s, queue, prm.seg_tmpl, prm.nseg0, prm.seg_cap);
+        auto gc = [&](auto kernel, int resident) {
+            const int grid = std::min(prm.chain_blocks, std::max(8, resident - prm.reserve));
+            hipLaunchKernelGGL(kernel, dim3(grid), dim3(kLanes * 4), 0, s, prm, src, dst, rhs,
+                               partials, st, force, queue);
+        };
+        if (prm.pow2) gc(rb_tbc_kernel<kT, 4, 2, true>, resident_chain<kT, 4, 2, true>());
+        else          gc(rb_tbc_kernel<kT, 4, 2, false>, resident_chain<kT, 4, 2, false>());
+        return;
+    }
     auto go = [&](auto kernel, int threads, int resident) {
         int grid = prm.nblocks;
         if (queue) {

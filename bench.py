@@ -26,9 +26,12 @@ events recorded around every pass on the library's stream
 (misor_enable_timing); peak = 8000 GB/s (MI355X HBM3E, MI355X_MICROARCH.md).
 traffic = HBM bytes per launch from the PMC profile committed under profiles/
 for this size and T (FETCH_SIZE x 2 + WRITE_SIZE, the gfx950 correction of
-MI355X_MICROARCH.md), or null.  floors_ms: the launch's HBM floor (24 B x
-cells at 8 TB/s) and its FP64 VALU floor (11 FP64 operations per lattice
-update at 16 lanes/clk/SIMD x 1024 SIMDs x 2.4 GHz).  The iteration-equivalent
+MI355X_MICROARCH.md) of every pass length the timed solve launches (its
+pass split, in config.pass_split), weighted by launches, or null.
+floors_ms: the launch's HBM floor (24 B x cells at 8 TB/s) and its FP64 VALU
+floor (FP64 operations per lattice update of the form that runs -- 9 with the
+power-of-two spacing identity, else 11 -- at 16 lanes/clk/SIMD x 1024 SIMDs x
+2.4 GHz).  The iteration-equivalent
 rate (24 B/LUP x T iterations / launch time, > 8 TB/s because T iterations
 share one pass) is reported separately under iteration_equivalent.
 
@@ -45,6 +48,7 @@ from __future__ import annotations
 import argparse
 import glob
 import json
+import math
 import os
 import sys
 import time
@@ -127,8 +131,10 @@ def cpu_baseline_multicore(n=8192, sweeps=40, reps=3):
                       "row bands (oracle/oracle_mt.c)" % (n, n, sweeps, reps, best, threads)}
 
 
-def pmc_summary(size, nranks, T):
-    """The committed PMC summary (tools/pmc_summary.py) for this size / ranks / T, or {}."""
+def pmc_summary(size, nranks, T, chain):
+    """The committed PMC summary (tools/pmc_summary.py) of the same launch shape
+    -- size, ranks, iterations per pass, chained kernel or not -- or {} (the
+    latest file in name order wins)."""
     best = {}
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
         try:
@@ -136,9 +142,18 @@ def pmc_summary(size, nranks, T):
         except Exception:
             continue
         if (d.get("size") == size and d.get("nranks", 1) == nranks
-                and d.get("iters_per_pass", 1) == T and "bytes_per_launch" in d):
-            best = d
+                and d.get("iters_per_pass", 1) == T and "bytes_per_launch" in d
+                and bool(d.get("chain", False)) == bool(chain)):
+            best = dict(d, file=os.path.basename(path))
     return best
+
+
+def pass_split(steps, T):
+    """Iterations of each pass of a solve capped at `steps` (misor_api.hip
+    misor_solve_rb_n: ceil(steps / T) passes, as even as possible)"""
+    n = -(-steps // T)
+    base, extra = divmod(steps, n)
+    return [base + 1] * extra + [base] * (n - extra)
 
 
 # assignment-6/dcavity.par read as 2D (SURVEY 8d config 5), sizes set per GPU
@@ -487,10 +502,40 @@ def main():
     hbm_min = BYTES_PER_LUP * local_cells
     achieved = hbm_min / (kern_ms * 1e-3) / 1e9  # GB/s per GPU
     iter_eq = hbm_min * iters_launch / (kern_ms * 1e-3) / 1e9
-    fp64_floor_ms = 11.0 * local_cells * iters_launch / (16 * 1024 * 2.4e9) * 1e3
+    # FP64 operations per update of the form the kernel runs: 11 in the
+    # reference's expression, 9 with the power-of-two spacing identity
+    # (sor_tb.h resid<true>, used when 1/dx^2 == 1/dy^2 == 2^m, m >= 1)
+    idx2, idy2 = 1.0 / (1.0 / n) ** 2, 1.0 / (1.0 / n) ** 2
+    pow2 = idx2 == idy2 and math.frexp(idx2)[0] == 0.5 and idx2 >= 2.0 and T > 1
+    fp64_ops = 9 if pow2 else 11
+    fp64_floor_ms = fp64_ops * local_cells * iters_launch / (16 * 1024 * 2.4e9) * 1e3
     dims = "%dx%d" % tuple(g.loc.dims)
-    pmc = pmc_summary(n, world, T)
-    traffic = pmc.get("bytes_per_launch")
+    chain = (T > 1 and g.get_tuning(M.TUNE_TB_CHAIN) == 1 and g.get_tuning(M.TUNE_TB_PERSISTENT)
+             == 1 and g.get_tuning(M.TUNE_TB_VARIANT) == 0)
+    split = pass_split(args.steps, T)
+    if len(split) != st["timed_passes"]:
+        split = None
+    # traffic / VALU of the timed launches: the committed PMC summaries of each
+    # pass length the split contains, weighted by its launches (null if one is
+    # missing)
+    traffic, valu, pmc_files = None, None, []
+    if split:
+        pm = {t: pmc_summary(n, world, t, chain) for t in set(split)}
+        if all(pm[t] for t in pm):
+            traffic = sum(pm[t]["bytes_per_launch"] for t in split) / len(split)
+            pmc_files = sorted(pm[t]["file"] for t in pm)
+            if all(pm[t].get("sq", {}).get("valu_insts") for t in pm):
+                valu = {"insts_per_launch": sum(pm[t]["sq"]["valu_insts"] for t in split) /
+                        len(split),
+                        "valu_busy_per_wave": round(sum(pm[t]["sq"].get("active_inst_valu", 0)
+                                                        for t in split) / len(split), 3),
+                        "source": "PMC summaries of the same launch shapes: " +
+                                  ", ".join(pmc_files)}
+    if split:
+        counts = {t: split.count(t) for t in sorted(set(split), reverse=True)}
+        split_txt = " + ".join("%d x %d" % (c, t) for t, c in counts.items())
+    else:
+        split_txt = "%d" % T
     out = {
         "metric": "red-black SOR MLUP/s + % HBM roofline at 1/2/4/8 MI355X, 32768^2 grid",
         "value": round(mlups, 1),
@@ -506,18 +551,22 @@ def main():
         "data": "synthetic (assignment-4 problem-2 fields, generated on device)",
         "config": {"workload": "2D Poisson red-black SOR (solveRB), %dx%d interior cells, "
                                "fixed %d iterations per timed region, 1 iteration = 1 step, "
-                               "%d iterations per kernel launch" % (imax, jmax, args.steps, T),
+                               "passes (kernel launches) of %s iterations" % (
+                                   imax, jmax, args.steps, split_txt),
+                   "iters_per_pass": T, "pass_split": split,
                    "imax": imax, "jmax": jmax, "omega": 1.9, "problem": 2,
                    "decomposition": dims, "baseline_config": 4},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / PEAK_GBS, 4),
                      "traffic": traffic,
                      "traffic_ratio": round(traffic / hbm_min, 4) if traffic else None,
-                     "kernel": "rb_tb_kernel" if T > 1 else "rb_sweep_kernel",
+                     "kernel": ("rb_tbc_kernel" if chain else "rb_tb_kernel") if T > 1
+                     else "rb_sweep_kernel",
                      "iters_per_launch": round(iters_launch, 3), "kernel_ms": round(kern_ms, 4),
                      "bytes_per_launch": hbm_min,
                      "floors_ms": {"hbm": round(hbm_min / (PEAK_GBS * 1e9) * 1e3, 4),
-                                   "fp64_valu": round(fp64_floor_ms, 4)},
+                                   "fp64_valu": round(fp64_floor_ms, 4),
+                                   "fp64_ops_per_update": fp64_ops},
                      "iteration_equivalent": {
                          "GBs": round(iter_eq, 1), "per_lup_bytes": BYTES_PER_LUP,
                          "note": "24 B/LUP x iterations per launch / launch time; exceeds "
@@ -544,12 +593,12 @@ def main():
                        "transport": "RCCL send/recv (pack/unpack kernels) + ncclAllReduce",
                        "note": "max over ranks; overlap = 1 - (wall - sweep span) / comm time "
                                "per pass"}
-    if pmc.get("sq"):
+    if pmc_files:
+        out["roofline"]["traffic_source"] = pmc_files
+    if valu:
         # what actually bounds the temporally blocked kernel: VALU issue
         # (SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES per wave, 2 waves per SIMD)
-        out["roofline"]["valu"] = {"insts_per_launch": pmc["sq"].get("valu_insts"),
-                                   "valu_busy_per_wave": pmc["sq"].get("active_inst_valu"),
-                                   "source": "profiles PMC summary, same size and T"}
+        out["roofline"]["valu"] = valu
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline()

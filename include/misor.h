@@ -233,6 +233,12 @@ enum {
 int misor_set_tuning(misor_grid* g, int key, int value);
 int misor_get_tuning(const misor_grid* g, int key, int* value);
 
+/* diagnostics: with MISOR_CHAIN_TRACE=1 in the environment when the grid is
+ * configured, the per-block timeline of the last chained pass (3 words per
+ * block L = by * nbx + bx: start and end on the 100 MHz wall clock, workgroup
+ * | 1 << 32 for the first block of a run); *n = words available */
+int misor_chain_trace(misor_grid* g, unsigned long long* out, long long cap, long long* n);
+
 int misor_enable_timing(misor_grid* g, int on);
 int misor_get_stats(const misor_grid* g, misor_stats* out);
 int misor_reset_stats(misor_grid* g);

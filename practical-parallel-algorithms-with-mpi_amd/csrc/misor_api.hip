@@ -149,11 +149,24 @@ struct misor_grid {
     // blocks, 2: edge blocks of a pipelined decomposed pass), and two work
     // areas (parts 0 / 1, part 2: they run concurrently on two streams)
     bool tb_chain = true;
-    struct ChainPlan {
+    // (each plan: the list of the main kernel and of the edge kernel --
+    // columns at a physical left / right side, launched beside it on xstream)
+    struct ChainList {
         unsigned long long* tmpl = nullptr;
         int nseg0 = 0, blocks = 0;
+        int run[9] = {};  // XCD runs of the list
+    };
+    struct ChainPlan {
+        ChainList main, edge;
+        bool built = false;
     } chain_plan[kMaxT + 1][3];
-    int* tb_work[2] = {nullptr, nullptr};
+    int* tb_work[4] = {nullptr, nullptr, nullptr, nullptr};  // main / edge x parts 0-1 / 2
+    long long tb_work_bytes[4] = {0, 0, 0, 0};
+    hipStream_t xstream[2] = {nullptr, nullptr};  // edge kernels (parts 0-1 / 2)
+    hipEvent_t ev_fork[2] = {}, ev_join[2] = {};
+    // MISOR_CHAIN_TRACE=1: per-block timeline of the last chained pass (diagnostics)
+    unsigned long long* chain_trace = nullptr;
+    long long chain_trace_blocks = 0, chain_trace_last = 0;
 
     // reductions
     double* red_partials = nullptr;
@@ -268,8 +281,20 @@ void misor_destroy(misor_grid* g) {
     (void)hipFree(g->partials);
     (void)hipFree(g->tb_queue);
     for (auto& row : g->chain_plan)
-        for (auto& pl : row) (void)hipFree(pl.tmpl);
+        for (auto& pl : row) {
+            (void)hipFree(pl.main.tmpl);
+            (void)hipFree(pl.edge.tmpl);
+        }
     for (int* w : g->tb_work) (void)hipFree(w);
+    for (int k = 0; k < 2; ++k) {
+        if (g->xstream[k]) {
+            (void)hipStreamSynchronize(g->xstream[k]);
+            (void)hipStreamDestroy(g->xstream[k]);
+        }
+        if (g->ev_fork[k]) (void)hipEventDestroy(g->ev_fork[k]);
+        if (g->ev_join[k]) (void)hipEventDestroy(g->ev_join[k]);
+    }
+    (void)hipFree(g->chain_trace);
     (void)hipFree(g->st);
     (void)hipHostFree(g->st_host);
     (void)hipFree(g->red_partials);
@@ -667,108 +692,156 @@ static void tb_geometry(const misor_grid* g, int T, SweepParams& tp) {
     tp.nblocks = tp.nbx * tp.nby;
 }
 
-// The initial segment lists of the chained passes (sor_tb.h rb_tbc_kernel),
-// for every pass length 1..Te and part.  Blocks in a part: all (0), those whose
-// cone stays clear of the halo (1, sor_tb.h tb_block's test), the rest (2).
-// Along a column, blocks of steady-able rows (chain_rows_ok) form runs, each
-// split into segments of about B / G blocks (B: blocks of the part, G:
-// workgroups resident at once), so that the initial list gives every
+// The initial segment list of a chained pass (sor_tb.h rb_tbc_kernel) of Tp
+// iterations, part `part`, built on first use.  Blocks in a part: all (0),
+// those whose cone stays clear of the halo (1, sor_tb.h tb_block's test), the
+// rest (2).  Along a column, blocks of steady-able rows (chain_rows_ok) form
+// runs, each split into segments of about B / G blocks (B: blocks of the
+// part, G: workgroups resident at once), so that the initial list gives every
 // resident workgroup about one segment; every other block (cone at a
 // physical bottom / top side, a last block off the ring) is a segment of its
 // own.  The list is column-interleaved (segment s of every column, then s + 1
 // ...): the XCD queues deal contiguous runs of it, so neighbouring columns --
 // whose strips share 4T columns -- march side by side on one XCD.
-static int build_chain_plans(misor_grid* g, int Te) {
+static void drop_chain_plans(misor_grid* g) {
     for (auto& row : g->chain_plan)
         for (auto& pl : row) {
-            (void)hipFree(pl.tmpl);
+            (void)hipFree(pl.main.tmpl);
+            (void)hipFree(pl.edge.tmpl);
             pl = misor_grid::ChainPlan{};
         }
-    if (!chain_on(g, g->tp.variant)) return MISOR_OK;
-    long long most = 0;
-    for (int Tp = 1; Tp <= std::max(2, Te); ++Tp) {
-        SweepParams tp = g->tp;
-        tb_geometry(g, Tp, tp);
-        const int W = tb_waves(tp.variant), OW = tb_out_width(Tp, tp.variant);
-        const int S = tb_ring_slots(Tp, tp.variant);
-        const int nbx = tp.nbx, nby = tp.nby;
-        auto rows = [&](int by, int& j0, int& j1) {
-            j0 = 1 + by * tp.rows_per_block;
-            j1 = by == nby - 1 ? tp.nj + 1 : j0 + tp.rows_per_block;
-        };
-        auto interior = [&](int bx, int by) {
-            int j0, j1;
-            rows(by, j0, j1);
-            const int lo = 1 + bx * W * OW - 2 * Tp;
-            const int hi = 1 + (bx * W + W - 1) * OW - 2 * Tp + kStripCells - 1;
-            return lo >= tp.int_lo_i && hi <= tp.int_hi_i && j0 - 2 * Tp >= tp.int_lo_j &&
-                   j1 - 1 + 2 * Tp <= tp.int_hi_j;
-        };
-        auto steady = [&](int by) {  // sor_tb.h chain_rows_ok
-            int j0, j1;
-            rows(by, j0, j1);
-            return j0 - 2 * Tp >= tp.upd_lo_j && j1 - 1 + 2 * Tp <= tp.upd_hi_j &&
-                   (j1 - j0) % S == 0 && j1 > j0;
-        };
-        const int G = std::max(8, tb_resident(Tp, tp.variant));
-        for (int part = 0; part < (g->dist ? 3 : 1); ++part) {
-            auto in_part = [&](int bx, int by) {
-                return part == 0 || interior(bx, by) == (part == 1);
-            };
-            long long B = 0;
-            for (int bx = 0; bx < nbx; ++bx)
-                for (int by = 0; by < nby; ++by) B += in_part(bx, by);
-            const double per = std::max(1.0, (double)B / G);  // blocks per segment
-            std::vector<std::vector<unsigned long long>> col(nbx);
-            for (int bx = 0; bx < nbx; ++bx) {
-                for (int by = 0; by < nby;) {
-                    if (!in_part(bx, by)) {
-                        ++by;
-                        continue;
-                    }
-                    if (!steady(by)) {
-                        col[bx].push_back(chain_word(bx, by, by + 1));
-                        ++by;
-                        continue;
-                    }
-                    int e = by;
-                    while (e < nby && in_part(bx, e) && steady(e)) ++e;
-                    const int n = e - by;
-                    const int k = std::min(n, std::max(1, (int)llround(n / per)));
-                    for (int q = 0; q < k; ++q)
-                        col[bx].push_back(chain_word(bx, by + (int)((long long)n * q / k),
-                                                     by + (int)((long long)n * (q + 1) / k)));
-                    by = e;
-                }
+}
+
+static int chain_plan(misor_grid* g, int Tp, int part, const misor_grid::ChainPlan** out) {
+    auto& pl = g->chain_plan[Tp][part];
+    *out = &pl;
+    if (pl.built) return MISOR_OK;
+    SweepParams tp = g->tp;
+    tb_geometry(g, Tp, tp);
+    const int W = tb_waves(tp.variant), OW = tb_out_width(Tp, tp.variant);
+    const int S = tb_ring_slots(Tp, tp.variant);
+    const int nbx = tp.nbx, nby = tp.nby;
+    auto rows = [&](int by, int& j0, int& j1) {
+        j0 = 1 + by * tp.rows_per_block;
+        j1 = by == nby - 1 ? tp.nj + 1 : j0 + tp.rows_per_block;
+    };
+    auto interior = [&](int bx, int by) {
+        int j0, j1;
+        rows(by, j0, j1);
+        const int lo = 1 + bx * W * OW - 2 * Tp;
+        const int hi = 1 + (bx * W + W - 1) * OW - 2 * Tp + kStripCells - 1;
+        return lo >= tp.int_lo_i && hi <= tp.int_hi_i && j0 - 2 * Tp >= tp.int_lo_j &&
+               j1 - 1 + 2 * Tp <= tp.int_hi_j;
+    };
+    auto steady = [&](int by) {  // sor_tb.h chain_rows_ok
+        int j0, j1;
+        rows(by, j0, j1);
+        return j0 - 2 * Tp >= tp.upd_lo_j && j1 - 1 + 2 * Tp <= tp.upd_hi_j &&
+               (j1 - j0) % S == 0 && j1 > j0;
+    };
+    auto in_part = [&](int bx, int by) { return part == 0 || interior(bx, by) == (part == 1); };
+    // a column with a strip at a physical left / right side marches the
+    // general, lane-masked way (sor_tb.h chain_run's cols_in)
+    auto edge_col = [&](int bx) {
+        for (int w = 0; w < W; ++w) {
+            const int c_out = 1 + (bx * W + w) * OW;
+            if (c_out > tp.ni) break;
+            const int c_ld = c_out - 2 * Tp;
+            if (!(c_ld >= tp.upd_lo_i && c_ld + kStripCells - 1 <= tp.upd_hi_i &&
+                  (c_out + OW - 1 <= tp.ni || (tp.ni & 1) == 0)))
+                return true;
+        }
+        return false;
+    };
+    // Cost model, in steady-block units: a block of an edge column costs
+    // kChainEdgeCost (kSteadyEdge chunks), a block of a row that is not
+    // steady-able (a segment of its own) that much plus its 4T warm-up rows.
+    // The segments are cut so that each costs about (total / resident
+    // workgroups): every workgroup starts one at once and they end together.
+    const char* ec = getenv("MISOR_CHAIN_EDGE_COST");
+    const double E = ec && atof(ec) > 0 ? atof(ec) : kChainEdgeCost;
+    const int H = tp.rows_per_block;
+    std::vector<unsigned long long> singles;
+    double cost = 0;
+    long long Bm = 0, Be = 0;
+    for (int bx = 0; bx < nbx; ++bx) {
+        const bool ecol = edge_col(bx);
+        for (int by = 0; by < nby; ++by) {
+            if (!in_part(bx, by)) continue;
+            if (!steady(by)) {
+                singles.push_back(chain_word(bx, by, by + 1));
+                cost += E * (H + 4.0 * Tp) / H;
+                ++Bm;
+            } else {
+                cost += ecol ? E : 1.0;
+                ++(ecol ? Be : Bm);
             }
-            std::vector<unsigned long long> list;
-            for (size_t q = 0;; ++q) {
-                bool any = false;
-                for (int bx = 0; bx < nbx; ++bx)
-                    if (q < col[bx].size()) {
-                        list.push_back(col[bx][q]);
-                        any = true;
-                    }
-                if (!any) break;
-            }
-            auto& pl = g->chain_plan[Tp][part];
-            pl.nseg0 = (int)list.size();
-            pl.blocks = (int)B;
-            most = std::max(most, (long long)list.size());
-            if (list.empty()) continue;
-            if (hipMalloc(&pl.tmpl, list.size() * sizeof(unsigned long long)) != hipSuccess ||
-                hipMemcpy(pl.tmpl, list.data(), list.size() * sizeof(unsigned long long),
-                          hipMemcpyHostToDevice) != hipSuccess)
-                return fail(MISOR_ENOMEM, "chain plan allocation failed");
         }
     }
-    const size_t bytes = kChainHead * sizeof(int) + (most + kChainSegCap) * sizeof(unsigned long long);
-    for (int k = 0; k < (g->dist ? 2 : 1); ++k) {
-        (void)hipFree(g->tb_work[k]);
-        g->tb_work[k] = nullptr;
-        if (hipMalloc(&g->tb_work[k], bytes) != hipSuccess)
-            return fail(MISOR_ENOMEM, "chain work area allocation failed");
+    const int G = std::max(8, tb_resident(Tp, tp.variant));
+    const double per = std::max(1.0, cost / G);  // cost of one segment
+    std::vector<unsigned long long> edge, inner;  // inner: column-interleaved
+    std::vector<std::vector<unsigned long long>> col(nbx);
+    for (int bx = 0; bx < nbx; ++bx) {
+        const bool ecol = edge_col(bx);
+        const double c1 = ecol ? E : 1.0;
+        for (int by = 0; by < nby;) {
+            if (!in_part(bx, by) || !steady(by)) {
+                ++by;
+                continue;
+            }
+            int e = by;
+            while (e < nby && in_part(bx, e) && steady(e)) ++e;
+            const int n = e - by;
+            const int k = std::min(n, std::max(1, (int)llround(n * c1 / per)));
+            for (int q = 0; q < k; ++q) {
+                const unsigned long long w = chain_word(
+                    bx, by + (int)((long long)n * q / k), by + (int)((long long)n * (q + 1) / k));
+                if (ecol) edge.push_back(w);
+                else col[bx].push_back(w);
+            }
+            by = e;
+        }
     }
+    for (size_t q = 0;; ++q) {
+        bool any = false;
+        for (int bx = 0; bx < nbx; ++bx)
+            if (q < col[bx].size()) {
+                inner.push_back(col[bx][q]);
+                any = true;
+            }
+        if (!any) break;
+    }
+    // XCD runs: the main list -- singles dealt round-robin first, then the
+    // inner list in 8 contiguous parts; the edge list round-robin
+    auto upload = [&](misor_grid::ChainList& L, const std::vector<unsigned long long>* xl,
+                      long long blocks) -> int {
+        std::vector<unsigned long long> list;
+        for (int x = 0; x < 8; ++x) {
+            L.run[x] = (int)list.size();
+            list.insert(list.end(), xl[x].begin(), xl[x].end());
+        }
+        L.run[8] = (int)list.size();
+        L.nseg0 = (int)list.size();
+        L.blocks = (int)blocks;
+        if (list.empty()) return MISOR_OK;
+        if (hipMalloc(&L.tmpl, list.size() * sizeof(unsigned long long)) != hipSuccess ||
+            hipMemcpy(L.tmpl, list.data(), list.size() * sizeof(unsigned long long),
+                      hipMemcpyHostToDevice) != hipSuccess)
+            return fail(MISOR_ENOMEM, "chain plan allocation failed");
+        return MISOR_OK;
+    };
+    std::vector<unsigned long long> xm[8], xe[8];
+    for (size_t k = 0; k < singles.size(); ++k) xm[k % 8].push_back(singles[k]);
+    for (int x = 0; x < 8; ++x)
+        for (size_t k = inner.size() * x / 8; k < inner.size() * (x + 1) / 8; ++k)
+            xm[x].push_back(inner[k]);
+    for (size_t k = 0; k < edge.size(); ++k) xe[k % 8].push_back(edge[k]);
+    int rc = upload(pl.main, xm, Bm);
+    if (rc) return rc;
+    rc = upload(pl.edge, xe, Be);
+    if (rc) return rc;
+    pl.built = true;
     return MISOR_OK;
 }
 
@@ -801,9 +874,53 @@ static int configure_tb(misor_grid* g, int T, int variant, int rows) {
     }
     tb_geometry(g, std::max(2, Te), tp);
     g->tb_nparts = tp.nblocks;
-    int rc = ensure_partials(g, (int)need);
-    if (rc) return rc;
-    return build_chain_plans(g, Te);
+    drop_chain_plans(g);  // geometry changed: rebuilt on first use
+    if (chain_on(g, variant)) {
+        for (int k = 0; k < 2; ++k) {  // the edge kernels' streams
+            if (g->xstream[k]) continue;
+            int lo = 0, hi = 0;
+            (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+            if (hipStreamCreateWithPriority(&g->xstream[k], hipStreamNonBlocking, hi) !=
+                    hipSuccess ||
+                hipEventCreateWithFlags(&g->ev_fork[k], hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&g->ev_join[k], hipEventDisableTiming) != hipSuccess)
+                return fail(MISOR_EHIP, "edge stream creation failed");
+        }
+        // work areas (parts 0 / 1, part 2): head, an initial list of at most
+        // one segment per block, the dynamic slots; sized once for every pass
+        // length (a launch may still be using them when a plan is built)
+        long long most = 1;
+        for (int Tp = 1; Tp <= std::max(2, Te); ++Tp) {
+            SweepParams q = tp;
+            tb_geometry(g, Tp, q);
+            most = std::max(most, (long long)q.nblocks);
+        }
+        const long long bytes = kChainHead * (long long)sizeof(int) +
+                                (most + kChainSegCap) * (long long)sizeof(unsigned long long);
+        const char* et = getenv("MISOR_CHAIN_TRACE");
+        if (et && et[0] == '1' && most > g->chain_trace_blocks) {
+            (void)hipDeviceSynchronize();
+            (void)hipFree(g->chain_trace);
+            g->chain_trace = nullptr;
+            g->chain_trace_blocks = 0;
+            if (hipMalloc(&g->chain_trace, 3 * most * sizeof(unsigned long long)) != hipSuccess)
+                return fail(MISOR_ENOMEM, "chain trace allocation failed");
+            g->chain_trace_blocks = most;
+        }
+        for (int k = 0; k < 4; ++k) {
+            if (bytes <= g->tb_work_bytes[k]) continue;
+            if (g->tb_work[k]) {
+                (void)hipDeviceSynchronize();
+                (void)hipFree(g->tb_work[k]);
+            }
+            g->tb_work[k] = nullptr;
+            g->tb_work_bytes[k] = 0;
+            if (hipMalloc(&g->tb_work[k], bytes) != hipSuccess)
+                return fail(MISOR_ENOMEM, "chain work area allocation failed");
+            g->tb_work_bytes[k] = bytes;
+        }
+    }
+    return ensure_partials(g, (int)need);
 }
 
 int misor_create(misor_grid** out, const misor_desc* d) {
@@ -1360,7 +1477,7 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
     const int nparts = T == 1 ? g->nparts : g->tb_nparts;
     double* const rhs = g->fld[kRhs];
     auto pass = [&](hipStream_t s, int part, const double* src, double* dst, int Tp, int force,
-                    double* partials) {
+                    double* partials) -> int {
         if (T == 1) {
             SweepParams sp = g->sp;
             sp.part = part;
@@ -1376,21 +1493,46 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
             tp.reserve = part == 1 ? g->tb_reserve : 0;
             if (Tp != T) tb_geometry(g, Tp, tp);  // narrower cone: wider strips
             if (tp.chain) {  // chained runs, work stealing (parts 0 / 1 and 2 concurrently)
-                const auto& pl = g->chain_plan[Tp][part];
-                if (pl.blocks == 0) return;
-                tp.seg_tmpl = pl.tmpl;
-                tp.nseg0 = pl.nseg0;
+                const misor_grid::ChainPlan* pl = nullptr;
+                int rc = chain_plan(g, Tp, part, &pl);
+                if (rc) return rc;
+                const int k = part == 2 ? 1 : 0;
                 tp.seg_cap = kChainSegCap;
-                tp.chain_blocks = pl.blocks;
-                launch_tb(s, Tp, tp, src, dst, rhs, partials, g->st, force,
-                          g->tb_work[part == 2 ? 1 : 0]);
-                return;
+                tp.trace = part == 2 ? nullptr : g->chain_trace;
+                if (tp.trace) g->chain_trace_last = tp.nblocks;
+                auto use = [&](SweepParams& q, const misor_grid::ChainList& L) {
+                    q.seg_tmpl = L.tmpl;
+                    q.nseg0 = L.nseg0;
+                    q.chain_blocks = L.blocks;
+                    for (int x = 0; x < 9; ++x) q.seg_run[x] = L.run[x];
+                };
+                const int eg = pl->edge.nseg0;  // edge workgroups: one per initial segment
+                if (pl->edge.blocks > 0) {      // fork: the edge kernel beside the main one
+                    SweepParams te = tp;
+                    use(te, pl->edge);
+                    te.chain_edge = 1;
+                    te.reserve = std::max(0, tb_resident(Tp, tp.variant) - eg);
+                    HIPCHK(hipEventRecord(g->ev_fork[k], s));
+                    HIPCHK(hipStreamWaitEvent(g->xstream[k], g->ev_fork[k], 0));
+                    launch_tb(g->xstream[k], Tp, te, src, dst, rhs, partials, g->st, force,
+                              g->tb_work[2 + k]);
+                    HIPCHK(hipEventRecord(g->ev_join[k], g->xstream[k]));
+                }
+                if (pl->main.blocks > 0) {
+                    use(tp, pl->main);
+                    tp.chain_edge = 0;
+                    tp.reserve += pl->edge.blocks > 0 ? eg : 0;
+                    launch_tb(s, Tp, tp, src, dst, rhs, partials, g->st, force, g->tb_work[k]);
+                }
+                if (pl->edge.blocks > 0) HIPCHK(hipStreamWaitEvent(s, g->ev_join[k], 0));
+                return MISOR_OK;
             }
             // persistent work-queue launch on the grid stream (whole passes and
             // interior blocks); the boundary blocks of a split pass are few
             int* q = (g->tb_persistent && part != 2 && s == g->stream) ? g->tb_queue : nullptr;
             launch_tb(s, Tp, tp, src, dst, rhs, partials, g->st, force, q);
         }
+        return MISOR_OK;
     };
     const int cur0 = g->cur;
     long long launched = 0;  // passes enqueued
@@ -1472,14 +1614,20 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
             // waited on at the end of the previous iteration) and decide k-2
             if (k >= 2) HIPCHK(hipStreamWaitEvent(g->stream, g->ev_dk[k & 1], 0));
             if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b], g->stream));
-            pass(g->stream, 1, src, dst, Tk, 0, part);
+            {
+                int rc_ = pass(g->stream, 1, src, dst, Tk, 0, part);
+                if (rc_) return rc_;
+            }
             HIPCHK(hipEventRecord(g->ev_i[k & 1], g->stream));
             // edge blocks: after the interior blocks of pass k-1, the edge blocks
             // of k-1 (this stream) and the exchange of src's halo (which follows
             // decide k-2 on cstream)
             if (k >= 1) HIPCHK(hipStreamWaitEvent(g->estream, g->ev_i[(k - 1) & 1], 0));
             HIPCHK(hipStreamWaitEvent(g->estream, g->ev_x, 0));
-            pass(g->estream, 2, src, dst, Tk, 0, part);
+            {
+                int rc_ = pass(g->estream, 2, src, dst, Tk, 0, part);
+                if (rc_) return rc_;
+            }
             HIPCHK(hipEventRecord(g->ev_e, g->estream));
             // cstream: dst's halo for pass k+1, then the residual of pass k
             HIPCHK(hipStreamWaitEvent(g->cstream, g->ev_e, 0));
@@ -1524,9 +1672,15 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
             if (rc) return rc;
             HIPCHK(hipEventRecord(g->ev_x, g->cstream));
             if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b], g->stream));
-            pass(g->stream, 1, src, dst, Tk, 0, g->partials);
+            {
+                int rc_ = pass(g->stream, 1, src, dst, Tk, 0, g->partials);
+                if (rc_) return rc_;
+            }
             HIPCHK(hipStreamWaitEvent(g->stream, g->ev_x, 0));
-            pass(g->stream, 2, src, dst, Tk, 0, g->partials);
+            {
+                int rc_ = pass(g->stream, 2, src, dst, Tk, 0, g->partials);
+                if (rc_) return rc_;
+            }
             if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b + 1], g->stream));
             launch_finish(g->stream, g->partials, nparts_of(Tk), Tk, g->st, cells, 0);
             if (b == batch - 1) {  // close the batch: all-reduce + decide of the last one
@@ -1549,7 +1703,10 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
                 if (rc) return rc;
             }
             if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b], g->stream));
-            pass(g->stream, 0, src, dst, Tk, 0, g->partials);
+            {
+                int rc_ = pass(g->stream, 0, src, dst, Tk, 0, g->partials);
+                if (rc_) return rc_;
+            }
             if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b + 1], g->stream));
             if (g->dist) {
                 launch_finish(g->stream, g->partials, nparts_of(Tk), Tk, g->st, cells, 0);
@@ -1601,7 +1758,10 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
         // the last pass ran past the iteration that ended the loop: redo it
         // with T - over iterations from its source (untouched since)
         const double* src = pbuf(g, cur0 + passes - 1);
-        pass(g->stream, 0, src, pbuf(g, g->cur), t_of(passes - 1) - over, 1, g->partials);
+        {
+            int rc_ = pass(g->stream, 0, src, pbuf(g, g->cur), t_of(passes - 1) - over, 1, g->partials);
+            if (rc_) return rc_;
+        }
         HIPCHK(hipGetLastError());
     }
     g->comm_timing = false;
@@ -1921,6 +2081,20 @@ int misor_get_tuning(const misor_grid* g, int key, int* value) {
     case MISOR_TUNE_TB_RESERVE: *value = g->tb_reserve; return MISOR_OK;
     default: return fail(MISOR_EINVAL, "unknown tuning key %d", key);
     }
+}
+
+int misor_chain_trace(misor_grid* g, unsigned long long* out, long long cap, long long* n) {
+    if (!g || !n) return fail(MISOR_EINVAL, "null argument");
+    *n = 0;
+    if (!g->chain_trace) return MISOR_OK;
+    HIPCHK(hipSetDevice(g->device));
+    HIPCHK(hipDeviceSynchronize());
+    const long long m = std::min(cap, 3 * g->chain_trace_last);
+    if (out && m > 0)
+        HIPCHK(hipMemcpy(out, g->chain_trace, m * sizeof(unsigned long long),
+                         hipMemcpyDeviceToHost));
+    *n = 3 * g->chain_trace_last;
+    return MISOR_OK;
 }
 
 int misor_reset_stats(misor_grid* g) {

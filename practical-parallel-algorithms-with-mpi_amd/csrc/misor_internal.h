@@ -137,6 +137,11 @@ struct SweepParams {
     int nseg0;                // segments of the launch's initial list
     int seg_cap;              // dynamic segment slots (created by steals)
     int chain_blocks;         // blocks in the launch (its part)
+    int chain_edge;           // the edge list (strips at a physical left / right side)
+    int chain_grid;           // edge list: its workgroups (the first of the launch)
+    int seg_run[9];           // XCD x takes the initial segments [seg_run[x], seg_run[x+1])
+    unsigned long long* trace;  // diagnostics (MISOR_CHAIN_TRACE): per block L, 3 words --
+                                // start and end (wall clock, 100 MHz), workgroup | run start
     const unsigned long long* seg_tmpl;  // the initial list (device; copied per launch)
 };
 
@@ -149,6 +154,8 @@ constexpr unsigned long long kChainMask = (1ull << kChainBits) - 1;
 constexpr int kChainHead = 16;
 constexpr int kChainSegCap = 4096;       // dynamic slots per launch
 constexpr int kChainRingsPerBlock = 4;   // block height of a chained pass, in ring lengths
+constexpr double kChainEdgeCost = 1.3;   // a block of a column at a physical left / right
+                                         // side, in steady blocks (segment lengths)
 __host__ __device__ inline unsigned long long chain_word(int col, int next, int end) {
     return ((unsigned long long)col << (2 * kChainBits)) |
            ((unsigned long long)end << kChainBits) | (unsigned long long)next;

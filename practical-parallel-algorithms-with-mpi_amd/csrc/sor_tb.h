@@ -135,6 +135,7 @@ __device__ __forceinline__ double resid(double rhs, double a, double b, double i
 
 typedef double d2 __attribute__((ext_vector_type(2)));
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
+typedef unsigned v2u __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ d2 ldv(const double* p) { return *reinterpret_cast<const d2*>(p); }
 
@@ -179,7 +180,10 @@ struct Lane {
 //           physical bottom / top side, and a last block row whose height is
 //           not a multiple of the ring.  Row tests and ghost-row copies are
 //           wave-uniform; no lane masks.
-enum { kEdge = 0, kPre = 1, kSteady = 2, kRowEdge = 3 };
+//  kSteadyEdge rows interior, static ring (as kSteady), columns general:
+//           the lane masks and ghost-column copies of kEdge, no row tests.
+//           Strips at a physical left / right side in chained runs.
+enum { kEdge = 0, kPre = 1, kSteady = 2, kRowEdge = 3, kSteadyEdge = 4 };
 
 // One iteration stage (stage index t, 0-based).  In = row rin of the previous
 // stage's output (stage 0: of the field in memory).  Returns row rin-2 of this
@@ -194,8 +198,8 @@ __device__ __forceinline__ d2 stage(const Lane& c, int t, bool fixrows, d2 In, i
     // BP: x-neighbours through ds_bpermute instead of DPP (interior modes)
     auto fl = [&](double v) { return BP ? bperm(v, c.bl) : from_left(v); };
     auto fr = [&](double v) { return BP ? bperm(v, c.br) : from_right(v); };
-    constexpr bool EDGE = MODE == kEdge;                // lane masks
-    constexpr bool ROWS = EDGE || MODE == kRowEdge;     // row tests, ghost rows
+    constexpr bool EDGE = MODE == kEdge || MODE == kSteadyEdge;  // lane masks
+    constexpr bool ROWS = MODE == kEdge || MODE == kRowEdge;     // row tests, ghost rows
     if (ROWS && fixrows) {
         if (c.gb && rin == 1) {  // row 0 := row 1 (A holds row 0)
             if (!EDGE || c.up_a) A.x = In.x;
@@ -215,6 +219,9 @@ __device__ __forceinline__ d2 stage(const Lane& c, int t, bool fixrows, d2 In, i
     auto tally = [&](double r, int row, int wsh, bool own_col) {
         if (MODE == kSteady) {
             acc = __builtin_fma(r, r, acc);
+        } else if (MODE == kSteadyEdge) {
+            const double rm = own_col ? r : 0.0;  // select: no branch, NaN-safe
+            acc = __builtin_fma(rm, rm, acc);
         } else if (MODE == kPre) {
         } else {
             const bool own_row = row >= (c.wlo ? 1 : c.j0 + wsh) &&
@@ -372,6 +379,7 @@ struct Sio {
     __amdgpu_buffer_rsrc_t p, r, d;  // p rows from rs, rhs rows from rs-1, dst rows from j0
     unsigned lane;                   // lane * 16
     unsigned st_lane;                // lane * 16 if the lane stores, else out of range
+    unsigned st_a, st_b;             // kSteadyEdge: per column (lane * 16 (+ 8) or out of range)
     unsigned row_bytes;              // pitch * 8
 };
 
@@ -382,7 +390,7 @@ __device__ __forceinline__ d2 bload(__amdgpu_buffer_rsrc_t rs, unsigned voff, un
 // one step of the steady march: stream row r0 = rs + n, tally and store.  PH
 // = n mod S (a constant): rhs row rs - 1 + j lives in ring slot j mod S, and
 // stage t reads rows j = n - 2t (red) and n - 2t - 1 (black)
-template <int T, int D, int Q, int PH, bool BP, bool P2>
+template <int T, int D, int Q, int PH, bool BP, bool P2, bool EM = false>
 __device__ __forceinline__ void steady_step(March<T, D>& m, d2* R, const Lane& c, const Sio& io,
                                             int r0, unsigned off_n) {
     constexpr int S = ring_slots<T, D>();
@@ -395,14 +403,25 @@ __device__ __forceinline__ void steady_step(March<T, D>& m, d2* R, const Lane& c
     d2 v = m.Pq[0];
 #pragma unroll
     for (int t = 0; t < T; ++t) {
-        v = stage<T, Q, kSteady, BP, P2>(c, t, t > 0, v, r0 - 2 * t, m.A[t], m.M1[t], m.M2[t],
-                                 R[(PH - 2 * t + 4 * S) % S], R[(PH - 2 * t - 1 + 4 * S) % S],
-                                 m.acc[t]);
+        v = stage<T, Q, EM ? kSteadyEdge : kSteady, BP, P2>(
+            c, t, t > 0, v, r0 - 2 * t, m.A[t], m.M1[t], m.M2[t], R[(PH - 2 * t + 4 * S) % S],
+            R[(PH - 2 * t - 1 + 4 * S) % S], m.acc[t]);
     }
     // row r0 - 2T = j0 + (n - 4T): dst descriptor starts at row j0; lanes that
     // do not store carry an out-of-range offset (the write is dropped)
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), io.d, io.st_lane,
-                                           off_n - 4u * T * io.row_bytes, 2);
+    if (EM) {  // per column: owned cells and the physical ghost column
+        // (through scalar copies: clang's __builtin_bit_cast of a vector
+        // element lvalue, bit_cast(v2u, v.y), reads element 0 -- both stores
+        // then wrote v.x)
+        const double vx = v.x, vy = v.y;
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, vx), io.d, io.st_a,
+                                              off_n - 4u * T * io.row_bytes, 2);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, vy), io.d, io.st_b,
+                                              off_n - 4u * T * io.row_bytes, 2);
+    } else {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), io.d, io.st_lane,
+                                               off_n - 4u * T * io.row_bytes, 2);
+    }
     // The store reads its data VGPRs after it issues, and on gfx950 a later
     // buffer_load can land in those VGPRs first: with the registers of step
     // n's row reused by a load a few instructions after the store, lanes 12-15
@@ -421,13 +440,13 @@ __device__ __forceinline__ void steady_step(March<T, D>& m, d2* R, const Lane& c
 }
 
 // S steps of the steady march, the first at slot phase P0 (colour Q0)
-template <int T, int D, int Q0, int P0, bool BP, bool P2, int... NN>
+template <int T, int D, int Q0, int P0, bool BP, bool P2, bool EM = false, int... NN>
 __device__ __forceinline__ void steady_chunk(March<T, D>& m, d2* R, const Lane& c, const Sio& io,
                                              int r0, unsigned off_n,
                                              std::integer_sequence<int, NN...>) {
     constexpr int S = ring_slots<T, D>();
-    (steady_step<T, D, Q0 ^ (NN & 1), (P0 + NN) % S, BP, P2>(m, R, c, io, r0 + NN,
-                                                       off_n + (unsigned)NN * io.row_bytes),
+    (steady_step<T, D, Q0 ^ (NN & 1), (P0 + NN) % S, BP, P2, EM>(
+         m, R, c, io, r0 + NN, off_n + (unsigned)NN * io.row_bytes),
      ...);
 }
 
@@ -1039,9 +1058,10 @@ __device__ __forceinline__ void for_each_block(const SweepParams& prm, int* __re
 // Work: segments = ranges of block rows of one column, one 64-bit word each
 // (chain_word): the next unclaimed block row N, the end E (exclusive), the
 // column.  A launch starts from a host-built list of segments (about one per
-// resident workgroup), dealt to the XCDs in contiguous runs (neighbouring
-// columns share an XCD's L2: the strips' overlapping columns).  A workgroup
-// takes a segment by ticket and claims its blocks one by one
+// resident workgroup, misor_api.hip chain_plan), in one run per XCD (the
+// slow blocks first; neighbouring columns on one XCD share its L2: the
+// strips' overlapping columns).  A workgroup takes a segment by ticket and
+// claims its blocks one by one
 // (atomicAdd(word, 1): block N is its if N < E).  Once the tickets are gone it
 // steals: it scans the segments for the most unclaimed blocks r = E - N, and
 // takes the top r/2 with a compare-and-swap of (N, E) -> (N, E - r/2) (the
@@ -1085,21 +1105,20 @@ __device__ __forceinline__ unsigned long long chain_load(const unsigned long lon
 __device__ void chain_acquire(const SweepParams& prm, int* head, unsigned long long* seg,
                               int* sh) {
     const int lane = threadIdx.x & 63;
-    const int n0 = prm.nseg0, qq = n0 / 8, rr = n0 % 8;
-    auto run_start = [&](int x) { return x < rr ? x * (qq + 1) : rr * (qq + 1) + (x - rr) * qq; };
+    const int n0 = prm.nseg0;
     // 1. the initial segments, by ticket: the home XCD's run first
     int got = 0;
     if (lane == 0) {
         const int home = blockIdx.x % 8;
         for (int probe = 0; probe < 8;) {
             const int x = (home + probe) & 7;
-            const int cnt = x < rr ? qq + 1 : qq;
+            const int cnt = prm.seg_run[x + 1] - prm.seg_run[x];
             const int b = atomicAdd(&head[x], 1);
             if (b >= cnt) {
                 ++probe;
                 continue;
             }
-            const int k = run_start(x) + b;
+            const int k = prm.seg_run[x] + b;
             const unsigned long long old = atomicAdd(&seg[k], 1ull);
             if (chain_next(old) < chain_end(old)) {  // else stolen empty before its owner came
                 sh[0] = chain_col(old);
@@ -1196,6 +1215,15 @@ __device__ __forceinline__ int chain_block_end(const SweepParams& prm, double (&
         acc[t] = 0.0;
     }
     if (threadIdx.x == 0) {
+        if (prm.trace) {  // diagnostics: when this block began and ended, who ran it
+            const unsigned long long now = wall_clock64();
+            unsigned long long* tr = prm.trace + 3ll * L;
+            tr[0] = *reinterpret_cast<volatile unsigned long long*>(sh + 4);
+            tr[1] = now;
+            tr[2] = blockIdx.x | (sh[6] ? 1ull << 32 : 0ull);
+            *reinterpret_cast<volatile unsigned long long*>(sh + 4) = now;
+            sh[6] = 0;
+        }
         int nb = -1;
         if (slot >= 0) {
             const unsigned long long old = atomicAdd(seg + slot, 1ull);
@@ -1221,16 +1249,18 @@ __device__ __forceinline__ int chain_block_end(const SweepParams& prm, double (&
 }
 
 // One wave's chained run over its strip of column bx, from block row by
-// (the colour of the first streamed row: Q0): steady chunks (cols_in: every
-// block of the run is steady-able) or the general march (kEdge).  Every wave
-// of the workgroup calls chain_block_end at the same block ends.
-template <int T, int WAVES, int D, int Q0, bool P2>
+// (the colour of the first streamed row: Q0): steady chunks over the static
+// ring -- with the lane masks of a strip at a physical left / right side if
+// EM (kSteadyEdge) -- or, for a block row that is not steady-able (general;
+// such a block is a segment of its own), the general paired march (kEdge).
+// Every wave of the workgroup calls chain_block_end at the same block ends.
+template <int T, int WAVES, int D, int Q0, bool P2, bool EM>
 __device__ __forceinline__ void chain_strip(const SweepParams& prm, const double* __restrict__ src,
                                             double* __restrict__ dst,
                                             const double* __restrict__ rhs,
                                             double* __restrict__ partials, double (*wsum)[WAVES],
                                             int* sh, unsigned long long* seg, Lane& c,
-                                            const Io& io, bool cols_in, int c_ld, int bx, int by,
+                                            const Io& io, bool general, int c_ld, int bx, int by,
                                             int slot, int pend, int lane) {
     constexpr int S = ring_slots<T, D>();
     const long long pitch = prm.pitch;
@@ -1258,7 +1288,7 @@ __device__ __forceinline__ void chain_strip(const SweepParams& prm, const double
 #pragma unroll
     for (int k = 0; k < 2 * T; ++k) m.R[k] = d2{0.0, 0.0};
 
-    if (!cols_in) {  // a strip at a physical left / right side: pairs throughout
+    if (!EM && general) {  // rows not steady-able: the general march, block by block
         march_pairs<T, D, Q0, kEdge, false, P2>(m, c, io, rs, j1 - 1 + 2 * T);
         for (;;) {
             const int nb = chain_block_end<T, WAVES>(prm, m.acc, partials, by * prm.nbx + bx, wsum,
@@ -1279,8 +1309,12 @@ __device__ __forceinline__ void chain_strip(const SweepParams& prm, const double
                                                  (short)0, (int)((long long)rows * pitch * 8),
                                                  0x00020000);
     };
-    // 4T warm-up steps, then the static ring: rhs row rs - 1 + j in slot j mod S
-    march_pairs<T, D, Q0, kPre, false, P2>(m, c, io, rs, rs + 4 * T - 1);
+    // 4T warm-up steps, then the static ring: rhs row rs - 1 + j in slot j mod S.
+    // (kPre updates every column it streams: right for interior strips, whose
+    // garbage columns never reach an owned one; a strip at a physical side
+    // needs the masks and ghost-column copies of kEdge -- its rows are
+    // interior, so nothing is tallied or stored)
+    march_pairs<T, D, Q0, EM ? kEdge : kPre, false, P2>(m, c, io, rs, rs + 4 * T - 1);
     d2 R[S];
 #pragma unroll
     for (int k = 0; k < S; ++k) R[k] = d2{0.0, 0.0};
@@ -1300,18 +1334,20 @@ __device__ __forceinline__ void chain_strip(const SweepParams& prm, const double
             sio.d = rsrc(dst, j0, j1 - j0);
             sio.lane = (unsigned)lane * 16u;
             sio.st_lane = c.own_a ? (unsigned)lane * 16u : 0x40000000u;
+            sio.st_a = c.st_a ? (unsigned)lane * 16u : 0x40000000u;
+            sio.st_b = c.st_b ? (unsigned)lane * 16u + 8u : 0x40000000u;
             sio.row_bytes = (unsigned)(pitch * 8);
             constexpr int P0 = (4 * T) % S;
             int r0 = vrs + 4 * T;
             unsigned off = 4u * T * sio.row_bytes;
             for (int k = 0; k < (j1 - j0) / S; ++k) {
-                steady_chunk<T, D, Q0, P0, false, P2>(m, R, c, sio, r0, off,
-                                                     std::make_integer_sequence<int, S>{});
+                steady_chunk<T, D, Q0, P0, false, P2, EM>(m, R, c, sio, r0, off,
+                                                         std::make_integer_sequence<int, S>{});
                 r0 += S;
                 off += (unsigned)S * sio.row_bytes;
             }
         }
-        if (!c.own_a) {  // lanes that do not own their columns tallied garbage
+        if (!EM && !c.own_a) {  // lanes that do not own their columns tallied garbage
 #pragma unroll
             for (int t = 0; t < T; ++t) m.acc[t] = 0.0;
         }
@@ -1324,34 +1360,13 @@ __device__ __forceinline__ void chain_strip(const SweepParams& prm, const double
     }
 }
 
-// one run of a chained pass: column bx from block row by (all waves)
-template <int T, int WAVES, int D, bool P2>
-__device__ __forceinline__ void chain_run(const SweepParams& prm, const double* __restrict__ src,
-                                          double* __restrict__ dst, const double* __restrict__ rhs,
-                                          double* __restrict__ partials, double (*wsum)[WAVES],
-                                          int* sh, unsigned long long* seg, int bx, int by,
-                                          int slot, int pend) {
-    constexpr int OW = kStripCells - 4 * T;
-    const int lane = threadIdx.x & 63;
-    // wave-uniform (as known to the compiler: the strip's descriptors and
-    // branches derive from it)
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+// the per-lane constants and pointers of a strip
+template <int T>
+__device__ __forceinline__ void chain_lane(const SweepParams& prm, const double* src,
+                                           double* dst, const double* rhs, int c_ld, int lane,
+                                           Lane& c, Io& io) {
     const int ni = prm.ni;
-    const int c_out = 1 + (bx * WAVES + wave) * OW;
-    if (bx == 0 && by == 0) copy_corners(prm, src, dst);
-    if (c_out > ni) {  // no strip for this wave: only the block ends
-        double acc[T];
-#pragma unroll
-        for (int t = 0; t < T; ++t) acc[t] = 0.0;
-        for (;;) {
-            by = chain_block_end<T, WAVES>(prm, acc, partials, by * prm.nbx + bx, wsum, sh, seg,
-                                           slot, pend, by);
-            if (by < 0) return;
-        }
-    }
-    const int c_ld = c_out - 2 * T;
     const long long pitch = prm.pitch;
-    Lane c;
     c.ia = c_ld + 2 * lane;
     c.ib = c.ia + 1;
     c.up_a = c.ia >= prm.upd_lo_i && c.ia <= prm.upd_hi_i;
@@ -1376,7 +1391,44 @@ __device__ __forceinline__ void chain_run(const SweepParams& prm, const double* 
     c.bl = ((lane + 63) & 63) * 4;
     c.br = ((lane + 1) & 63) * 4;
     const long long base = (long long)kYOff * pitch + kXOff + c.ia;
-    Io io{src + base, rhs + base, dst + base, pitch};
+    io = Io{src + base, rhs + base, dst + base, pitch};
+}
+
+// one run of a chained pass: column bx from block row by (all waves).
+// EDGE = 0: the columns clear of the physical left / right sides (steady
+// chunks) and the blocks of non-steady rows (the general march); EDGE = 1:
+// the steady rows of the columns at a physical left / right side, every
+// strip in kSteadyEdge chunks.  The two are separate kernels (rb_tbc_kernel's
+// EDGE), launched side by side: one kernel with both kinds of steady chunks
+// makes the register allocator spill them at T = 8.
+template <int T, int WAVES, int D, bool P2, int EDGE>
+__device__ __forceinline__ void chain_run(const SweepParams& prm, const double* __restrict__ src,
+                                          double* __restrict__ dst, const double* __restrict__ rhs,
+                                          double* __restrict__ partials, double (*wsum)[WAVES],
+                                          int* sh, unsigned long long* seg, int bx, int by,
+                                          int slot, int pend) {
+    constexpr int OW = kStripCells - 4 * T;
+    const int lane = threadIdx.x & 63;
+    // wave-uniform (as known to the compiler: the strip's descriptors and
+    // branches derive from it)
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int ni = prm.ni;
+    const int c_out = 1 + (bx * WAVES + wave) * OW;
+    if (bx == 0 && by == 0) copy_corners(prm, src, dst);
+    if (c_out > ni) {  // no strip for this wave: only the block ends
+        double acc[T];
+#pragma unroll
+        for (int t = 0; t < T; ++t) acc[t] = 0.0;
+        for (;;) {
+            by = chain_block_end<T, WAVES>(prm, acc, partials, by * prm.nbx + bx, wsum, sh, seg,
+                                           slot, pend, by);
+            if (by < 0) return;
+        }
+    }
+    const int c_ld = c_out - 2 * T;
+    Lane c;
+    Io io;
+    chain_lane<T>(prm, src, dst, rhs, c_ld, lane, c, io);
     int j0, j1;
     block_rows(prm, by, j0, j1);
     // steady chunks for strips clear of the physical left / right sides, in
@@ -1387,32 +1439,55 @@ __device__ __forceinline__ void chain_run(const SweepParams& prm, const double* 
     // keeps those in segments of their own.  (A row-tested-only march for
     // the latter, kRowEdge, in the same kernel as the steady runs makes the
     // register allocator spill the runs' ring.)
-    const bool cols_in = c_ld >= prm.upd_lo_i && c_ld + kStripCells - 1 <= prm.upd_hi_i &&
-                         (c_out + OW - 1 <= ni || (ni & 1) == 0) &&
-                         chain_rows_ok<T, D>(prm, j0, j1);
+    // steady chunks in runs of steady-able block rows; the general
+    // lane-masked, row-tested march (kEdge) for the few block rows whose cone
+    // reaches a physical bottom / top side (or a column's last block of a
+    // height the ring does not divide) -- the host keeps those in segments
+    // of their own.  (A row-tested-only march for the latter, kRowEdge, in
+    // the same kernel as the steady runs makes the register allocator spill
+    // the runs' ring.)
+    const bool general = !chain_rows_ok<T, D>(prm, j0, j1);
     // the colour of the run's first streamed row: every block but a column's
     // last is an even number of rows tall, so the same at every block start
-    if (((prm.parity + j0 - 2 * T) & 1) != 0)
-        chain_strip<T, WAVES, D, 1, P2>(prm, src, dst, rhs, partials, wsum, sh, seg, c, io, cols_in,
-                                        c_ld, bx, by, slot, pend, lane);
-    else
-        chain_strip<T, WAVES, D, 0, P2>(prm, src, dst, rhs, partials, wsum, sh, seg, c, io, cols_in,
-                                        c_ld, bx, by, slot, pend, lane);
+    const bool q1 = ((prm.parity + j0 - 2 * T) & 1) != 0;
+    // (EDGE strips keep one row in flight, not D: the lane masks need the
+    // registers; the ring has the same S slots for D = 1 and 2)
+    static_assert(ring_slots<T, 1>() == ring_slots<T, D>(), "edge ring");
+    if constexpr (EDGE != 0) {  // kSteadyEdge for every strip
+        if (q1)
+            chain_strip<T, WAVES, 1, 1, P2, true>(prm, src, dst, rhs, partials, wsum, sh, seg, c,
+                                                  io, false, c_ld, bx, by, slot, pend, lane);
+        else
+            chain_strip<T, WAVES, 1, 0, P2, true>(prm, src, dst, rhs, partials, wsum, sh, seg, c,
+                                                  io, false, c_ld, bx, by, slot, pend, lane);
+    } else {  // (the host puts every column with a strip at a physical side in the EDGE list)
+        if (q1)
+            chain_strip<T, WAVES, D, 1, P2, false>(prm, src, dst, rhs, partials, wsum, sh, seg, c,
+                                                   io, general, c_ld, bx, by, slot, pend, lane);
+        else
+            chain_strip<T, WAVES, D, 0, P2, false>(prm, src, dst, rhs, partials, wsum, sh, seg, c,
+                                                   io, general, c_ld, bx, by, slot, pend, lane);
+    }
 }
 
 // chained persistent pass (2-column strips); work = the launch's work area
 // (int head[kChainHead], then the segment words; misor_api.hip chain plans)
-template <int T, int WAVES, int D, bool P2>
+template <int T, int WAVES, int D, bool P2, int EDGE = 0>
 __global__ __launch_bounds__(kLanes* WAVES, 2) void rb_tbc_kernel(
     SweepParams prm, const double* __restrict__ src, double* __restrict__ dst,
     const double* __restrict__ rhs, double* __restrict__ partials,
     const DevState* __restrict__ st, int force, int* __restrict__ work) {
     __shared__ double wsum[T][WAVES];
-    __shared__ int sh[4];
+    // sh[0..3]: the run (chain_acquire), sh[4..5]: trace clock, sh[6]: run start
+    __shared__ __attribute__((aligned(8))) int sh[8];
     if (!force && st->done) return;
     unsigned long long* seg = reinterpret_cast<unsigned long long*>(work + kChainHead);
     for (;;) {
         if (threadIdx.x < kLanes) chain_acquire(prm, work, seg, sh);
+        if (prm.trace && threadIdx.x == 0) {
+            *reinterpret_cast<volatile unsigned long long*>(sh + 4) = wall_clock64();
+            sh[6] = 1;
+        }
         __syncthreads();
         const int bx = __builtin_amdgcn_readfirstlane(sh[0]);
         const int by = __builtin_amdgcn_readfirstlane(sh[1]);
@@ -1420,7 +1495,8 @@ __global__ __launch_bounds__(kLanes* WAVES, 2) void rb_tbc_kernel(
         const int pend = __builtin_amdgcn_readfirstlane(sh[3]);
         __syncthreads();  // sh is rewritten by the run's block ends
         if (bx < 0) break;
-        chain_run<T, WAVES, D, P2>(prm, src, dst, rhs, partials, wsum, sh, seg, bx, by, slot, pend);
+        chain_run<T, WAVES, D, P2, EDGE>(prm, src, dst, rhs, partials, wsum, sh, seg, bx, by, slot,
+                                         pend);
     }
 }
 

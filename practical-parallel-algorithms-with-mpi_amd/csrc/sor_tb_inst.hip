@@ -29,10 +29,10 @@ static int resident2() {
     return n;
 }
 
-template <int T, int W, int D, bool P2>
+template <int T, int W, int D, bool P2, int E>
 static int resident_chain() {
     static int n = 0;
-    if (n == 0) n = persistent_grid(rb_tbc_kernel<T, W, D, P2>, kLanes * W);
+    if (n == 0) n = persistent_grid(rb_tbc_kernel<T, W, D, P2, E>, kLanes * W);
     return n;
 }
 
@@ -65,8 +65,14 @@ void MISOR_CAT(launch_tb_t, MISOR_TB_T)(hipStream_t s, const SweepParams& prm,
             hipLaunchKernelGGL(kernel, dim3(grid), dim3(kLanes * 4), 0, s, prm, src, dst, rhs,
                                partials, st, force, queue);
         };
-        if (prm.pow2) gc(rb_tbc_kernel<kT, 4, 2, true>, resident_chain<kT, 4, 2, true>());
-        else          gc(rb_tbc_kernel<kT, 4, 2, false>, resident_chain<kT, 4, 2, false>());
+        // main kernel, or the edge kernel (columns at a physical left / right side)
+        if (prm.chain_edge) {
+            if (prm.pow2) gc(rb_tbc_kernel<kT, 4, 2, true, 1>, resident_chain<kT, 4, 2, true, 1>());
+            else          gc(rb_tbc_kernel<kT, 4, 2, false, 1>, resident_chain<kT, 4, 2, false, 1>());
+        } else {
+            if (prm.pow2) gc(rb_tbc_kernel<kT, 4, 2, true, 0>, resident_chain<kT, 4, 2, true, 0>());
+            else          gc(rb_tbc_kernel<kT, 4, 2, false, 0>, resident_chain<kT, 4, 2, false, 0>());
+        }
         return;
     }
     auto go = [&](auto kernel, int threads, int resident) {

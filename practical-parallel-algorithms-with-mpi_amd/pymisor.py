@@ -112,6 +112,8 @@ SIGNATURES = {
     "misor_enable_timing": (C.c_int, [C.c_void_p, C.c_int]),
     "misor_get_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
     "misor_reset_stats": (C.c_int, [C.c_void_p]),
+    "misor_chain_trace": (C.c_int, [C.c_void_p, C.c_void_p, C.c_longlong,
+                                    C.POINTER(C.c_longlong)]),
     "misor3_decompose": (C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int),
                                    C.POINTER(C.c_int)]),
     "misor3_create": (C.c_int, [C.POINTER(C.c_void_p), C.POINTER(Desc3)]),
@@ -324,6 +326,19 @@ class Grid:
 
     def reset_stats(self):
         _check(lib().misor_reset_stats(self.h))
+
+    def chain_trace(self):
+        """per-block timeline of the last chained pass (MISOR_CHAIN_TRACE=1 at
+        configure time): array (blocks, 3) of start, end (100 MHz clock) and
+        workgroup | 1 << 32 for a run's first block; None if not traced"""
+        import numpy as np
+        n = C.c_longlong(0)
+        _check(lib().misor_chain_trace(self.h, None, 0, C.byref(n)))
+        if n.value == 0:
+            return None
+        out = np.zeros(n.value, dtype=np.uint64)
+        _check(lib().misor_chain_trace(self.h, out.ctypes.data, n.value, C.byref(n)))
+        return out.reshape(-1, 3)
 
 
 _PROBLEMS = {"dcavity": PROBLEM_DCAVITY, "canal": PROBLEM_CANAL}

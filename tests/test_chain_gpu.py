@@ -74,17 +74,33 @@ def test_chain_res_deterministic_and_equal_to_unchained(T):
 
 @pytest.mark.parametrize("T", [2, 7, 8])
 def test_chain_converges_mid_pass(T):
-    """convergence inside a chained pass: the pass is recomputed with fewer
-    iterations; count and p are solveRB's"""
-    ni, nj = 700, 1900
-    p, rhs = orc.poisson_init(ni, nj)
-    want = p.copy()
-    eps = 2e-3
+    """convergence inside a chained pass: eps is put between the residual of
+    iteration ks (not a multiple of T) and the smallest one before it (the
+    oracle's residual sequence), so solveRB stops at ks, inside a pass; the
+    pass is recomputed with fewer iterations, and count and p are solveRB's"""
+    ni, nj = 260, 1100
+    rng = np.random.default_rng(T + 11)
+    # scaled so every residual is < 1 (solveRB's loop starts from res = 1.0)
+    p0 = rng.standard_normal((nj + 2, ni + 2)) * 2.0 ** -30
+    rhs = np.zeros_like(p0)
+    res = {}
+    q = p0.copy()
+    for k in range(1, 40):  # one iteration at a time: res[k] after k iterations
+        res[k] = orc.solve_rb(q, rhs, 1.0 / ni, 1.0 / nj, 1.9, 1e-300, 1)[1]
+    for ks in range(2 * T + 1, 40):
+        lo = min(res[k] for k in range(1, ks))
+        if res[ks] < lo * (1 - 1e-6) and ks % T:
+            break
+    else:
+        pytest.skip("no strictly decreasing residual step in range")
+    eps = ((res[ks] + lo) / 2) ** 0.5
+    want = p0.copy()
     it_ref, res_ref = orc.solve_rb(want, rhs, 1.0 / ni, 1.0 / nj, 1.9, eps, 100000)
-    it, res, got, _ = run(p, rhs, 1.0 / ni, 1.0 / nj, 100000, T, omega=1.9, eps=eps, rows=54)
+    assert it_ref == ks
+    it, r, got, _ = run(p0, rhs, 1.0 / ni, 1.0 / nj, 100000, T, omega=1.9, eps=eps, rows=36)
     assert it == it_ref
     assert np.array_equal(got, want)
-    assert abs(res - res_ref) <= 1e-12 * res_ref
+    assert abs(r - res_ref) <= 1e-12 * res_ref
 
 
 def test_chain_rings_env(monkeypatch):

@@ -3,6 +3,8 @@
 
     python tools/pmc_summary.py gpurun_out/prof_<tag> profiles/r01_pmc_tb7_32768.json \
         --size 32768 --iters 7 [--kernel rb_tb_kernel]
+    python tools/pmc_summary.py gpurun_out/prof_<tag> profiles/r03_pmc_tb{T}_32768.json \
+        --size 32768 --iters all      (one summary per pass length found)
 
 HBM bytes per launch, corrected as MI355X_MICROARCH.md prescribes for gfx950:
 FETCH_SIZE (KB) x 1024 x 2 (it tallies 128-B requests at 64 B) + WRITE_SIZE (KB)
@@ -14,6 +16,7 @@ import csv
 import glob
 import json
 import os
+import re
 
 
 def rows(d, prefix, kernel):
@@ -21,7 +24,7 @@ def rows(d, prefix, kernel):
     for path in glob.glob(os.path.join(d, "**", prefix + "*counter_collection.csv"),
                           recursive=True):
         for r in csv.DictReader(open(path)):
-            if kernel in r["Kernel_Name"]:
+            if re.search(kernel, r["Kernel_Name"]):
                 out.setdefault(r["Counter_Name"], []).append(
                     (r["Kernel_Name"], int(r["Dispatch_Id"]), float(r["Counter_Value"])))
     return out
@@ -37,17 +40,32 @@ def main():
     ap.add_argument("out")
     ap.add_argument("--size", type=int, default=32768)
     ap.add_argument("--nranks", type=int, default=1)
-    ap.add_argument("--iters", type=int, required=True)
+    ap.add_argument("--iters", required=True,
+                    help="iterations per pass of the launches to summarise, or 'all'")
     ap.add_argument("--kernel", default=None,
-                    help="kernel name substring (default: rb_tb_kernel<ITERS, -- only the "
-                         "full passes, not the warm-up or remainder instantiations)")
+                    help="kernel name regex (default: the temporally blocked kernels, chained "
+                         "rb_tbc_kernel or not, of ITERS iterations -- only full passes)")
     ap.add_argument("--rows", type=int, default=0)
     a = ap.parse_args()
-    if a.kernel is None:
-        a.kernel = "rb_tb_kernel<%d," % a.iters
-    f = rows(a.dir, "fetch", a.kernel)
-    w = rows(a.dir, "write", a.kernel)
-    s = rows(a.dir, "sq", a.kernel)
+    if a.iters == "all":
+        ts = set()
+        for path in glob.glob(os.path.join(a.dir, "**", "fetch*counter_collection.csv"),
+                              recursive=True):
+            for r in csv.DictReader(open(path)):
+                m = re.search(r"rb_tbc?_kernel<(\d+),", r["Kernel_Name"])
+                if m:
+                    ts.add(int(m.group(1)))
+        for t in sorted(ts):
+            summarise(a, t, a.out.replace("{T}", str(t)))
+    else:
+        summarise(a, int(a.iters), a.out)
+
+
+def summarise(a, iters, path_out):
+    kernel = a.kernel or r"rb_tbc?_kernel<%d," % iters
+    f = rows(a.dir, "fetch", kernel)
+    w = rows(a.dir, "write", kernel)
+    s = rows(a.dir, "sq", kernel)
     # full-iteration launches only (a capped solve's last pass may run fewer)
     fetch = f["FETCH_SIZE"]
     write = w["WRITE_SIZE"]
@@ -55,14 +73,15 @@ def main():
     wr = mean(write) * 1024
     cells = float(a.size) * a.size / a.nranks
     hbm_min = 24 * cells
+    kname = fetch[0][0].split("(")[0].replace("void ", "")
     out = {
-        "size": a.size, "nranks": a.nranks, "iters_per_pass": a.iters,
-        "kernel": fetch[0][0].split("(")[0].replace("void ", ""),
+        "size": a.size, "nranks": a.nranks, "iters_per_pass": iters,
+        "kernel": kname, "chain": "rb_tbc_kernel" in kname,
         "rows_per_block": a.rows or None, "launches": len(fetch),
         "fetch_size_kb_raw": mean(fetch), "write_size_kb": mean(write),
         "read_bytes_corrected": rd, "write_bytes": wr, "bytes_per_launch": rd + wr,
         "hbm_minimum_bytes_per_launch": hbm_min,
-        "algorithmic_bytes_per_launch": hbm_min * a.iters,
+        "algorithmic_bytes_per_launch": hbm_min * iters,
         "ratio_to_hbm_minimum": (rd + wr) / hbm_min,
     }
     if s:
@@ -75,12 +94,15 @@ def main():
                 sq[name] = round(mean(s[k]) / cyc, 3)
         if "SQ_INSTS_VALU" in s:
             sq["valu_insts"] = mean(s["SQ_INSTS_VALU"])
+            # lane-instructions per owned cell update (64 lanes per wave instruction)
+            sq["valu_lane_insts_per_update"] = round(mean(s["SQ_INSTS_VALU"]) * 64 /
+                                                     (cells * iters), 2)
         out["sq"] = sq
     out["note"] = ("one launch = %d solveRB iterations (temporally blocked); FETCH_SIZE x1024 x2 "
                    "(gfx950 correction, MI355X_MICROARCH.md HBM) + WRITE_SIZE x1024; separate "
                    "rocprofv3 --pmc passes (tools/profile_bench.sh); the HBM minimum of a launch "
-                   "is 24 B x cells (p, rhs read once, p written once)" % a.iters)
-    json.dump(out, open(a.out, "w"), indent=1)
+                   "is 24 B x cells (p, rhs read once, p written once)" % iters)
+    json.dump(out, open(path_out, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
 

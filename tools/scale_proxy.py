@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--variants", default="-1", help="TB variants to try (-1: default)")
     ap.add_argument("--remap", default="1", help="XCD-aware block remap settings to try")
     ap.add_argument("--persistent", default="1", help="work-queue launch settings to try")
+    ap.add_argument("--chain", default="1", help="chained-pass settings to try (TUNE_TB_CHAIN)")
     ap.add_argument("--reserve", default="16",
                     help="slots a pipelined interior launch leaves free (--comm), settings to try")
     ap.add_argument("--no-timing", action="store_true", help="no per-pass HIP events (wall only)")
@@ -58,10 +59,11 @@ def main():
         dist.init_process_group("nccl", init_method="tcp://127.0.0.1:29533", rank=0,
                                 world_size=1, device_id=torch.device("cuda", 0))
         dist.barrier()
-    combos = [(int(t), int(v), int(r), int(x), int(pp), int(rv)) for t in args.tsteps.split(",")
+    combos = [(int(t), int(v), int(r), int(x), int(pp), int(rv), int(ch))
+              for t in args.tsteps.split(",")
               for v in args.variants.split(",") for r in args.rows.split(",")
               for x in args.remap.split(",") for pp in args.persistent.split(",")
-              for rv in args.reserve.split(",")]
+              for rv in args.reserve.split(",") for ch in args.chain.split(",")]
     base = args.base_ms or None
     print("%-2s %-12s %2s %2s %5s %10s %10s %10s %6s" % (
         "N", "local", "T", "v", "rows", "ms/iter", "wall/iter", "MLUP/s/GPU", "eff"), flush=True)
@@ -88,7 +90,8 @@ def main():
         hrow = {}
         for _ in range(args.rounds):
             for c in combos:
-                T, v, r, x, pp, rv = c
+                T, v, r, x, pp, rv, ch = c
+                g.set_tuning(M.TUNE_TB_CHAIN, ch)
                 g.set_tuning(M.TUNE_TB_PERSISTENT, pp)
                 g.set_tuning(M.TUNE_TB_RESERVE, rv)
                 g.set_tuning(M.TUNE_XCD_REMAP, x)
@@ -107,7 +110,7 @@ def main():
                 res[c][0].append(st["sweep_ms"] / max(st["timed_sweeps"], 1))
                 res[c][1].append(wall * 1e3 / args.sweeps)
         for c in combos:
-            T, v, r, x, pp, rv = c
+            T, v, r, x, pp, rv, ch = c
             ms = float(np.median(res[c][0]))
             wall = float(np.median(res[c][1]))
             if ms <= 0:  # --no-timing: wall clock only
@@ -117,8 +120,8 @@ def main():
                 base = ms * N
             eff = base / (N * ms)
             print("%-2d %-12s %2d %2d %5d %10.4f %10.4f %10.0f %6.3f  remap=%d persistent=%d "
-                  "reserve=%d" % (N, "%dx%d" % (ni, nj), T, v, hrow[c], ms, wall, mlups, eff, x,
-                                  pp, rv), flush=True)
+                  "reserve=%d chain=%d" % (N, "%dx%d" % (ni, nj), T, v, hrow[c], ms, wall, mlups,
+                                           eff, x, pp, rv, ch), flush=True)
         g.close()
 
 

@@ -389,6 +389,102 @@ def run_ns3d(args, world, rank, local_rank, dist, torch):
     return out
 
 
+def run_poisson_local(args, N):
+    """The decomposed leg of the headline bench with N in-process ranks on ONE
+    GPU (libmisor's LOCAL: transport, host threads of this process): the same
+    Grid code, pass loop and comm timing as N processes over RCCL, so the
+    N > 1 JSON line (comm block, overlap) is produced and checked where only
+    one GPU exists.  Not a scaling measurement (the ranks share the GPU).
+    --check: the gathered p after the timed solve against a 1-rank solve of
+    the same iterations, bit for bit."""
+    import threading
+
+    import numpy as np
+    import pymisor as M
+
+    n = args.size
+    pdims = list(M.decompose(N, 0, 1 << 20, 1 << 20).dims) if args.scaling == "weak" else [1, 1]
+    imax, jmax = n * pdims[0], n * pdims[1]
+    cid = ("LOCAL:bench%d" % os.getpid()).encode()
+    bar = threading.Barrier(N)
+    res = [None] * N
+    err = []
+    total_iters = max(args.warmup, 1) + 2 * args.steps
+
+    def body(r):
+        try:
+            g = M.Grid(imax, jmax, 1.0 / n, 1.0 / n, 1.9, 1e-300, args.steps, device=0,
+                       nranks=N, rank=r, comm_id=cid)
+            if args.tsteps > 0:
+                g.set_tuning(M.TUNE_TSTEPS, args.tsteps)
+            g.poisson_init(float(pdims[0]), float(pdims[1]), 2)
+            g.solve_rb(itermax=max(args.warmup, 1))
+            g.solve_rb(itermax=args.steps)
+            g.enable_timing(True)
+            g.reset_stats()
+            g.synchronize()
+            bar.wait()
+            t0 = time.perf_counter()
+            it, _ = g.solve_rb(itermax=args.steps)
+            g.synchronize()
+            bar.wait()
+            el = time.perf_counter() - t0
+            st = g.stats()
+            p = g.gather(M.P) if args.check else None
+            res[r] = dict(it=it, el=el, st=st, p=p, dims=tuple(g.loc.dims),
+                          cells=g.loc.ni * g.loc.nj, T=st["iters_per_pass"])
+            g.close()
+        except BaseException as e:  # surfaced in the main thread
+            err.append((r, repr(e)))
+            bar.abort()
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(N)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if err:
+        raise RuntimeError("local ranks failed: %s" % err)
+    assert all(x["it"] == args.steps for x in res)
+    elapsed = max(x["el"] for x in res)
+    passes = max(max(x["st"]["timed_passes"], 1) for x in res)
+    kern_ms = max(x["st"]["sweep_ms"] / max(x["st"]["timed_passes"], 1) for x in res)
+    halo = max(x["st"]["halo_ms"] / max(x["st"]["halos"], 1) for x in res)
+    ared = max(x["st"]["allreduce_ms"] / max(x["st"]["allreduces"], 1) for x in res)
+    comm = max((x["st"]["halo_ms"] + x["st"]["allreduce_ms"]) / passes for x in res)
+    wall = elapsed * 1e3 / passes
+    exposed = max(0.0, wall - kern_ms)
+    out = {
+        "metric": "red-black SOR MLUP/s + % HBM roofline at 1/2/4/8 MI355X, 32768^2 grid",
+        "value": round(float(imax) * jmax * args.steps / elapsed / 1e6, 1),
+        "unit": "MLUP/s", "n_gpus": 1, "local_ranks": N, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (assignment-4 problem-2 fields, generated on device)",
+        "config": {"workload": "2D Poisson red-black SOR (solveRB), %dx%d interior cells, %d "
+                               "in-process ranks on ONE GPU (plumbing check of the decomposed "
+                               "path; not a scaling number)" % (imax, jmax, N),
+                   "imax": imax, "jmax": jmax, "decomposition": "%dx%d" % res[0]["dims"],
+                   "iters_per_pass": res[0]["T"], "baseline_config": 4},
+        "comm": {"halo_ms_per_exchange": round(halo, 4), "allreduce_ms_per_call": round(ared, 4),
+                 "sweep_ms_per_pass": round(kern_ms, 4), "wall_ms_per_pass": round(wall, 4),
+                 "comm_ms_per_pass": round(comm, 4),
+                 "overlap": round(1.0 - min(1.0, exposed / comm), 3) if comm > 0 else None,
+                 "transport": "in-process LOCAL: device copies + events (stands in for RCCL)",
+                 "note": "max over ranks; overlap = 1 - (wall - sweep span) / comm time per pass"},
+    }
+    if args.check:
+        with M.Grid(imax, jmax, 1.0 / n, 1.0 / n, 1.9, 1e-300, total_iters, device=0) as g1:
+            if args.tsteps > 0:
+                g1.set_tuning(M.TUNE_TSTEPS, args.tsteps)
+            g1.poisson_init(float(pdims[0]), float(pdims[1]), 2)
+            it1, _ = g1.solve_rb(itermax=total_iters)
+            ref = g1.download(M.P)
+        same = bool(np.array_equal(res[0]["p"], ref)) and it1 == total_iters
+        out["check"] = {"iterations": total_iters, "p_bit_identical_to_1_rank": same}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -408,6 +504,11 @@ def main():
                     help="poisson: strong (default: the --size^2 grid split over the GPUs, "
                          "BASELINE config 4) or weak (--size^2 cells per GPU: the global grid "
                          "is the process grid times --size^2, same spacing 1/--size)")
+    ap.add_argument("--local-ranks", type=int, default=0,
+                    help="poisson, one process: N in-process ranks on this one GPU (the "
+                         "decomposed path's plumbing; not a scaling measurement)")
+    ap.add_argument("--check", action="store_true",
+                    help="with --local-ranks: gathered p bit for bit against one rank")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -438,6 +539,11 @@ def main():
             dist.destroy_process_group()
         if rank == 0:
             print(json.dumps(out), flush=True)
+        return
+
+    if args.local_ranks > 1 and world == 1:
+        out = run_poisson_local(args, args.local_ranks)
+        print(json.dumps(out), flush=True)
         return
 
     import pymisor as M

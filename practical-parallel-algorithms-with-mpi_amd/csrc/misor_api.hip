@@ -647,6 +647,12 @@ static bool chain_on(const misor_grid* g, int variant) {
     return g->tb_chain && g->tb_persistent && variant == kDefaultTbVariant;
 }
 
+// residual partials per stage of a pass: one per block, or one per block and
+// wave for a chained pass (sor_tb.h chain_block_end)
+static int tb_parts(const SweepParams& tp) {
+    return tp.chain ? tp.nblocks * tb_waves(tp.variant) : tp.nblocks;
+}
+
 static void tb_geometry(const misor_grid* g, int T, SweepParams& tp) {
     const int nj = g->loc.nj, req = g->tb_rows_req;
     tp.nbx = tb_nbx(g->loc.ni, T, tp.variant);
@@ -870,10 +876,10 @@ static int configure_tb(misor_grid* g, int T, int variant, int rows) {
         if ((q.rows_per_block + 4LL * kMaxT + 8) * tp.pitch * 8 >= (1LL << 30))
             return fail(MISOR_EINVAL, "tb rows %d: a block of rows exceeds 1 GiB",
                         q.rows_per_block);
-        need = std::max(need, (long long)Tp * q.nblocks);
+        need = std::max(need, (long long)Tp * tb_parts(q));
     }
     tb_geometry(g, std::max(2, Te), tp);
-    g->tb_nparts = tp.nblocks;
+    g->tb_nparts = tb_parts(tp);
     drop_chain_plans(g);  // geometry changed: rebuilt on first use
     if (chain_on(g, variant)) {
         for (int k = 0; k < 2; ++k) {  // the edge kernels' streams
@@ -1507,24 +1513,46 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
                     for (int x = 0; x < 9; ++x) q.seg_run[x] = L.run[x];
                 };
                 const int eg = pl->edge.nseg0;  // edge workgroups: one per initial segment
-                if (pl->edge.blocks > 0) {      // fork: the edge kernel beside the main one
-                    SweepParams te = tp;
-                    use(te, pl->edge);
-                    te.chain_edge = 1;
-                    te.reserve = std::max(0, tb_resident(Tp, tp.variant) - eg);
+                // Where the two kernels run.  Default (3): the main kernel forked to
+                // xstream, the edge kernel on s.  The other way round (0: edge on
+                // xstream, launched first; 1: launched after the main one) the edge
+                // kernel's 16-odd workgroups did not start until the main kernel's
+                // workgroups retired, in every pass of a multi-pass solve but the
+                // first, though its slots were free (profiles/r03_chain_xmode.txt:
+                // 8.5-8.9 ms per 32768^2 pass against 6.0); 2: both on s, serialised.
+                // MISOR_CHAIN_XMODE: experiments.
+                static const int xmode = [] {
+                    const char* e = getenv("MISOR_CHAIN_XMODE");
+                    return e ? atoi(e) : 3;
+                }();
+                SweepParams te = tp;
+                use(te, pl->edge);
+                te.chain_edge = 1;
+                te.reserve = std::max(0, tb_resident(Tp, tp.variant) - eg);
+                SweepParams tm = tp;
+                use(tm, pl->main);
+                tm.chain_edge = 0;
+                tm.reserve += pl->edge.blocks > 0 ? eg : 0;
+                const bool has_e = pl->edge.blocks > 0, has_m = pl->main.blocks > 0;
+                // (no edge list: the main kernel alone, on s)
+                const bool fork = has_e && has_m && xmode != 2;
+                hipStream_t es = fork && xmode != 3 ? g->xstream[k] : s;
+                hipStream_t ms = fork && xmode == 3 ? g->xstream[k] : s;
+                if (fork) {
                     HIPCHK(hipEventRecord(g->ev_fork[k], s));
                     HIPCHK(hipStreamWaitEvent(g->xstream[k], g->ev_fork[k], 0));
-                    launch_tb(g->xstream[k], Tp, te, src, dst, rhs, partials, g->st, force,
-                              g->tb_work[2 + k]);
+                }
+                auto launch_e = [&]() {
+                    launch_tb(es, Tp, te, src, dst, rhs, partials, g->st, force, g->tb_work[2 + k]);
+                };
+                if (has_e && xmode != 1) launch_e();
+                if (has_m)
+                    launch_tb(ms, Tp, tm, src, dst, rhs, partials, g->st, force, g->tb_work[k]);
+                if (has_e && xmode == 1) launch_e();
+                if (fork) {
                     HIPCHK(hipEventRecord(g->ev_join[k], g->xstream[k]));
+                    HIPCHK(hipStreamWaitEvent(s, g->ev_join[k], 0));
                 }
-                if (pl->main.blocks > 0) {
-                    use(tp, pl->main);
-                    tp.chain_edge = 0;
-                    tp.reserve += pl->edge.blocks > 0 ? eg : 0;
-                    launch_tb(s, Tp, tp, src, dst, rhs, partials, g->st, force, g->tb_work[k]);
-                }
-                if (pl->edge.blocks > 0) HIPCHK(hipStreamWaitEvent(s, g->ev_join[k], 0));
                 return MISOR_OK;
             }
             // persistent work-queue launch on the grid stream (whole passes and
@@ -1583,7 +1611,7 @@ int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
         if (T == 1 || Tk == T) return nparts;
         SweepParams tp = g->tp;
         tb_geometry(g, Tk, tp);
-        return tp.nblocks;
+        return tb_parts(tp);
     };
     // iterations covered by the first p passes, and the passes that cover `it`
     auto covered = [&](long long p) -> long long {

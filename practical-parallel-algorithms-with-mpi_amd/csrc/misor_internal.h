@@ -154,8 +154,12 @@ constexpr unsigned long long kChainMask = (1ull << kChainBits) - 1;
 constexpr int kChainHead = 16;
 constexpr int kChainSegCap = 4096;       // dynamic slots per launch
 constexpr int kChainRingsPerBlock = 4;   // block height of a chained pass, in ring lengths
-constexpr double kChainEdgeCost = 1.3;   // a block of a column at a physical left / right
-                                         // side, in steady blocks (segment lengths)
+constexpr double kChainEdgeCost = 2.0;   // a block of a column at a physical left / right
+                                         // side, in steady blocks (segment lengths): a
+                                         // kSteadyEdge block measures ~1.5; the edge
+                                         // kernel's workgroups cannot steal from the main
+                                         // one's, so it is given a few more than its share
+                                         // (profiles/r03_chain_edge_cost.txt)
 __host__ __device__ inline unsigned long long chain_word(int col, int next, int end) {
     return ((unsigned long long)col << (2 * kChainBits)) |
            ((unsigned long long)end << kChainBits) | (unsigned long long)next;

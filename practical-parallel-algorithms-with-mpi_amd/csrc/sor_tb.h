@@ -1100,8 +1100,9 @@ __device__ __forceinline__ unsigned long long chain_load(const unsigned long lon
 }
 
 // The run a workgroup takes next, into sh[0..3] = column, block row, segment
-// slot (-1: a private range), end of a private range; sh[0] = -1: no work
-// left.  Wave 0 only.
+// slot (-1: a private range), end of the blocks it owns (own_end); sh[8] =
+// the blocks its segment had unclaimed; sh[0] = -1: no work left.  Wave 0
+// only.
 __device__ void chain_acquire(const SweepParams& prm, int* head, unsigned long long* seg,
                               int* sh) {
     const int lane = threadIdx.x & 63;
@@ -1124,7 +1125,8 @@ __device__ void chain_acquire(const SweepParams& prm, int* head, unsigned long l
                 sh[0] = chain_col(old);
                 sh[1] = chain_next(old);
                 sh[2] = k;
-                sh[3] = 0;
+                sh[3] = chain_next(old) + 1;  // blocks claimed: the first
+                sh[8] = chain_end(old) - chain_next(old);
                 got = 1;
                 break;
             }
@@ -1181,12 +1183,14 @@ __device__ void chain_acquire(const SweepParams& prm, int* head, unsigned long l
                     sh[0] = chain_col(w);
                     sh[1] = m;
                     sh[2] = -1;
-                    sh[3] = E;
+                    sh[3] = E;  // a private range: all its blocks are the thief's
+                    sh[8] = E - m;
                     if (E - m >= 2) {  // the rest of the stolen range becomes stealable
                         const int d = atomicAdd(&head[8], 1);
                         if (d < prm.seg_cap) {
                             atomicExch(seg + n0 + d, chain_word(chain_col(w), m + 1, E));
                             sh[2] = n0 + d;
+                            sh[3] = m + 1;  // stealable: blocks claimed one by one
                         }
                     }
                     ok = 1;
@@ -1199,53 +1203,54 @@ __device__ void chain_acquire(const SweepParams& prm, int* head, unsigned long l
     }
 }
 
-// End of block L of a run: the block's residual partials (as block_partials),
-// then the claim of the run's next block.  Returns its block row, or -1.
+// End of block L of a run: the block's residual partials, one per wave and
+// stage at fixed slots (partials[(t * nblocks + L) * WAVES + wave]: no
+// barrier), then the run's next block.  The owner of a segment claims its
+// blocks a few at a time (sh[8]: the unclaimed blocks it saw at its last
+// claim; k = that / 8, 1..4), so most block ends need no atomic and no
+// barrier: own_end (wave-uniform, the same in every wave) is the end of the
+// blocks already claimed.  Returns the next block row, or -1.
 template <int T, int WAVES>
 __device__ __forceinline__ int chain_block_end(const SweepParams& prm, double (&acc)[T],
-                                               double* partials, int L, double (*wsum)[WAVES],
-                                               int* sh, unsigned long long* seg, int slot,
-                                               int pend, int by) {
+                                               double* partials, int L, int* sh,
+                                               unsigned long long* seg, int slot, int by,
+                                               int& own_end) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
+    double mine = 0.0;
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         const double s = wave_sum(acc[t]);
-        if (lane == 0) wsum[t][wave] = s;
+        if (lane == t) mine = s;
         acc[t] = 0.0;
     }
+    if (lane < T)
+        partials[((long long)lane * prm.nblocks + L) * WAVES + wave] = mine;
+    if (threadIdx.x == 0 && prm.trace) {  // diagnostics: when this block began and ended, who ran it
+        const unsigned long long now = wall_clock64();
+        unsigned long long* tr = prm.trace + 3ll * L;
+        tr[0] = *reinterpret_cast<volatile unsigned long long*>(sh + 4);
+        tr[1] = now;
+        tr[2] = blockIdx.x | (sh[6] ? 1ull << 32 : 0ull);
+        *reinterpret_cast<volatile unsigned long long*>(sh + 4) = now;
+        sh[6] = 0;
+    }
+    if (by + 1 < own_end) return by + 1;
+    if (slot < 0) return -1;  // a private range: own_end is its end
+    __syncthreads();  // every wave has read the last claim
     if (threadIdx.x == 0) {
-        if (prm.trace) {  // diagnostics: when this block began and ended, who ran it
-            const unsigned long long now = wall_clock64();
-            unsigned long long* tr = prm.trace + 3ll * L;
-            tr[0] = *reinterpret_cast<volatile unsigned long long*>(sh + 4);
-            tr[1] = now;
-            tr[2] = blockIdx.x | (sh[6] ? 1ull << 32 : 0ull);
-            *reinterpret_cast<volatile unsigned long long*>(sh + 4) = now;
-            sh[6] = 0;
-        }
-        int nb = -1;
-        if (slot >= 0) {
-            const unsigned long long old = atomicAdd(seg + slot, 1ull);
-            if (chain_next(old) < chain_end(old)) nb = chain_next(old);
-        } else if (by + 1 < pend) {
-            nb = by + 1;
-        }
-        sh[1] = nb;
+        const int k = min(4, max(1, sh[8] / 8));
+        const unsigned long long old = atomicAdd(seg + slot, (unsigned long long)k);
+        const int N = chain_next(old), E = chain_end(old);
+        sh[1] = N < E ? N : -1;
+        sh[7] = min(N + k, E);
+        sh[8] = E - N;
     }
     __syncthreads();
-    if (threadIdx.x < T) {
-        const int t = threadIdx.x;
-        double s = 0.0;
-#pragma unroll
-        for (int w = 0; w < WAVES; ++w) s += wsum[t][w];
-        partials[(long long)t * prm.nblocks + L] = s;
-    }
     // wave-uniform (the buffer descriptors and row offsets of the next block
     // derive from it: they must be scalars)
-    const int nb = __builtin_amdgcn_readfirstlane(sh[1]);
-    __syncthreads();  // wsum and sh are rewritten at the next block end
-    return nb;
+    own_end = __builtin_amdgcn_readfirstlane(sh[7]);
+    return __builtin_amdgcn_readfirstlane(sh[1]);
 }
 
 // One wave's chained run over its strip of column bx, from block row by
@@ -1261,7 +1266,7 @@ __device__ __forceinline__ void chain_strip(const SweepParams& prm, const double
                                             double* __restrict__ partials, double (*wsum)[WAVES],
                                             int* sh, unsigned long long* seg, Lane& c,
                                             const Io& io, bool general, int c_ld, int bx, int by,
-                                            int slot, int pend, int lane) {
+                                            int slot, int own_end, int lane) {
     constexpr int S = ring_slots<T, D>();
     const long long pitch = prm.pitch;
     int j0, j1;
@@ -1291,8 +1296,8 @@ __device__ __forceinline__ void chain_strip(const SweepParams& prm, const double
     if (!EM && general) {  // rows not steady-able: the general march, block by block
         march_pairs<T, D, Q0, kEdge, false, P2>(m, c, io, rs, j1 - 1 + 2 * T);
         for (;;) {
-            const int nb = chain_block_end<T, WAVES>(prm, m.acc, partials, by * prm.nbx + bx, wsum,
-                                                     sh, seg, slot, pend, by);
+            const int nb = chain_block_end<T, WAVES>(prm, m.acc, partials, by * prm.nbx + bx, sh,
+                                                     seg, slot, by, own_end);
             if (nb < 0) return;
             by = nb;
             block_rows(prm, by, j0, j1);
@@ -1351,8 +1356,8 @@ __device__ __forceinline__ void chain_strip(const SweepParams& prm, const double
 #pragma unroll
             for (int t = 0; t < T; ++t) m.acc[t] = 0.0;
         }
-        const int nb = chain_block_end<T, WAVES>(prm, m.acc, partials, by * prm.nbx + bx, wsum,
-                                                 sh, seg, slot, pend, by);
+        const int nb = chain_block_end<T, WAVES>(prm, m.acc, partials, by * prm.nbx + bx, sh, seg,
+                                                 slot, by, own_end);
         if (nb < 0) return;
         by = nb;
         block_rows(prm, by, j0, j1);
@@ -1406,7 +1411,7 @@ __device__ __forceinline__ void chain_run(const SweepParams& prm, const double* 
                                           double* __restrict__ dst, const double* __restrict__ rhs,
                                           double* __restrict__ partials, double (*wsum)[WAVES],
                                           int* sh, unsigned long long* seg, int bx, int by,
-                                          int slot, int pend) {
+                                          int slot, int own_end) {
     constexpr int OW = kStripCells - 4 * T;
     const int lane = threadIdx.x & 63;
     // wave-uniform (as known to the compiler: the strip's descriptors and
@@ -1420,8 +1425,8 @@ __device__ __forceinline__ void chain_run(const SweepParams& prm, const double* 
 #pragma unroll
         for (int t = 0; t < T; ++t) acc[t] = 0.0;
         for (;;) {
-            by = chain_block_end<T, WAVES>(prm, acc, partials, by * prm.nbx + bx, wsum, sh, seg,
-                                           slot, pend, by);
+            by = chain_block_end<T, WAVES>(prm, acc, partials, by * prm.nbx + bx, sh, seg, slot,
+                                           by, own_end);
             if (by < 0) return;
         }
     }
@@ -1456,17 +1461,17 @@ __device__ __forceinline__ void chain_run(const SweepParams& prm, const double* 
     if constexpr (EDGE != 0) {  // kSteadyEdge for every strip
         if (q1)
             chain_strip<T, WAVES, 1, 1, P2, true>(prm, src, dst, rhs, partials, wsum, sh, seg, c,
-                                                  io, false, c_ld, bx, by, slot, pend, lane);
+                                                  io, false, c_ld, bx, by, slot, own_end, lane);
         else
             chain_strip<T, WAVES, 1, 0, P2, true>(prm, src, dst, rhs, partials, wsum, sh, seg, c,
-                                                  io, false, c_ld, bx, by, slot, pend, lane);
+                                                  io, false, c_ld, bx, by, slot, own_end, lane);
     } else {  // (the host puts every column with a strip at a physical side in the EDGE list)
         if (q1)
             chain_strip<T, WAVES, D, 1, P2, false>(prm, src, dst, rhs, partials, wsum, sh, seg, c,
-                                                   io, general, c_ld, bx, by, slot, pend, lane);
+                                                   io, general, c_ld, bx, by, slot, own_end, lane);
         else
             chain_strip<T, WAVES, D, 0, P2, false>(prm, src, dst, rhs, partials, wsum, sh, seg, c,
-                                                   io, general, c_ld, bx, by, slot, pend, lane);
+                                                   io, general, c_ld, bx, by, slot, own_end, lane);
     }
 }
 
@@ -1477,12 +1482,16 @@ __global__ __launch_bounds__(kLanes* WAVES, 2) void rb_tbc_kernel(
     SweepParams prm, const double* __restrict__ src, double* __restrict__ dst,
     const double* __restrict__ rhs, double* __restrict__ partials,
     const DevState* __restrict__ st, int force, int* __restrict__ work) {
-    __shared__ double wsum[T][WAVES];
-    // sh[0..3]: the run (chain_acquire), sh[4..5]: trace clock, sh[6]: run start
-    __shared__ __attribute__((aligned(8))) int sh[8];
+    __shared__ double wsum[T][WAVES];  // (unused by the chained march: per-wave partials)
+    // sh[0..3]: the run (chain_acquire), sh[4..5]: trace clock, sh[6]: run start,
+    // sh[7]: own_end of the last claim, sh[8]: unclaimed blocks seen then
+    __shared__ __attribute__((aligned(8))) int sh[12];
     if (!force && st->done) return;
     unsigned long long* seg = reinterpret_cast<unsigned long long*>(work + kChainHead);
     for (;;) {
+        // every wave has read the last claim of the previous run (a run's
+        // last block end can leave the waves apart: no barrier on its way out)
+        __syncthreads();
         if (threadIdx.x < kLanes) chain_acquire(prm, work, seg, sh);
         if (prm.trace && threadIdx.x == 0) {
             *reinterpret_cast<volatile unsigned long long*>(sh + 4) = wall_clock64();
@@ -1492,11 +1501,11 @@ __global__ __launch_bounds__(kLanes* WAVES, 2) void rb_tbc_kernel(
         const int bx = __builtin_amdgcn_readfirstlane(sh[0]);
         const int by = __builtin_amdgcn_readfirstlane(sh[1]);
         const int slot = __builtin_amdgcn_readfirstlane(sh[2]);
-        const int pend = __builtin_amdgcn_readfirstlane(sh[3]);
+        const int own_end = __builtin_amdgcn_readfirstlane(sh[3]);
         __syncthreads();  // sh is rewritten by the run's block ends
         if (bx < 0) break;
         chain_run<T, WAVES, D, P2, EDGE>(prm, src, dst, rhs, partials, wsum, sh, seg, bx, by, slot,
-                                         pend);
+                                         own_end);
     }
 }
 

@@ -75,6 +75,29 @@ def main():
         le.min(), np.percentile(le, 10), np.median(le), np.percentile(le, 90), le.max()))
     print("busy fraction of the span: mean %.3f min %.3f" % (b.mean() / (span * 10e-6),
                                                            b.min() / (span * 10e-6)))
+    # runs: per workgroup, its blocks in time order; a run = a first block and
+    # the chained ones after it
+    order = np.lexsort((st, wg))
+    runs = []
+    cur = None
+    for i in order:
+        if first[i] or cur is None or cur[0] != wg[i]:
+            if cur is not None:
+                runs.append(cur)
+            cur = [wg[i], st[i], 0]
+        cur[2] += 1
+    runs.append(cur)
+    rl = np.array([r[2] for r in runs])
+    rs = np.array([r[1] for r in runs]) * 10e-6
+    late = rs > 0.05 * span * 10e-6
+    print("runs: %d; blocks per run: initial median %.0f, stolen median %.0f p10 %.0f p90 %.0f; "
+          "steals started at (ms) p10 %.3f median %.3f p90 %.3f max %.3f" % (
+              len(runs), np.median(rl[~late]) if (~late).any() else 0,
+              np.median(rl[late]) if late.any() else 0,
+              np.percentile(rl[late], 10) if late.any() else 0,
+              np.percentile(rl[late], 90) if late.any() else 0,
+              *(np.percentile(rs[late], [10, 50, 90]).tolist() + [rs.max()] if late.any()
+                else [0, 0, 0, 0])))
     # active workgroups over time (20 bins)
     edges = np.linspace(0, span, 21)
     act = []

@@ -226,9 +226,11 @@ enum {
                                     * interior launch leaves to the exchange / all-reduce /
                                     * edge-block streams (default 16) */
     MISOR_TUNE_TB_CHAIN = 13       /* temporally blocked kernel, persistent, default variant:
-                                    * 1 (default) = chained vertical runs of short blocks
-                                    * with work stealing (no warm-up rows between the blocks
-                                    * of a run); 0 = one block per work item */
+                                    * 1 = chained vertical runs of short blocks with work
+                                    * stealing (no warm-up rows between the blocks of a
+                                    * run); 0 = one block per work item; -1 (default) =
+                                    * chained on local blocks below 2^28 cells.  Get: 1 if
+                                    * chained passes are in effect */
 };
 int misor_set_tuning(misor_grid* g, int key, int value);
 int misor_get_tuning(const misor_grid* g, int key, int* value);

@@ -148,7 +148,7 @@ struct misor_grid {
     // segment list of every pass length and part (0: whole pass, 1: interior
     // blocks, 2: edge blocks of a pipelined decomposed pass), and two work
     // areas (parts 0 / 1, part 2: they run concurrently on two streams)
-    bool tb_chain = true;
+    int tb_chain = -1;  // 1 on, 0 off, -1 automatic: on for local blocks below kChainCells
     // (each plan: the list of the main kernel and of the edge kernel --
     // columns at a physical left / right side, launched beside it on xstream)
     struct ChainList {
@@ -644,7 +644,9 @@ static int pick_tb_rows(int ni, int nj, int T, int variant) {
 // dropped.  An explicit request gives uniform blocks of that height, the last
 // row taking the rest.
 static bool chain_on(const misor_grid* g, int variant) {
-    return g->tb_chain && g->tb_persistent && variant == kDefaultTbVariant;
+    const bool want = g->tb_chain > 0 ||
+                      (g->tb_chain < 0 && (long long)g->loc.ni * g->loc.nj < kChainCells);
+    return want && g->tb_persistent && variant == kDefaultTbVariant;
 }
 
 // residual partials per stage of a pass: one per block, or one per block and
@@ -1118,8 +1120,10 @@ int misor_create(misor_grid** out, const misor_desc* d) {
         e = getenv("MISOR_NS_FUSE");  // A/B switch (bench.py --workload ns)
         g->ns_fuse = !(e && e[0] == '0');
     }
-    const int T0 = (long long)g->loc.ni * g->loc.nj >= kTsteps8Cells ? kDefaultTsteps
-                                                                      : kSmallBlockTsteps;
+    // T: 8 on large local blocks; on small ones 8 with chained passes (the
+    // default there), 7 without (misor_internal.h)
+    const long long cells = (long long)g->loc.ni * g->loc.nj;
+    const int T0 = cells >= kTsteps8Cells || g->tb_chain != 0 ? kDefaultTsteps : kSmallBlockTsteps;
     if (configure_tb(g, T0, kDefaultTbVariant, 0) != MISOR_OK)
         CREATE_FAIL(MISOR_ENOMEM, "%s", g_err.c_str());
     if (hipStreamSynchronize(g->stream) != hipSuccess)
@@ -2079,7 +2083,7 @@ int misor_set_tuning(misor_grid* g, int key, int value) {
         g->tb_persistent = value != 0;
         return configure_tb(g, g->tsteps, g->tp.variant, g->tb_rows_req);
     case MISOR_TUNE_TB_CHAIN:
-        g->tb_chain = value != 0;
+        g->tb_chain = value < 0 ? -1 : value != 0;
         return configure_tb(g, g->tsteps, g->tp.variant, g->tb_rows_req);
     case MISOR_TUNE_NS_FUSE: g->ns_fuse = value != 0; return MISOR_OK;
     case MISOR_TUNE_FINISH2: g->finish2 = value != 0; return MISOR_OK;
@@ -2103,7 +2107,7 @@ int misor_get_tuning(const misor_grid* g, int key, int* value) {
     case MISOR_TUNE_TB_VARIANT: *value = g->tp.variant; return MISOR_OK;
     case MISOR_TUNE_TB_ROWS: *value = g->tp.rows_per_block; return MISOR_OK;
     case MISOR_TUNE_TB_PERSISTENT: *value = g->tb_persistent; return MISOR_OK;
-    case MISOR_TUNE_TB_CHAIN: *value = g->tb_chain; return MISOR_OK;
+    case MISOR_TUNE_TB_CHAIN: *value = chain_on(g, g->tp.variant); return MISOR_OK;
     case MISOR_TUNE_NS_FUSE: *value = g->ns_fuse; return MISOR_OK;
     case MISOR_TUNE_FINISH2: *value = g->finish2; return MISOR_OK;
     case MISOR_TUNE_TB_RESERVE: *value = g->tb_reserve; return MISOR_OK;

@@ -154,6 +154,12 @@ constexpr unsigned long long kChainMask = (1ull << kChainBits) - 1;
 constexpr int kChainHead = 16;
 constexpr int kChainSegCap = 4096;       // dynamic slots per launch
 constexpr int kChainRingsPerBlock = 4;   // block height of a chained pass, in ring lengths
+// chained passes by default on local blocks below this many cells: there the
+// unchained blocks are short and their 4T warm-up rows cost most (one 8-GPU
+// rank's 8192 x 16384 of the 32768^2 bench: 0.106 vs 0.110-0.118 ms per
+// iteration); on larger blocks the unchained 576-row blocks are ahead
+// (32768^2: 0.661 vs 0.695-0.709; profiles/r03_chain_rows.txt)
+constexpr long long kChainCells = 1LL << 28;
 constexpr double kChainEdgeCost = 2.0;   // a block of a column at a physical left / right
                                          // side, in steady blocks (segment lengths): a
                                          // kSteadyEdge block measures ~1.5; the edge

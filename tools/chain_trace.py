@@ -33,6 +33,7 @@ def main():
     ni, nj = (int(x) for x in a.shape.split("x"))
     g = M.Grid(ni, nj, 1.0 / a.size, 1.0 / a.size, 1.9, 1e-300, a.T * a.per_solve, device=0)
     g.poisson_init(1.0, 1.0, 2)
+    g.set_tuning(M.TUNE_TB_CHAIN, 1)
     g.set_tuning(M.TUNE_TSTEPS, a.T)
     if a.rows:
         g.set_tuning(M.TUNE_TB_ROWS, a.rows)
@@ -87,6 +88,28 @@ def main():
             cur = [wg[i], st[i], 0]
         cur[2] += 1
     runs.append(cur)
+    # block durations by position in the run and by column kind
+    pos = np.zeros(len(st), dtype=np.int64)
+    prev_w, k = None, 0
+    for i in order:
+        k = 0 if (first[i] or wg[i] != prev_w) else k + 1
+        pos[i] = k
+        prev_w = wg[i]
+    nbx = int(np.ceil(ni / (4 * (128 - 4 * a.T))))
+    col = np.arange(len(st)) % nbx
+    edge = (col == 0) | (col == nbx - 1)
+    print("block us by position in run: %s; edge columns median %.1f, others %.1f" % (
+        ", ".join("%d: %.1f (p90 %.1f, n %d)" % (q, np.median(dur[pos == q]),
+                                                 np.percentile(dur[pos == q], 90),
+                                                 (pos == q).sum())
+                  for q in range(4) if (pos == q).any()) +
+        ", 4+: %.1f (p90 %.1f)" % (np.median(dur[pos >= 4]), np.percentile(dur[pos >= 4], 90)),
+        np.median(dur[edge]), np.median(dur[~edge])))
+    # durations over time (when in the pass a block ran)
+    tb = np.linspace(0, span, 11)
+    print("median block us per 10%% of the span (non-edge, chained): %s" % " ".join(
+        "%.0f" % np.median(dur[(st >= tb[q]) & (st < tb[q + 1]) & ~edge & ~first])
+        if ((st >= tb[q]) & (st < tb[q + 1]) & ~edge & ~first).any() else "-" for q in range(10)))
     rl = np.array([r[2] for r in runs])
     rs = np.array([r[1] for r in runs]) * 10e-6
     late = rs > 0.05 * span * 10e-6

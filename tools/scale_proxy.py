@@ -38,7 +38,8 @@ def main():
     ap.add_argument("--variants", default="-1", help="TB variants to try (-1: default)")
     ap.add_argument("--remap", default="1", help="XCD-aware block remap settings to try")
     ap.add_argument("--persistent", default="1", help="work-queue launch settings to try")
-    ap.add_argument("--chain", default="1", help="chained-pass settings to try (TUNE_TB_CHAIN)")
+    ap.add_argument("--chain", default="-1",
+                    help="chained-pass settings to try (TUNE_TB_CHAIN; -1: automatic)")
     ap.add_argument("--reserve", default="16",
                     help="slots a pipelined interior launch leaves free (--comm), settings to try")
     ap.add_argument("--no-timing", action="store_true", help="no per-pass HIP events (wall only)")

@@ -245,13 +245,27 @@ __device__ __forceinline__ double g_val(const FgArgs& a, const Uv3& S, const Uv3
     return vc + a.dt * (a.inverseRe * (dv2dx2 + dv2dy2) - duvdx - dv2dy + a.gy);
 }
 
-__global__ __launch_bounds__(kTx* kTy) void fg_rhs_kernel(CLay u, CLay v, Lay f, Lay g, Lay rhs,
-                                                          int ni, int nj, FgArgs a, int wl,
-                                                          int wr, int wb, int wt) {
-    const int i = 1 + blockIdx.x * kTx + threadIdx.x;
-    const int j0 = 1 + (blockIdx.y * kTy + threadIdx.y) * kFgBand;
+// Workgroups of kFgW columns (4 waves side by side) x one band of kFgRows
+// rows, dealt to the XCDs in contiguous runs of the row-major block order:
+// the workgroups an XCD runs at once are horizontal neighbours, so the lines
+// at a wave's column edges (u(i-2..i-1), u(i+1), v(i+-1)) and the band's 4
+// overlap rows come from its L2.  (Round 2's 64 x 4-band workgroups, dealt
+// round-robin, fetched those neighbour lines from HBM: reads 1.68x the
+// algorithmic 16 B/cell, profiles/r03_pmc_ns16384_base.json.)
+constexpr int kFgW = 256, kFgRows = 64;
+
+__global__ __launch_bounds__(kFgW) void fg_rhs_kernel(CLay u, CLay v, Lay f, Lay g, Lay rhs,
+                                                      int ni, int nj, FgArgs a, int wl, int wr,
+                                                      int wb, int wt, int nbx, int nblocks) {
+    // XCD-aware block order: workgroup w runs on XCD w % 8; XCD x takes the
+    // blocks [x nblocks / 8, (x + 1) nblocks / 8) in order
+    const int w = blockIdx.x, x = w & 7, k = w >> 3;
+    const int L = (int)((long long)nblocks * x / 8) + k;
+    if (L >= (int)((long long)nblocks * (x + 1) / 8)) return;
+    const int i = 1 + (L % nbx) * kFgW + threadIdx.x;
+    const int j0 = 1 + (L / nbx) * kFgRows;
     if (i > ni || j0 > nj) return;
-    const int j1 = min(nj, j0 + kFgBand - 1);
+    const int j1 = min(nj, j0 + kFgRows - 1);
     const bool has_fl = i > 1 || wl;  // F(i-1, j) is local (F(0, j) = U(0, j) on a left wall)
     Uv3 S, C, N;
     double gprev;
@@ -304,14 +318,17 @@ __global__ __launch_bounds__(kTx* kTy) void fg_rhs_kernel(CLay u, CLay v, Lay f,
 
 void launch_compute_fg_rhs(const NsLaunch& L, const double* u, const double* v, double* f,
                            double* g, double* rhs) {
-    const int bands = (L.nj + kFgBand - 1) / kFgBand;
-    dim3 grid((L.ni + kTx - 1) / kTx, (bands + kTy - 1) / kTy);
+    const int nbx = (L.ni + kFgW - 1) / kFgW, nby = (L.nj + kFgRows - 1) / kFgRows;
+    const int nblocks = nbx * nby;
+    // every XCD run has at most ceil(nblocks / 8) blocks: 8 x that many workgroups
+    const int grid = 8 * ((nblocks + 7) / 8);
     const NsParams& P = L.prm;
     FgArgs a{P.dt, 1.0 / P.re, 1.0 / P.dx, 1.0 / P.dy, P.gamma, P.gx, P.gy,
              1.0 / P.dx, 1.0 / P.dy, 1.0 / P.dt};
-    hipLaunchKernelGGL(fg_rhs_kernel, grid, dim3(kTx, kTy), 0, L.s, CLay{u, L.pitch},
+    hipLaunchKernelGGL(fg_rhs_kernel, dim3(grid), dim3(kFgW), 0, L.s, CLay{u, L.pitch},
                        CLay{v, L.pitch}, Lay{f, L.pitch}, Lay{g, L.pitch}, Lay{rhs, L.pitch},
-                       L.ni, L.nj, a, L.wall_left, L.wall_right, L.wall_bottom, L.wall_top);
+                       L.ni, L.nj, a, L.wall_left, L.wall_right, L.wall_bottom, L.wall_top, nbx,
+                       nblocks);
 }
 
 // the RHS cells fg_rhs_kernel leaves to after the f, g exchange: column 1
@@ -456,16 +473,22 @@ void launch_absmax2(const NsLaunch& L, const double* u, const double* v, double*
 // f, g, p -> u, v instead of that pass plus a 16-B/cell re-read of u, v
 // (misor_api.hip misor_adapt_uv / misor_max_uv).
 //
-// Walk: tiles of kRedThreads columns x kAH rows in row-major order, a
-// workgroup takes every gridDim-th tile, so the workgroups running at any time
-// cover one compact stretch of rows (like a one-thread-per-cell launch; the
-// row-strided walk of absmax2_kernel writes 1024 scattered rows at once and
-// ran adaptUV at ~4 TB/s).  A thread loads its column's kAH rows of f, g,
-// p(i+1) and kAH+1 rows of p at once, then updates and stores them.  Cells
-// inside [1, ni] x [1, nj] get adaptUV's update and contribute their new
-// value, the physical ghost cells of the reduction region their unchanged
-// one.  One partial per workgroup (max: order-free, exact).
-constexpr int kAH = 8;
+// Walk: tiles of 2 kRedThreads columns (two per lane: 16-byte loads and
+// stores of the column pairs (odd, even), whose first column starts a
+// 16-byte word in the padded layout) x kAR rows, row-major; a workgroup takes
+// every gridDim-th tile, so the workgroups running at any time cover one
+// compact stretch of rows.  Tiles inside [1, ni] x [1, nj] run without lane
+// masks or branches; p(i+1) of a pair's first column is its second column,
+// of the second one an 8-byte load (the same lines), p(j+1) the next row's
+// p (one extra row per tile).  The cells of the reduction region outside the
+// interior (the physical ghost cells) contribute their unchanged value in a
+// separate walk; max is order-free and idempotent, so a cell counted twice
+// changes nothing.  One partial per workgroup.
+constexpr int kAR = 4;
+
+typedef double ad2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ ad2 ld2(const double* q) { return *reinterpret_cast<const ad2*>(q); }
 
 __global__ __launch_bounds__(kRedThreads) void adapt_absmax_kernel(CLay f, CLay g, CLay p, Lay u,
                                                                    Lay v, int ni, int nj,
@@ -473,49 +496,82 @@ __global__ __launch_bounds__(kRedThreads) void adapt_absmax_kernel(CLay f, CLay 
                                                                    double* partials) {
     __shared__ double su[kRedThreads / 64], sv[kRedThreads / 64];
     double mu = 2.2250738585072014e-308, mv = 2.2250738585072014e-308;  // DBL_MIN
-    const int ntx = (R.w + kRedThreads - 1) / kRedThreads, nty = (R.h + kAH - 1) / kAH;
+    constexpr int TW = 2 * kRedThreads;
+    const int ntx = (ni + TW - 1) / TW, nty = (nj + kAR - 1) / kAR;
+    const long long pitch = p.pitch;
+    auto at = [&](int i, int j) { return (long long)(j + kYOff) * pitch + (i + kXOff); };
     for (int t = blockIdx.x; t < ntx * nty; t += gridDim.x) {
-        const int ii = (t % ntx) * kRedThreads + (int)threadIdx.x, jj0 = (t / ntx) * kAH;
-        if (ii >= R.w) continue;
-        const int i = R.ilo + ii;
-        const bool icol = i >= 1 && i <= ni;
-        double pc[kAH + 1], pe[kAH], fv[kAH], gv[kAH];
+        const int tx = t % ntx, ty = t / ntx;
+        const int ia = 1 + tx * TW + 2 * (int)threadIdx.x;
+        const int j0 = 1 + ty * kAR;
+        if ((tx + 1) * TW <= ni && j0 + kAR - 1 <= nj) {  // interior tile (workgroup-uniform)
+            ad2 pc[kAR + 1], fv[kAR], gv[kAR];
+            double pe[kAR];
 #pragma unroll
-        for (int q = 0; q < kAH; ++q) {
-            const int j = R.jlo + jj0 + q;
-            if (jj0 + q < R.h) {
-                if (icol && j >= 1 && j <= nj) {
-                    pc[q] = p(i, j);
-                    pe[q] = p(i + 1, j);
-                    fv[q] = f(i, j);
-                    gv[q] = g(i, j);
-                } else {  // a physical ghost cell: its unchanged value
-                    fv[q] = u(i, j);
-                    gv[q] = v(i, j);
+            for (int q = 0; q < kAR; ++q) {
+                const long long o = at(ia, j0 + q);
+                fv[q] = ld2(f.a + o);
+                gv[q] = ld2(g.a + o);
+                pc[q] = ld2(p.a + o);
+                pe[q] = p.a[o + 2];  // p(ib + 1, j)
+            }
+            pc[kAR] = ld2(p.a + at(ia, j0 + kAR));  // p(., j + 1) of the tile's last row
+#pragma unroll
+            for (int q = 0; q < kAR; ++q) {
+                const long long o = at(ia, j0 + q);
+                // :447-452, per column
+                const double a0 = fv[q].x - (pc[q].y - pc[q].x) * fx;
+                const double a1 = fv[q].y - (pe[q] - pc[q].y) * fx;
+                const double b0 = gv[q].x - (pc[q + 1].x - pc[q].x) * fy;
+                const double b1 = gv[q].y - (pc[q + 1].y - pc[q].y) * fy;
+                *reinterpret_cast<ad2*>(u.a + o) = ad2{a0, a1};
+                *reinterpret_cast<ad2*>(v.a + o) = ad2{b0, b1};
+                mu = fmax(mu, fmax(fabs(a0), fabs(a1)));
+                mv = fmax(mv, fmax(fabs(b0), fabs(b1)));
+            }
+        } else {  // a tile at the right / top end: per cell
+            for (int q = 0; q < kAR; ++q) {
+                const int j = j0 + q;
+                if (j > nj) break;
+                for (int c = 0; c < 2; ++c) {
+                    const int i = ia + c;
+                    if (i > ni) break;
+                    const double pc0 = p(i, j);
+                    const double a = f(i, j) - (p(i + 1, j) - pc0) * fx;
+                    const double b = g(i, j) - (p(i, j + 1) - pc0) * fy;
+                    u(i, j) = a;
+                    v(i, j) = b;
+                    mu = fmax(mu, fabs(a));
+                    mv = fmax(mv, fabs(b));
                 }
             }
         }
-        {
-            const int j = R.jlo + jj0 + kAH;  // p(i, j+1) of the tile's last row
-            if (icol && jj0 + kAH - 1 < R.h && j - 1 >= 1 && j - 1 <= nj) pc[kAH] = p(i, j);
-        }
-#pragma unroll
-        for (int q = 0; q < kAH; ++q) {
-            const int j = R.jlo + jj0 + q;
-            if (jj0 + q >= R.h) break;
-            double a = fv[q], b = gv[q];
-            if (icol && j >= 1 && j <= nj) {
-                const double pn = q + 1 < kAH ? ((j + 1 <= nj) ? pc[q + 1] : p(i, j + 1))
-                                              : pc[kAH];
-                a = fv[q] - (pe[q] - pc[q]) * fx;  // :447-452
-                b = gv[q] - (pn - pc[q]) * fy;
-                u(i, j) = a;
-                v(i, j) = b;
+    }
+    // the region's cells outside the interior: physical ghost columns and rows
+    // (R covers [ilo, ilo + w) x [jlo, jlo + h); the interior is [1, ni] x [1, nj])
+    {
+        const int nl = R.ilo == 0 ? R.h : 0;                      // column 0
+        const int nr = R.ilo + R.w - 1 == ni + 1 ? R.h : 0;      // column ni + 1
+        const int nb = R.jlo == 0 ? R.w : 0;                      // row 0
+        const int nt = R.jlo + R.h - 1 == nj + 1 ? R.w : 0;      // row nj + 1
+        const int n = nl + nr + nb + nt;
+        for (int k = blockIdx.x * kRedThreads + threadIdx.x; k < n; k += gridDim.x * kRedThreads) {
+            int i, j;
+            if (k < nl) {
+                i = 0;
+                j = R.jlo + k;
+            } else if (k < nl + nr) {
+                i = ni + 1;
+                j = R.jlo + (k - nl);
+            } else if (k < nl + nr + nb) {
+                i = R.ilo + (k - nl - nr);
+                j = 0;
+            } else {
+                i = R.ilo + (k - nl - nr - nb);
+                j = nj + 1;
             }
-            a = fabs(a);
-            b = fabs(b);
-            mu = (mu > a) ? mu : a;
-            mv = (mv > b) ? mv : b;
+            mu = fmax(mu, fabs(u(i, j)));
+            mv = fmax(mv, fabs(v(i, j)));
         }
     }
     mu = wmax(mu);

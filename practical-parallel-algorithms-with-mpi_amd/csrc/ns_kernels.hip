@@ -402,9 +402,15 @@ constexpr int kRedBlocks = 1024;
 constexpr int kRedThreads = 256;
 
 int reduce_blocks(int ni, int nj) {
+    // MISOR_RED_BLOCKS: tuning experiments (read once)
+    static const int cap = [] {
+        const char* e = getenv("MISOR_RED_BLOCKS");
+        const int v = e ? atoi(e) : 0;
+        return v > 0 && v <= 8192 ? v : kRedBlocks;
+    }();
     long long cells = (long long)(ni + 2) * (nj + 2);
     long long b = (cells + kRedThreads - 1) / kRedThreads;
-    return (int)(b < kRedBlocks ? (b < 1 ? 1 : b) : kRedBlocks);
+    return (int)(b < cap ? (b < 1 ? 1 : b) : cap);
 }
 
 namespace {
@@ -484,12 +490,12 @@ void launch_absmax2(const NsLaunch& L, const double* u, const double* v, double*
 // interior (the physical ghost cells) contribute their unchanged value in a
 // separate walk; max is order-free and idempotent, so a cell counted twice
 // changes nothing.  One partial per workgroup.
-constexpr int kAR = 4;
 
 typedef double ad2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ ad2 ld2(const double* q) { return *reinterpret_cast<const ad2*>(q); }
 
+template <int kAR>
 __global__ __launch_bounds__(kRedThreads) void adapt_absmax_kernel(CLay f, CLay g, CLay p, Lay u,
                                                                    Lay v, int ni, int nj,
                                                                    double fx, double fy, Region R,
@@ -593,7 +599,15 @@ __global__ __launch_bounds__(kRedThreads) void adapt_absmax_kernel(CLay f, CLay 
 
 void launch_adapt_absmax(const NsLaunch& L, const double* f, const double* g, const double* p,
                          double* u, double* v, double* partials) {
-    hipLaunchKernelGGL(adapt_absmax_kernel, dim3(reduce_blocks(L.ni, L.nj)), dim3(kRedThreads), 0,
+    // rows per tile: 8 (16384^2: 2.06 ms against 2.12 for 4 and 2.14 for 2,
+    // profiles/r03_ns_adapt_rows.txt; MISOR_ADAPT_ROWS: tuning experiments)
+    static const int rows = [] {
+        const char* e = getenv("MISOR_ADAPT_ROWS");
+        return e && atoi(e) == 4 ? 4 : e && atoi(e) == 2 ? 2 : 8;
+    }();
+    auto k = rows == 8 ? adapt_absmax_kernel<8> : rows == 2 ? adapt_absmax_kernel<2>
+                                                            : adapt_absmax_kernel<4>;
+    hipLaunchKernelGGL(k, dim3(reduce_blocks(L.ni, L.nj)), dim3(kRedThreads), 0,
                        L.s, CLay{f, L.pitch}, CLay{g, L.pitch}, CLay{p, L.pitch},
                        Lay{u, L.pitch}, Lay{v, L.pitch}, L.ni, L.nj, L.prm.dt / L.prm.dx,
                        L.prm.dt / L.prm.dy, region_of(L), partials);

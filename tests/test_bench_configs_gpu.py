@@ -123,8 +123,9 @@ def test_ns_dcavity_16384_two_steps(golden):
 
 def test_decomposed_8_ranks_32768_windows():
     """BASELINE config 4 at 8 GPUs: the 4 x 2 split of 32768^2 that bench.py
-    --gpus 8 runs (one rank's block 8192 x 16384: T = 7, its automatic block
-    geometry, pipelined passes with the slot reserve, 2T-deep exchanges), as 8
+    --gpus 8 runs (one rank's block 8192 x 16384: T = 8, chained passes with
+    their automatic geometry -- main and edge kernels, work stealing --,
+    pipelined passes with the slot reserve, 2T-deep exchanges), as 8
     in-process ranks on the one GPU of the test box; windows at the physical
     corners and where two and four rank blocks meet, bit for bit against the
     oracle run on the window (see test_full_size_32768_windows)"""
@@ -144,6 +145,7 @@ def test_decomposed_8_ranks_32768_windows():
                 g.poisson_init(1.0, 1.0, 2)
                 p0, rhs = g.download(M.P), g.download(M.RHS)
                 it, _ = g.solve_rb()
+                assert g.get_tuning(M.TUNE_TB_CHAIN) == 1  # chained on a 2^27-cell block
                 outs[r] = (g.loc, p0, rhs, g.download(M.P), it, g.stats()["iters_per_pass"])
         except BaseException as e:
             errs.append((r, repr(e)))
@@ -156,7 +158,7 @@ def test_decomposed_8_ranks_32768_windows():
         assert not t.is_alive(), "rank thread hung"
     assert not errs, errs
     assert all(o[4] == k for o in outs)
-    assert all(o[5] == 7 for o in outs)  # T of a 2^27-cell block (misor_api.hip)
+    assert all(o[5] == 8 for o in outs)  # T of a 2^27-cell block (misor_api.hip)
     assert tuple(outs[0][0].dims) == (4, 2) and (outs[0][0].ni, outs[0][0].nj) == (8192, 16384)
 
     def assemble(idx):

@@ -1071,8 +1071,10 @@ __device__ __forceinline__ void for_each_block(const SweepParams& prm, int* __re
 // claimed exactly once, by a workgroup that runs it.
 //
 // Modes along a run (the colour of each row is the same as in tb_strip2):
-// strips at a physical left / right side march in pairs (kEdge) throughout;
-// the others keep the static ring at every block boundary -- a block whose
+// columns with a strip at a physical left / right side form a list of their
+// own, run by a second kernel (EDGE = 1: steady chunks with lane masks,
+// kSteadyEdge, one row in flight to stay within the registers) beside the
+// main one; every strip keeps the static ring at every block boundary -- a block whose
 // cone touches a physical bottom / top side (or the column's last block, of
 // any height) is marched in pairs (kRowEdge) between two ring conversions,
 // the rest run steady chunks.  Every block height but the column's last is a

@@ -24,7 +24,7 @@ B="python bench.py --workload ns --no-cpu-baseline --steps 4 --warmup 2"
 timeout -s KILL 180 rocprofv3 --kernel-trace --stats -d $o -o trace --output-format csv -- $B > $o/trace.log 2>&1
 timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE -d $o -o fetch --output-format csv -- $B > $o/fetch.log 2>&1
 timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE -d $o -o write --output-format csv -- $B > $o/write.log 2>&1
-timeout -k 10 300 python tools/scale_proxy.py --tsteps 7,8 --rows 0 --rounds 2 --sweeps 56 --chain -1,0 \
+timeout -k 10 300 python tools/scale_proxy.py --tsteps 7,8 --rows 0 --rounds 2 --sweeps 56 --chain=-1,0 \
     > gpurun_out/scale_proxy_$tag.txt 2>&1
 timeout -k 10 200 python bench.py --local-ranks 8 --size 8192 --steps 20 --warmup 3 --check \
     > gpurun_out/bench_local8_$tag.json 2> gpurun_out/bench_local8_$tag.err

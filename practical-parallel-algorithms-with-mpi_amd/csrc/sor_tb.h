@@ -167,6 +167,34 @@ struct Lane {
     double idx2, idy2, coef;
 };
 
+// The per-lane residual accumulator.  MISOR_RES_BINNED (a cost experiment,
+// never the product build: tools/gpu_res_cost.sh) makes
+// the steady chunks deposit r^2 into two fixed bins instead (q1 = (M1 + x) -
+// M1, q2 = (M2 + (x - q1)) - M2, each added exactly): an order-independent
+// sum, i.e. what a partition-independent residual costs in the sweep.
+#ifdef MISOR_RES_BINNED
+struct TallyAcc {
+    double s1, s2;
+    __device__ TallyAcc& operator=(double v) {
+        s1 = v;
+        s2 = 0.0;
+        return *this;
+    }
+    __device__ operator double() const { return s1 + s2; }
+};
+__device__ __forceinline__ void tally_steady(TallyAcc& a, double r) {
+    constexpr double M1 = 0x1.8p+40, M2 = 0x1.8p-12;  // bins of 2^-12 and 2^-64
+    const double x = r * r;
+    const double q1 = (M1 + x) - M1;
+    const double q2 = (M2 + (x - q1)) - M2;
+    a.s1 += q1;
+    a.s2 += q2;
+}
+#else
+using TallyAcc = double;
+__device__ __forceinline__ void tally_steady(double& a, double r) { a = __builtin_fma(r, r, a); }
+#endif
+
 // How a step is compiled:
 //  kEdge    general: per-lane update / residual masks, ghost-row and
 //           ghost-column copies, row tests.  Strips at a physical left /
@@ -192,9 +220,9 @@ enum { kEdge = 0, kPre = 1, kSteady = 2, kRowEdge = 3, kSteadyEdge = 4 };
 // Stage 0 reads the ghost rows as they are in memory -- the state after the
 // previous pass, or whatever the caller uploaded, as the reference's first
 // iteration does.  Q: colour of the rows (0: column ia is red in row rin-1).
-template <int T, int Q, int MODE, bool BP = false, bool P2 = false>
+template <int T, int Q, int MODE, bool BP = false, bool P2 = false, class Acc>
 __device__ __forceinline__ d2 stage(const Lane& c, int t, bool fixrows, d2 In, int rin, d2& A,
-                                    d2& M1, d2& M2, d2 Ra, d2 Rb, double& acc) {
+                                    d2& M1, d2& M2, d2 Ra, d2 Rb, Acc& acc) {
     // BP: x-neighbours through ds_bpermute instead of DPP (interior modes)
     auto fl = [&](double v) { return BP ? bperm(v, c.bl) : from_left(v); };
     auto fr = [&](double v) { return BP ? bperm(v, c.br) : from_right(v); };
@@ -218,7 +246,7 @@ __device__ __forceinline__ d2 stage(const Lane& c, int t, bool fixrows, d2 In, i
     const int sh = 2 * T - 1 - 2 * t;
     auto tally = [&](double r, int row, int wsh, bool own_col) {
         if (MODE == kSteady) {
-            acc = __builtin_fma(r, r, acc);
+            tally_steady(acc, r);
         } else if (MODE == kSteadyEdge) {
             const double rm = own_col ? r : 0.0;  // select: no branch, NaN-safe
             acc = __builtin_fma(rm, rm, acc);
@@ -289,7 +317,7 @@ struct March {
     d2 A[T], M1[T], M2[T];
     d2 R[2 * T];     // paired march: R[k] = rhs(r0 - 1 - k)
     d2 Pq[D], Rq[D];  // rows in flight: p(r0 .. r0+D-1), rhs(r0-1 .. r0+D-2)
-    double acc[T];
+    TallyAcc acc[T];
     d2 keep[2];
 };
 
@@ -1212,8 +1240,8 @@ __device__ void chain_acquire(const SweepParams& prm, int* head, unsigned long l
 // claim; k = that / 8, 1..4), so most block ends need no atomic and no
 // barrier: own_end (wave-uniform, the same in every wave) is the end of the
 // blocks already claimed.  Returns the next block row, or -1.
-template <int T, int WAVES>
-__device__ __forceinline__ int chain_block_end(const SweepParams& prm, double (&acc)[T],
+template <int T, int WAVES, class Acc>
+__device__ __forceinline__ int chain_block_end(const SweepParams& prm, Acc (&acc)[T],
                                                double* partials, int L, int* sh,
                                                unsigned long long* seg, int slot, int by,
                                                int& own_end) {

@@ -17,6 +17,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIBPATH = os.path.join(HERE, "lib", "libmisor.so")
+_DEFAULT_LIBPATH = LIBPATH
 
 P, RHS, U, V, F, G = range(6)
 NOSLIP, SLIP, OUTFLOW, PERIODIC = 1, 2, 3, 4
@@ -147,6 +148,10 @@ class MisorError(RuntimeError):
     pass
 
 
+# diagnostics that an older library (A/B runs) may lack; the default library must have all
+_DIAGNOSTIC = {"misor_chain_trace"}
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -155,6 +160,8 @@ def lib():
                              "practical-parallel-algorithms-with-mpi_amd` (or __graft_entry__.build())")
         L = C.CDLL(LIBPATH)
         for name, (res, args) in SIGNATURES.items():
+            if name in _DIAGNOSTIC and LIBPATH != _DEFAULT_LIBPATH and not hasattr(L, name):
+                continue  # an older library loaded for an A/B run (tools/scale_proxy.py --lib)
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -92,7 +92,11 @@ def main():
         for _ in range(args.rounds):
             for c in combos:
                 T, v, r, x, pp, rv, ch = c
-                g.set_tuning(M.TUNE_TB_CHAIN, ch)
+                try:
+                    g.set_tuning(M.TUNE_TB_CHAIN, ch)
+                except M.MisorError:  # an older library (--lib A/B runs): no chained passes
+                    if ch != -1:
+                        raise
                 g.set_tuning(M.TUNE_TB_PERSISTENT, pp)
                 g.set_tuning(M.TUNE_TB_RESERVE, rv)
                 g.set_tuning(M.TUNE_XCD_REMAP, x)

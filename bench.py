@@ -376,10 +376,16 @@ def run_ns3d(args, world, rank, local_rank, dist, torch):
             if d.get("size") == n and "bytes_per_launch" in d:
                 traffic = d["bytes_per_launch"]
         fused = g.get_tuning(M.TUNE3_SWEEP) == 1
+        resident = g.get_tuning(M.TUNE3_RESIDENT) == 1
         out["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": 8000.0,
                            "unit": "GB/s", "frac": round(ach / 8000.0, 4),
-                           "traffic": traffic if fused else None,
-                           "kernel": ("3D solve: k3_sweep (one fused red+black launch) + "
+                           "traffic": traffic if fused and not resident else None,
+                           "kernel": ("3D solve: k3_resident (the whole solve in one "
+                                      "cooperative launch, p resident in LDS, two grid "
+                                      "barriers per iteration; achieved = the 24 B/LUP a "
+                                      "streaming sweep would move, p never leaves the CUs)"
+                                      if resident else
+                                      "3D solve: k3_sweep (one fused red+black launch) + "
                                       "k3_finish per iteration" if fused else
                                       "3D solve: k3_rb_pass x2 + k3_finish per iteration"),
                            "solve_ms_per_iteration": round(solve_ms / solve_iters, 5)}

@@ -325,8 +325,13 @@ enum {
     MISOR3_TUNE_FOLD = 4,   /* single rank, fused sweep: 1 (default) = each sweep launch first
                              * applies the previous sweep's loop test (one launch per
                              * iteration); 0 = a finish kernel after every sweep */
-    MISOR3_TUNE_RHS_AHEAD = 5 /* fused sweep: plane steps between an rhs load and its first
-                               * use, 1 or 2; 0 (default) = 2 on marches of >= 16 planes */
+    MISOR3_TUNE_RHS_AHEAD = 5, /* fused sweep: plane steps between an rhs load and its first
+                                * use, 1 or 2; 0 (default) = 2 on marches of >= 16 planes */
+    MISOR3_TUNE_RESIDENT = 6  /* single rank: the whole solve in one cooperative launch with
+                               * p resident in LDS (boxes of 32x16x16 cells, grid barriers
+                               * between the colour passes) when the grid fits the device
+                               * (128^3 on 256 CUs); 1 / -1 (default) = when it fits, 0 = never.
+                               * misor3_get_tuning returns whether the next solve uses it */
 };
 int misor3_set_tuning(misor_grid3* g, int key, int value);
 int misor3_get_tuning(const misor_grid3* g, int key, int* value);

@@ -88,6 +88,8 @@ struct misor_grid3 {
     int rows = 8;              // MISOR3_TUNE_ROWS
     int kchunk = 0;            // MISOR3_TUNE_KCHUNK (0: automatic)
     int fold = 1;              // MISOR3_TUNE_FOLD: single rank, loop test inside the sweep
+    int resident = -1;         // MISOR3_TUNE_RESIDENT: whole solve in one launch when it fits
+    void* rbar = nullptr;      // its grid-barrier state
     int rhs_ahead = 0;         // MISOR3_TUNE_RHS_AHEAD: fused sweep's rhs loads 1 or 2 steps
                                // ahead; 0: 2 on marches of >= 16 planes, else 1
     double dx = 0, dy = 0, dz = 0, dt = 0, dt_bound = 0;
@@ -220,6 +222,7 @@ void misor3_destroy(misor_grid3* g) {
     for (auto& f : g->alloc)
         if (f) (void)hipFree(f);
     (void)hipFree(g->partials);
+    (void)hipFree(g->rbar);
     (void)hipFree(g->out);
     (void)hipHostFree(g->out_host);
     (void)hipFree(g->st);
@@ -637,6 +640,41 @@ int misor3_solve(misor_grid3* g, int* iters, double* res) {
         if (res) *res = 1.0;
         return MISOR_OK;
     }
+    // p resident in LDS, one cooperative launch for the whole solve (ns3d_resident.hip)
+    if (!dist(g) && g->resident != 0 && resident3_boxes(g->g) > 0 &&
+        g->partials_cap >= 2 * resident3_boxes(g->g)) {
+        if (!g->rbar) HIPCHK3(hipMalloc(&g->rbar, resident3_bar_bytes()));
+        *g->st_host = s0;
+        if (g->timing) HIPCHK3(hipEventRecord(g->ev[0], g->stream));
+        HIPCHK3(hipMemcpyAsync(g->st, g->st_host, sizeof(DevState), hipMemcpyHostToDevice,
+                               g->stream));
+        const int lr = launch3_resident(g->stream, g->g, g->fld[MISOR3_P], g->fld[MISOR3_RHS],
+                                        1.0 / dx2, 1.0 / dy2, 1.0 / dz2, factor, cells,
+                                        g->partials, g->st, g->rbar);
+        if (lr < 0) return fail3(MISOR_EHIP, "resident solve: launch failed");
+        if (lr == 0) {
+            if (g->timing) HIPCHK3(hipEventRecord(g->ev[1], g->stream));
+            HIPCHK3(hipMemcpyAsync(g->st_host, g->st, sizeof(DevState), hipMemcpyDeviceToHost,
+                                   g->stream));
+            int aborted = 0;
+            if (resident3_aborted(g->rbar, g->stream, &aborted) != 0)
+                return fail3(MISOR_EHIP, "resident solve: state readback failed");
+            if (aborted)
+                return fail3(MISOR_EHIP, "resident solve: a grid barrier timed out (p undefined)");
+            g->alt_stale = true;  // the fused sweep's partner buffer no longer matches p
+            g->last_iters = g->st_host->it;
+            if (g->timing) {
+                float ms = 0.f;
+                HIPCHK3(hipEventElapsedTime(&ms, g->ev[0], g->ev[1]));
+                g->solve_ms += ms;
+                g->solve_iters += g->st_host->it;
+            }
+            if (iters) *iters = g->st_host->it;
+            if (res) *res = g->st_host->res;
+            return MISOR_OK;
+        }
+        // lr == 1: the device refused the cooperative grid -- the streaming sweep below
+    }
     const bool fused = g->sweep != 0;
     if (!fused && dist(g)) return fail3(MISOR_ESTATE, "the two-pass solve is single-rank only");
     const int kc = g->kchunk > 0 ? g->kchunk : auto_kchunk(g->g, g->rows);
@@ -756,6 +794,10 @@ int misor3_set_tuning(misor_grid3* g, int key, int value) {
         if (value < 0 || value > 2) return fail3(MISOR_EINVAL, "rhs_ahead must be 0, 1 or 2");
         g->rhs_ahead = value;
         return MISOR_OK;
+    case MISOR3_TUNE_RESIDENT:
+        if (value < -1 || value > 1) return fail3(MISOR_EINVAL, "resident must be -1, 0 or 1");
+        g->resident = value;
+        return MISOR_OK;
     }
     return fail3(MISOR_EINVAL, "unknown tuning key %d", key);
 }
@@ -770,6 +812,10 @@ int misor3_get_tuning(const misor_grid3* g, int key, int* value) {
         return MISOR_OK;
     case MISOR3_TUNE_FOLD: *value = g->fold; return MISOR_OK;
     case MISOR3_TUNE_RHS_AHEAD: *value = g->rhs_ahead; return MISOR_OK;
+    case MISOR3_TUNE_RESIDENT:
+        *value = !dist(g) && g->resident != 0 && resident3_boxes(g->g) > 0 &&
+                 g->partials_cap >= 2 * resident3_boxes(g->g);
+        return MISOR_OK;
     }
     return fail3(MISOR_EINVAL, "unknown tuning key %d", key);
 }

@@ -346,6 +346,16 @@ void launch3_sweep_folded(hipStream_t s, const G3& g, const double* src, double*
                           double factor, int rows, int kc, double* partials,
                           const double* prev_partials, const DevState* st_in, DevState* st_out,
                           double cells, bool ra2 = false);
+// the whole solve in one cooperative launch, p resident in LDS
+// (ns3d_resident.hip): boxes for this grid (0: not possible here), the size of
+// its barrier state, the launch (0 ok, 1 refused -> fall back, < 0 error) and
+// whether a barrier wait timed out
+int resident3_boxes(const G3& g);
+size_t resident3_bar_bytes();
+int launch3_resident(hipStream_t s, const G3& g, double* p, const double* rhs, double idx2,
+                     double idy2, double idz2, double factor, double cells, double* partials,
+                     DevState* st, void* bar);
+int resident3_aborted(const void* bar, hipStream_t s, int* aborted);
 void launch3_fold_decide(hipStream_t s, const G3& g, int rows, int kc,
                          const double* prev_partials, const DevState* st_in, DevState* st_out,
                          double cells);

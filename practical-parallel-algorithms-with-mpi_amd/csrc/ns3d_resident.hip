@@ -1,0 +1,333 @@
+// ns3d_resident.hip -- the whole 3D red-black solve (assignment-6/src/
+// solver.c:175-297) in ONE launch for grids whose pressure field fits in the
+// GPU's combined LDS (256 CUs x 160 KB = 40 MB: p of the reference's 128^3 is
+// 17 MB).
+//
+// Why: at 128^3 an iteration of the streaming sweep (k3_sweep, one launch per
+// iteration) is a single resident round whose length is its k-march's latency
+// chain, ~26 us for 2M cells.  Here every workgroup keeps one
+// box of p (32 x 16 x 16 cells + a one-cell shell) in LDS and its rhs in
+// registers for the whole solve, and the iterations are separated by grid
+// barriers instead of kernel boundaries:
+//
+//   red pass (LDS)  -> its box-surface cells to p in HBM -> grid barrier ->
+//   red shell cells from the neighbours' surfaces -> black pass -> black
+//   surface cells + the workgroup's residual partial -> grid barrier ->
+//   black shell cells; every workgroup sums all partials in the same fixed
+//   order and applies the loop test (res = (res + sum)/N, solver.c:283-289),
+//   so all stop after the same iteration.
+//
+// Semantics are solve()'s, cell by cell: red cells (i+j+k odd) only read
+// black ones and vice versa, so the shell needs only the colour the next pass
+// reads; the Neumann ghost-face copy of the iteration's end (solver.c:237-278,
+// faces only, edges and corners never touched) is done by the owner of the
+// face cell right after updating it -- the ghost is read by that cell alone.
+// Launched cooperatively (hipLaunchCooperativeKernel refuses a grid that cannot
+// be co-resident, and the host then falls back to k3_sweep); every barrier wait
+// is bounded: on a timeout the kernel raises an abort flag that every
+// workgroup checks, all of them exit, and the host reports the failure.
+//
+// Memory ordering across XCDs (their L2s are not coherent with each other):
+// each wave issues an agent-scope release fence before the barrier arrival
+// (its stores written back) and an acquire fence after it (stale lines
+// invalidated); the only global data the loop writes are box-surface cells
+// and partials.
+
+#include <cstdlib>
+
+#include "misor_internal.h"
+
+namespace misor {
+
+namespace {
+
+constexpr int kRbx = 32, kRby = 16, kRbz = 16;  // box of cells per workgroup
+constexpr int kRsx = kRbx + 2;                   // LDS strides (one-cell shell)
+constexpr int kRsy = (kRby + 2) * kRsx;
+constexpr int kRcells = (kRbz + 2) * kRsy;
+constexpr int kRfaces = 2 * (kRby * kRbz + kRbx * kRbz + kRbx * kRby);  // shell face cells
+constexpr int kRthreads = 256;
+constexpr int kRq = kRfaces / kRthreads;  // shell cells per thread
+static_assert(kRfaces % kRthreads == 0, "shell cells per thread");
+static_assert(kRbx == 32 && kRby == 16 && kRthreads == 256,
+              "thread t: column pair t & 15, row t >> 4, all planes of the box");
+constexpr long long kSpinLimit = 1ll << 22;  // polls (~1 us each) before a barrier gives up
+
+struct Bar3 {
+    unsigned count;  // arrivals so far (zeroed before each launch)
+    int abort;       // 1: a barrier timed out -- every workgroup leaves
+};
+
+__device__ __forceinline__ double rwave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// fixed-order sum over the workgroup (wave trees, then waves 0..3 in order);
+// every thread gets the result
+__device__ __forceinline__ double rblock_sum(double v, double* sh) {
+    v = rwave_sum(v);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+    __syncthreads();
+    return ((sh[0] + sh[1]) + sh[2]) + sh[3];
+}
+
+// grid barrier number n (1-based): returns false if the solve was aborted.
+// mode (experiments, MISOR3_RESIDENT_MODE): bit 0 = the agent-scope fences by
+// thread 0 only (after a workgroup-scope release by every wave)
+__device__ bool rgrid_sync(Bar3* bar, unsigned n, int* sh_flag, int mode) {
+    if (mode & 1) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __syncthreads();
+        if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    } else {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const unsigned target = n * gridDim.x;
+        __hip_atomic_fetch_add(&bar->count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int ab = 0;
+        long long polls = 0;
+        while (__hip_atomic_load(&bar->count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+               target) {
+            if (__hip_atomic_load(&bar->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                ab = 1;
+                break;
+            }
+            if (++polls > kSpinLimit) {
+                __hip_atomic_store(&bar->abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ab = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        *sh_flag = ab;
+        if (mode & 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
+    if (!(mode & 1)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    return *sh_flag == 0;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(kRthreads, 1) void k3_resident(G3 g, double* __restrict__ p,
+                                                            const double* __restrict__ rhs,
+                                                            double idx2, double idy2, double idz2,
+                                                            double factor, double cells,
+                                                            double* __restrict__ partials,
+                                                            DevState* __restrict__ st,
+                                                            Bar3* __restrict__ bar, int nbx,
+                                                            int nby, int mode) {
+    __shared__ double L[kRcells];
+    __shared__ double sh[4];
+    __shared__ int sh_flag;
+    const int t = threadIdx.x;
+    const int b = blockIdx.x;
+    const int ox = 1 + (b % nbx) * kRbx;  // global coordinates of the box's first cell
+    const int oy = 1 + (b / nbx % nby) * kRby;
+    const int oz = 1 + b / (nbx * nby) * kRbz;
+    const int I = g.I, J = g.J, K = g.K;
+    const int sx = (int)g.sx, sxy = (int)g.sxy;  // resident grids are < 2^31 cells
+
+    // p: the box and its shell (ghosts included; cells past a ragged edge: 0)
+    for (int q = t; q < kRcells; q += kRthreads) {
+        const int lz = q / kRsy, ly = q / kRsx % (kRby + 2), lx = q % kRsx;
+        const int i = ox - 1 + lx, j = oy - 1 + ly, k = oz - 1 + lz;
+        L[q] = (i <= I + 1 && j <= J + 1 && k <= K + 1) ? p[k * sxy + j * sx + i] : 0.0;
+    }
+    // this thread's cells: the column pair (i0, i0+1) of row j, planes oz .. oz+15
+    const int px = t & 15, y = t >> 4;
+    const int i0 = ox + 2 * px, j = oy + y;
+    double rh[kRbz][2];
+#pragma unroll
+    for (int z = 0; z < kRbz; ++z) {
+        const int k = oz + z;
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+            rh[z][e] = (i0 + e <= I && j <= J && k <= K) ? rhs[k * sxy + j * sx + i0 + e] : 0.0;
+    }
+    // shell cells this thread refreshes: LDS position, global offset, colour
+    // (bit 0: (i+j+k) & 1) and whether it is a neighbour's interior cell
+    int sl[kRq], sg[kRq], sc[kRq];
+#pragma unroll
+    for (int m = 0; m < kRq; ++m) {
+        const int f = t + kRthreads * m;
+        int lx, ly, lz;
+        if (f < 2 * kRby * kRbz) {  // x faces
+            const int r = f % (kRby * kRbz);
+            lx = f < kRby * kRbz ? 0 : kRbx + 1;
+            ly = 1 + r % kRby;
+            lz = 1 + r / kRby;
+        } else if (f < 2 * kRby * kRbz + 2 * kRbx * kRbz) {  // y faces
+            const int h = f - 2 * kRby * kRbz, r = h % (kRbx * kRbz);
+            ly = h < kRbx * kRbz ? 0 : kRby + 1;
+            lx = 1 + r % kRbx;
+            lz = 1 + r / kRbx;
+        } else {  // z faces
+            const int h = f - 2 * kRby * kRbz - 2 * kRbx * kRbz, r = h % (kRbx * kRby);
+            lz = h < kRbx * kRby ? 0 : kRbz + 1;
+            lx = 1 + r % kRbx;
+            ly = 1 + r / kRbx;
+        }
+        const int i = ox - 1 + lx, jj = oy - 1 + ly, k = oz - 1 + lz;
+        const bool inner = i >= 1 && i <= I && jj >= 1 && jj <= J && k >= 1 && k <= K;
+        sl[m] = (lz * (kRby + 2) + ly) * kRsx + lx;
+        sg[m] = inner ? k * sxy + jj * sx + i : -1;
+        sc[m] = (i + jj + k) & 1;
+    }
+    // the shell cells of colour `col` (0: black, i+j+k even; 1: red)
+    auto refresh = [&](int col) {
+        double v[kRq];
+#pragma unroll
+        for (int m = 0; m < kRq; ++m)
+            v[m] = (sg[m] >= 0 && sc[m] == col) ? p[sg[m]] : 0.0;
+#pragma unroll
+        for (int m = 0; m < kRq; ++m)
+            if (sg[m] >= 0 && sc[m] == col) L[sl[m]] = v[m];
+    };
+    // one colour pass: update, residual, ghost faces, box-surface cells to p
+    double acc = 0.0;
+    auto pass = [&](int col) {
+#pragma unroll
+        for (int z = 0; z < kRbz; ++z) {
+            const int k = oz + z;
+            const int e = ((i0 + j + k) & 1) == col ? 0 : 1;  // the pair element of colour col
+            const int i = i0 + e;
+            if (i > I || j > J || k > K) continue;
+            const int x = 2 * px + e;
+            const int o = ((z + 1) * (kRby + 2) + (y + 1)) * kRsx + x + 1;
+            const double c = L[o];
+            const double tx = (L[o + 1] - 2.0 * c) + L[o - 1];
+            const double ty = (L[o + kRsx] - 2.0 * c) + L[o - kRsx];
+            const double tz = (L[o + kRsy] - 2.0 * c) + L[o - kRsy];
+            const double r = (e ? rh[z][1] : rh[z][0]) - ((tx * idx2 + ty * idy2) + tz * idz2);
+            const double v = c - (factor * r);
+            L[o] = v;
+            acc += (r * r);
+            // Neumann ghost faces (read by this cell only)
+            if (i == 1) L[o - 1] = v;
+            if (i == I) L[o + 1] = v;
+            if (j == 1) L[o - kRsx] = v;
+            if (j == J) L[o + kRsx] = v;
+            if (k == 1) L[o - kRsy] = v;
+            if (k == K) L[o + kRsy] = v;
+            // box-surface cells: the neighbours' shells
+            if (!(mode & 2) &&
+                (x == 0 || x == kRbx - 1 || y == 0 || y == kRby - 1 || z == 0 || z == kRbz - 1))
+                p[k * sxy + j * sx + i] = v;
+        }
+    };
+
+    double res = st->res;
+    int it = st->it, done = st->done;
+    const double epssq = st->epssq;
+    const int itermax = st->itermax;
+    unsigned nbar = 0;
+    bool ok = true;
+    __syncthreads();
+    // mode bit 1 / 2 (timing experiments only, results wrong): no shell
+    // exchange / no grid barriers
+    while (!done) {
+        pass(1);  // red: i+j+k odd (solver.c: the sweep starts at (1,1,1))
+        if (!(mode & 4) && !(ok = rgrid_sync(bar, ++nbar, &sh_flag, mode))) break;
+        if (!(mode & 2)) refresh(1);
+        __syncthreads();
+        pass(0);
+        const double s = rblock_sum(acc, sh);
+        acc = 0.0;
+        double* part = partials + (it & 1) * gridDim.x;
+        if (t == 0) part[b] = s;
+        if (!(mode & 4) && !(ok = rgrid_sync(bar, ++nbar, &sh_flag, mode))) break;
+        if (!(mode & 2)) refresh(0);
+        // every workgroup: the same fixed-order sum of all partials
+        double q = 0.0;
+        for (int w = t; w < (int)gridDim.x; w += kRthreads) q += part[w];
+        const double S = rblock_sum(q, sh);
+        res = (res + S) / cells;
+        ++it;
+        done = !((res >= epssq) && (it < itermax));
+        __syncthreads();
+    }
+    if (!ok) return;
+    // the box and the ghost faces next to it, back to p
+#pragma unroll
+    for (int z = 0; z < kRbz; ++z) {
+        const int k = oz + z;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int i = i0 + e;
+            if (i > I || j > J || k > K) continue;
+            const int o = ((z + 1) * (kRby + 2) + (y + 1)) * kRsx + 2 * px + e + 1;
+            const int go = k * sxy + j * sx + i;
+            p[go] = L[o];
+            if (i == 1) p[go - 1] = L[o - 1];
+            if (i == I) p[go + 1] = L[o + 1];
+            if (j == 1) p[go - sx] = L[o - kRsx];
+            if (j == J) p[go + sx] = L[o + kRsx];
+            if (k == 1) p[go - sxy] = L[o - kRsy];
+            if (k == K) p[go + sxy] = L[o + kRsy];
+        }
+    }
+    if (b == 0 && t == 0) {
+        st->it = it;
+        st->res = res;
+        st->done = done;
+    }
+}
+
+// boxes of the resident solve for this grid, or 0 if it cannot run here
+int resident3_boxes(const G3& g) {
+    if (g.koff != 0 || !g.lo_phys || !g.hi_phys) return 0;  // single domain only
+    if ((long long)(g.K + 2) * g.sxy >= (1ll << 31)) return 0;
+    const int nbx = (g.I + kRbx - 1) / kRbx, nby = (g.J + kRby - 1) / kRby,
+              nbz = (g.K + kRbz - 1) / kRbz;
+    const long long nb = (long long)nbx * nby * nbz;
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(k3_resident),
+                                                     kRthreads, 0) != hipSuccess)
+        return 0;
+    return nb <= (long long)cus * per ? (int)nb : 0;
+}
+
+size_t resident3_bar_bytes() { return sizeof(Bar3); }
+
+// 0: launched; 1: the device refused the cooperative grid (the caller falls
+// back to the streaming sweep); < 0: error
+int launch3_resident(hipStream_t s, const G3& g, double* p, const double* rhs, double idx2,
+                     double idy2, double idz2, double factor, double cells, double* partials,
+                     DevState* st, void* bar) {
+    const int nb = resident3_boxes(g);
+    if (nb == 0) return 1;
+    int nbx = (g.I + kRbx - 1) / kRbx, nby = (g.J + kRby - 1) / kRby;
+    if (hipMemsetAsync(bar, 0, sizeof(Bar3), s) != hipSuccess) return -1;
+    G3 ga = g;
+    Bar3* b = static_cast<Bar3*>(bar);
+    static int mode = [] {
+        const char* e = getenv("MISOR3_RESIDENT_MODE");
+        return e ? atoi(e) : 1;
+    }();
+    void* args[] = {&ga, &p, const_cast<double**>(&rhs), &idx2, &idy2, &idz2, &factor, &cells,
+                    &partials, &st, &b, &nbx, &nby, &mode};
+    const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k3_resident),
+                                                    dim3(nb), dim3(kRthreads), args, 0, s);
+    if (e == hipSuccess) return 0;
+    (void)hipGetLastError();  // clear the refusal
+    return 1;
+}
+
+int resident3_aborted(const void* bar, hipStream_t s, int* aborted) {
+    Bar3 h{};
+    if (hipMemcpyAsync(&h, bar, sizeof(Bar3), hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return -1;
+    *aborted = h.abort;
+    return 0;
+}
+
+}  // namespace misor

@@ -31,6 +31,7 @@ COMM_ID_BYTES = 128
 # 3D field ids (misor3_*)
 P3, RHS3, U3, V3, W3, F3, G3, H3 = range(8)
 TUNE3_SWEEP, TUNE3_ROWS, TUNE3_KCHUNK, TUNE3_FOLD, TUNE3_RHS_AHEAD = 1, 2, 3, 4, 5
+TUNE3_RESIDENT = 6  # whole solve in one cooperative launch, p in LDS (when it fits)
 
 _dp = C.POINTER(C.c_double)
 

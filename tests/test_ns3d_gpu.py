@@ -52,9 +52,10 @@ def random_state(shape, seed):
 # the grid), the loop test folded into the next sweep (default, single rank)
 # or a finish kernel after every sweep, rhs loaded one or two plane steps
 # ahead (default: by march length), and the two colour-pass form
+# (sweep, rows, kchunk[, fold[, rhs_ahead[, resident]]]); resident 0 unless given
 SOLVE_TUNES = [(1, 8, 0), (1, 4, 4), (1, 12, 5), (1, 8, 3 + 4), (1, 8, 0, 0), (1, 4, 4, 0),
                (1, 12, 5, 0), (1, 8, 0, 0, 2), (1, 4, 4, 1, 2), (1, 12, 5, 0, 2), (1, 8, 3 + 4, 0, 2), (1, 8, 16, 0, 1),
-               (0, 8, 0)]
+               (0, 8, 0), (1, 8, 0, 1, 0, 1)]
 
 
 def set_tune(g, tune):
@@ -65,6 +66,9 @@ def set_tune(g, tune):
         g.set_tuning(M.TUNE3_FOLD, tune[3])
     if len(tune) > 4:
         g.set_tuning(M.TUNE3_RHS_AHEAD, tune[4])
+    g.set_tuning(M.TUNE3_RESIDENT, tune[5] if len(tune) > 5 else 0)
+    if len(tune) > 5 and tune[5]:
+        assert g.get_tuning(M.TUNE3_RESIDENT) == 1  # the grid fits: the resident solve runs
 
 
 def pair(prm, st, dt, tune=None):
@@ -151,7 +155,7 @@ def test_compute_timestep_at_rest(golden):
 @pytest.mark.parametrize("dims,itermax", [((5, 4, 3), 37), ((12, 9, 7), 11),
                                           ((64, 16, 8), 25), ((131, 37, 19), 9),
                                           ((125, 13, 30), 4), ((249, 25, 17), 2),
-                                          ((256, 128, 64), 3)])
+                                          ((256, 128, 64), 3), ((128, 128, 128), 5)])
 def test_solve_fixed_iterations_bitwise(golden, dims, itermax, tune):
     prm = params(golden, "a6_dcavity.par", imax=dims[0], jmax=dims[1], kmax=dims[2],
                  eps=1e-150, itermax=itermax)
@@ -230,7 +234,8 @@ def run_gpu(prm, steps, tune=None):
     return g, np.array(iters), t
 
 
-@pytest.mark.parametrize("tune", [(1, 8, 0), (0, 8, 0), (1, 4, 4), (1, 8, 0, 0), (1, 8, 0, 0, 2)])
+@pytest.mark.parametrize("tune", [(1, 8, 0), (0, 8, 0), (1, 4, 4), (1, 8, 0, 0), (1, 8, 0, 0, 2),
+                                  (1, 8, 0, 1, 0, 1)])
 @pytest.mark.parametrize("fixture,par", [("ns3d_dcavity_short.npz", "a6_dcavity.par"),
                                          ("ns3d_canal_short.npz", "a6_canal.par")])
 def test_short_run_matches_reference_fixture(golden, fixture, par, tune):
@@ -259,12 +264,27 @@ def test_medium_run_matches_oracle(golden):
             assert np.array_equal(g.download(GPU_FIELD[n]), getattr(ns, n)), n
 
 
+def test_resident_only_when_it_fits(golden):
+    """288 x 128 x 64 needs 288 boxes of 32x16x16 (> 256 CUs): the streaming sweep runs"""
+    prm = params(golden, "a6_dcavity.par", imax=288, jmax=128, kmax=64, itermax=2)
+    with M.Grid3(prm) as g:
+        g.set_tuning(M.TUNE3_RESIDENT, 1)
+        assert g.get_tuning(M.TUNE3_RESIDENT) == 0
+    prm = params(golden, "a6_dcavity.par", imax=128, jmax=128, kmax=128, itermax=2)
+    with M.Grid3(prm) as g:
+        assert g.get_tuning(M.TUNE3_RESIDENT) == 1
+
+
 def test_tuning_keys(golden):
     prm = params(golden, "a6_dcavity.par", imax=8, jmax=8, kmax=8)
     with M.Grid3(prm) as g:
         assert g.get_tuning(M.TUNE3_SWEEP) == 1 and g.get_tuning(M.TUNE3_ROWS) == 8
         assert g.get_tuning(M.TUNE3_KCHUNK) >= 8
         assert g.get_tuning(M.TUNE3_FOLD) == 1 and g.get_tuning(M.TUNE3_RHS_AHEAD) == 0
-        for key, bad in ((M.TUNE3_SWEEP, 2), (M.TUNE3_ROWS, 5), (M.TUNE3_KCHUNK, 2), (99, 0)):
+        assert g.get_tuning(M.TUNE3_RESIDENT) == 1  # 8^3 fits: the default solve is resident
+        g.set_tuning(M.TUNE3_RESIDENT, 0)
+        assert g.get_tuning(M.TUNE3_RESIDENT) == 0
+        for key, bad in ((M.TUNE3_SWEEP, 2), (M.TUNE3_ROWS, 5), (M.TUNE3_KCHUNK, 2),
+                         (M.TUNE3_RESIDENT, 2), (99, 0)):
             with pytest.raises(M.MisorError):
                 g.set_tuning(key, bad)

@@ -3,7 +3,8 @@ iteration counts from a random state, device time from the library's HIP
 events, p checked bit-identical across variants.
 
     python tools/tune3d.py --size 384 --iters 60 [--configs 1,8,0 1,4,0 0,8,0 ...]
-    (a config is sweep,rows,kchunk[,fold[,rhs_ahead]]; MISOR3_TUNE_*)
+    (a config is sweep,rows,kchunk[,fold[,rhs_ahead[,resident]]]; MISOR3_TUNE_*;
+    resident defaults to 0 here)
 """
 import argparse
 import os
@@ -39,12 +40,15 @@ def main():
             sw, rows, kc = v[:3]
             fold = v[3] if len(v) > 3 else 1
             ahead = v[4] if len(v) > 4 else 0
+            res3 = v[5] if len(v) > 5 else 0
             with M.Grid3(prm) as g:
                 g.set_tuning(M.TUNE3_SWEEP, sw)
                 g.set_tuning(M.TUNE3_ROWS, rows)
                 g.set_tuning(M.TUNE3_KCHUNK, kc)
                 g.set_tuning(M.TUNE3_FOLD, fold)
                 g.set_tuning(M.TUNE3_RHS_AHEAD, ahead)
+                g.set_tuning(M.TUNE3_RESIDENT, res3)
+                res3 = g.get_tuning(M.TUNE3_RESIDENT)
                 g.upload(M.RHS3, rhs)
                 best = None
                 for r in range(a.reps + 1):
@@ -60,9 +64,10 @@ def main():
                     ref = p
                 kc_eff = g.get_tuning(M.TUNE3_KCHUNK)
             mlups = n ** 3 / (best / 1e3) / 1e6
-            print("n=%d sweep=%d rows=%d kc=%d fold=%d ahead=%d: %.4f ms/iter  %.0f MLUP/s  "
-                  "%.3f of 8 TB/s (24 B/LUP)  %s" % (n, sw, rows, kc_eff, fold, ahead, best, mlups,
-                                                     mlups * 24e-6 / 8.0, same), flush=True)
+            print("n=%d sweep=%d rows=%d kc=%d fold=%d ahead=%d resident=%d: %.4f ms/iter  "
+                  "%.0f MLUP/s  %.3f of 8 TB/s (24 B/LUP)  %s" % (
+                      n, sw, rows, kc_eff, fold, ahead, res3, best, mlups, mlups * 24e-6 / 8.0,
+                      same), flush=True)
 
 
 if __name__ == "__main__":

@@ -88,7 +88,7 @@ struct misor_grid3 {
     int rows = 8;              // MISOR3_TUNE_ROWS
     int kchunk = 0;            // MISOR3_TUNE_KCHUNK (0: automatic)
     int fold = 1;              // MISOR3_TUNE_FOLD: single rank, loop test inside the sweep
-    int resident = -1;         // MISOR3_TUNE_RESIDENT: whole solve in one launch when it fits
+    int resident = 0;          // MISOR3_TUNE_RESIDENT: whole solve in one launch when it fits
     void* rbar = nullptr;      // its grid-barrier state
     int rhs_ahead = 0;         // MISOR3_TUNE_RHS_AHEAD: fused sweep's rhs loads 1 or 2 steps
                                // ahead; 0: 2 on marches of >= 16 planes, else 1

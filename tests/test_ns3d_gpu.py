@@ -272,6 +272,7 @@ def test_resident_only_when_it_fits(golden):
         assert g.get_tuning(M.TUNE3_RESIDENT) == 0
     prm = params(golden, "a6_dcavity.par", imax=128, jmax=128, kmax=128, itermax=2)
     with M.Grid3(prm) as g:
+        g.set_tuning(M.TUNE3_RESIDENT, -1)
         assert g.get_tuning(M.TUNE3_RESIDENT) == 1
 
 
@@ -281,9 +282,10 @@ def test_tuning_keys(golden):
         assert g.get_tuning(M.TUNE3_SWEEP) == 1 and g.get_tuning(M.TUNE3_ROWS) == 8
         assert g.get_tuning(M.TUNE3_KCHUNK) >= 8
         assert g.get_tuning(M.TUNE3_FOLD) == 1 and g.get_tuning(M.TUNE3_RHS_AHEAD) == 0
-        assert g.get_tuning(M.TUNE3_RESIDENT) == 1  # 8^3 fits: the default solve is resident
+        assert g.get_tuning(M.TUNE3_RESIDENT) == 0  # default: the streaming sweep
+        g.set_tuning(M.TUNE3_RESIDENT, -1)
+        assert g.get_tuning(M.TUNE3_RESIDENT) == 1  # 8^3 fits
         g.set_tuning(M.TUNE3_RESIDENT, 0)
-        assert g.get_tuning(M.TUNE3_RESIDENT) == 0
         for key, bad in ((M.TUNE3_SWEEP, 2), (M.TUNE3_ROWS, 5), (M.TUNE3_KCHUNK, 2),
                          (M.TUNE3_RESIDENT, 2), (99, 0)):
             with pytest.raises(M.MisorError):

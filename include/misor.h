@@ -330,7 +330,7 @@ enum {
     MISOR3_TUNE_RESIDENT = 6  /* single rank: the whole solve in one cooperative launch with
                                * p resident in LDS (boxes of 32x16x16 cells, grid barriers
                                * between the colour passes) when the grid fits the device
-                               * (128^3 on 256 CUs); 1 / -1 = when it fits, 0 (default) = never.
+                               * (128^3 on 256 CUs); 1 / -1 (default) = when it fits, 0 = never.
                                * misor3_get_tuning returns whether the next solve uses it */
 };
 int misor3_set_tuning(misor_grid3* g, int key, int value);

@@ -88,8 +88,9 @@ struct misor_grid3 {
     int rows = 8;              // MISOR3_TUNE_ROWS
     int kchunk = 0;            // MISOR3_TUNE_KCHUNK (0: automatic)
     int fold = 1;              // MISOR3_TUNE_FOLD: single rank, loop test inside the sweep
-    int resident = 0;          // MISOR3_TUNE_RESIDENT: whole solve in one launch when it fits
-    void* rbar = nullptr;      // its grid-barrier state
+    int resident = -1;         // MISOR3_TUNE_RESIDENT: whole solve in one launch when it fits
+    void* rbar = nullptr;      // its grid-barrier state and partials, uncached memory
+    double* rmbox = nullptr;   // its exchange mailbox (p's layout), uncached memory
     int rhs_ahead = 0;         // MISOR3_TUNE_RHS_AHEAD: fused sweep's rhs loads 1 or 2 steps
                                // ahead; 0: 2 on marches of >= 16 planes, else 1
     double dx = 0, dy = 0, dz = 0, dt = 0, dt_bound = 0;
@@ -223,6 +224,7 @@ void misor3_destroy(misor_grid3* g) {
         if (f) (void)hipFree(f);
     (void)hipFree(g->partials);
     (void)hipFree(g->rbar);
+    (void)hipFree(g->rmbox);
     (void)hipFree(g->out);
     (void)hipHostFree(g->out_host);
     (void)hipFree(g->st);
@@ -641,16 +643,27 @@ int misor3_solve(misor_grid3* g, int* iters, double* res) {
         return MISOR_OK;
     }
     // p resident in LDS, one cooperative launch for the whole solve (ns3d_resident.hip)
-    if (!dist(g) && g->resident != 0 && resident3_boxes(g->g) > 0 &&
-        g->partials_cap >= 2 * resident3_boxes(g->g)) {
-        if (!g->rbar) HIPCHK3(hipMalloc(&g->rbar, resident3_bar_bytes()));
+    if (!dist(g) && g->resident != 0 && resident3_boxes(g->g) > 0) {
+        // barrier state + 2 x 256 partials, and a mailbox of p's layout for the
+        // box-surface cells, in uncached memory: coherent across the XCDs' L2s
+        // without cache write-backs / invalidations at every barrier
+        if (!g->rbar)
+            HIPCHK3(hipExtMallocWithFlags(&g->rbar, resident3_bar_bytes() + 2 * 256 * sizeof(double),
+                                          hipDeviceMallocUncached));
+        if (!g->rmbox)
+            HIPCHK3(hipExtMallocWithFlags(reinterpret_cast<void**>(&g->rmbox),
+                                          sizeof(double) * (size_t)g->nalloc,
+                                          hipDeviceMallocUncached));
+        double* const rpart =
+            reinterpret_cast<double*>(static_cast<char*>(g->rbar) + resident3_bar_bytes());
+        double* const mbox0 = g->rmbox + (g->fld[MISOR3_P] - g->mem[MISOR3_P]);
         *g->st_host = s0;
         if (g->timing) HIPCHK3(hipEventRecord(g->ev[0], g->stream));
         HIPCHK3(hipMemcpyAsync(g->st, g->st_host, sizeof(DevState), hipMemcpyHostToDevice,
                                g->stream));
         const int lr = launch3_resident(g->stream, g->g, g->fld[MISOR3_P], g->fld[MISOR3_RHS],
                                         1.0 / dx2, 1.0 / dy2, 1.0 / dz2, factor, cells,
-                                        g->partials, g->st, g->rbar);
+                                        rpart, g->st, g->rbar, mbox0);
         if (lr < 0) return fail3(MISOR_EHIP, "resident solve: launch failed");
         if (lr == 0) {
             if (g->timing) HIPCHK3(hipEventRecord(g->ev[1], g->stream));
@@ -813,8 +826,7 @@ int misor3_get_tuning(const misor_grid3* g, int key, int* value) {
     case MISOR3_TUNE_FOLD: *value = g->fold; return MISOR_OK;
     case MISOR3_TUNE_RHS_AHEAD: *value = g->rhs_ahead; return MISOR_OK;
     case MISOR3_TUNE_RESIDENT:
-        *value = !dist(g) && g->resident != 0 && resident3_boxes(g->g) > 0 &&
-                 g->partials_cap >= 2 * resident3_boxes(g->g);
+        *value = !dist(g) && g->resident != 0 && resident3_boxes(g->g) > 0;
         return MISOR_OK;
     }
     return fail3(MISOR_EINVAL, "unknown tuning key %d", key);

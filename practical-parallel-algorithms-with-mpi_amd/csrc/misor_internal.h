@@ -354,7 +354,7 @@ int resident3_boxes(const G3& g);
 size_t resident3_bar_bytes();
 int launch3_resident(hipStream_t s, const G3& g, double* p, const double* rhs, double idx2,
                      double idy2, double idz2, double factor, double cells, double* partials,
-                     DevState* st, void* bar);
+                     DevState* st, void* bar, double* mbox);
 int resident3_aborted(const void* bar, hipStream_t s, int* aborted);
 void launch3_fold_decide(hipStream_t s, const G3& g, int rows, int kc,
                          const double* prev_partials, const DevState* st_in, DevState* st_out,

@@ -47,6 +47,7 @@ constexpr int kRsy = (kRby + 2) * kRsx;
 constexpr int kRcells = (kRbz + 2) * kRsy;
 constexpr int kRfaces = 2 * (kRby * kRbz + kRbx * kRbz + kRbx * kRby);  // shell face cells
 constexpr int kRthreads = 256;
+constexpr int kRg = 4;  // planes per group of a colour pass (its LDS reads issued together)
 constexpr int kRq = kRfaces / kRthreads;  // shell cells per thread
 static_assert(kRfaces % kRthreads == 0, "shell cells per thread");
 static_assert(kRbx == 32 && kRby == 16 && kRthreads == 256,
@@ -54,8 +55,10 @@ static_assert(kRbx == 32 && kRby == 16 && kRthreads == 256,
 constexpr long long kSpinLimit = 1ll << 22;  // polls (~1 us each) before a barrier gives up
 
 struct Bar3 {
-    unsigned count;  // arrivals so far (zeroed before each launch)
-    int abort;       // 1: a barrier timed out -- every workgroup leaves
+    unsigned count;       // arrivals so far (zeroed before each launch)
+    int abort;            // 1: a barrier timed out -- every workgroup leaves
+    unsigned pad[14];
+    unsigned xcd[8 * 16];  // mode bit 5: arrivals per group blockIdx % 8, one 64-B line each
 };
 
 __device__ __forceinline__ double rwave_sum(double v) {
@@ -78,7 +81,11 @@ __device__ __forceinline__ double rblock_sum(double v, double* sh) {
 // mode (experiments, MISOR3_RESIDENT_MODE): bit 0 = the agent-scope fences by
 // thread 0 only (after a workgroup-scope release by every wave)
 __device__ bool rgrid_sync(Bar3* bar, unsigned n, int* sh_flag, int mode) {
-    if (mode & 1) {
+    if (mode & 24) {  // exchange data and partials by agent-scope atomics: no cache upkeep
+        __builtin_amdgcn_s_waitcnt(0);  // this wave's stores acknowledged by memory
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __syncthreads();
+    } else if (mode & 1) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __syncthreads();
         if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -87,8 +94,19 @@ __device__ bool rgrid_sync(Bar3* bar, unsigned n, int* sh_flag, int mode) {
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        const unsigned target = n * gridDim.x;
-        __hip_atomic_fetch_add(&bar->count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned target = n * gridDim.x;
+        if (mode & 32) {  // two levels: the last of each group blockIdx % 8 arrives globally
+            const unsigned x = blockIdx.x & 7, nb = gridDim.x;
+            const unsigned cx = (nb - x + 7) / 8;
+            const unsigned old = __hip_atomic_fetch_add(&bar->xcd[16 * x], 1u, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+            if (old + 1 == n * cx)
+                __hip_atomic_fetch_add(&bar->count, 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            target = n * (nb < 8 ? nb : 8);
+        } else {
+            __hip_atomic_fetch_add(&bar->count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         int ab = 0;
         long long polls = 0;
         while (__hip_atomic_load(&bar->count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
@@ -105,10 +123,13 @@ __device__ bool rgrid_sync(Bar3* bar, unsigned n, int* sh_flag, int mode) {
             __builtin_amdgcn_s_sleep(1);
         }
         *sh_flag = ab;
-        if (mode & 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if ((mode & 25) == 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
     __syncthreads();
-    if (!(mode & 1)) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (mode & 24)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    else if (!(mode & 1))
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     return *sh_flag == 0;
 }
 
@@ -121,7 +142,8 @@ __global__ __launch_bounds__(kRthreads, 1) void k3_resident(G3 g, double* __rest
                                                             double* __restrict__ partials,
                                                             DevState* __restrict__ st,
                                                             Bar3* __restrict__ bar, int nbx,
-                                                            int nby, int mode) {
+                                                            int nby, int mode,
+                                                            double* __restrict__ mbox) {
     __shared__ double L[kRcells];
     __shared__ double sh[4];
     __shared__ int sh_flag;
@@ -179,12 +201,27 @@ __global__ __launch_bounds__(kRthreads, 1) void k3_resident(G3 g, double* __rest
         sg[m] = inner ? k * sxy + jj * sx + i : -1;
         sc[m] = (i + jj + k) & 1;
     }
+    // where box-surface cells are exchanged: p itself, or (mode bit 3) a
+    // mailbox of p's layout in uncached memory
+    double* const xch = (mode & 8) ? mbox : p;
+    // mode bit 3 or 4: exchanged cells and partials moved by relaxed agent-scope
+    // atomics (coherent across the XCDs' L2s without write-backs / invalidations)
+    const bool xa = (mode & 24) != 0;
+    auto xload = [&](const double* a) {
+        return xa ? __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *a;
+    };
+    auto xstore = [&](double* a, double v) {
+        if (xa)
+            __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+            *a = v;
+    };
     // the shell cells of colour `col` (0: black, i+j+k even; 1: red)
     auto refresh = [&](int col) {
         double v[kRq];
 #pragma unroll
         for (int m = 0; m < kRq; ++m)
-            v[m] = (sg[m] >= 0 && sc[m] == col) ? p[sg[m]] : 0.0;
+            v[m] = (sg[m] >= 0 && sc[m] == col) ? xload(xch + sg[m]) : 0.0;
 #pragma unroll
         for (int m = 0; m < kRq; ++m)
             if (sg[m] >= 0 && sc[m] == col) L[sl[m]] = v[m];
@@ -192,33 +229,51 @@ __global__ __launch_bounds__(kRthreads, 1) void k3_resident(G3 g, double* __rest
     // one colour pass: update, residual, ghost faces, box-surface cells to p
     double acc = 0.0;
     auto pass = [&](int col) {
+        // groups of kRg planes: every LDS read of a group is issued before its
+        // stores (a store may alias a later read as far as the compiler knows,
+        // so one cell at a time would serialise on LDS latency)
+        const int e0 = ((i0 + j + oz) & 1) == col ? 0 : 1;  // pair element of colour col, z = 0
 #pragma unroll
-        for (int z = 0; z < kRbz; ++z) {
-            const int k = oz + z;
-            const int e = ((i0 + j + k) & 1) == col ? 0 : 1;  // the pair element of colour col
-            const int i = i0 + e;
-            if (i > I || j > J || k > K) continue;
-            const int x = 2 * px + e;
-            const int o = ((z + 1) * (kRby + 2) + (y + 1)) * kRsx + x + 1;
-            const double c = L[o];
-            const double tx = (L[o + 1] - 2.0 * c) + L[o - 1];
-            const double ty = (L[o + kRsx] - 2.0 * c) + L[o - kRsx];
-            const double tz = (L[o + kRsy] - 2.0 * c) + L[o - kRsy];
-            const double r = (e ? rh[z][1] : rh[z][0]) - ((tx * idx2 + ty * idy2) + tz * idz2);
-            const double v = c - (factor * r);
-            L[o] = v;
-            acc += (r * r);
-            // Neumann ghost faces (read by this cell only)
-            if (i == 1) L[o - 1] = v;
-            if (i == I) L[o + 1] = v;
-            if (j == 1) L[o - kRsx] = v;
-            if (j == J) L[o + kRsx] = v;
-            if (k == 1) L[o - kRsy] = v;
-            if (k == K) L[o + kRsy] = v;
-            // box-surface cells: the neighbours' shells
-            if (!(mode & 2) &&
-                (x == 0 || x == kRbx - 1 || y == 0 || y == kRby - 1 || z == 0 || z == kRbz - 1))
-                p[k * sxy + j * sx + i] = v;
+        for (int z0 = 0; z0 < kRbz; z0 += kRg) {
+            double c[kRg], xm[kRg], xp[kRg], ym[kRg], yp[kRg], zm[kRg], zp[kRg];
+#pragma unroll
+            for (int u = 0; u < kRg; ++u) {
+                const int z = z0 + u, e = e0 ^ (z & 1);
+                const int o = ((z + 1) * (kRby + 2) + (y + 1)) * kRsx + 2 * px + e + 1;
+                c[u] = L[o];
+                xm[u] = L[o - 1];
+                xp[u] = L[o + 1];
+                ym[u] = L[o - kRsx];
+                yp[u] = L[o + kRsx];
+                zm[u] = L[o - kRsy];
+                zp[u] = L[o + kRsy];
+            }
+#pragma unroll
+            for (int u = 0; u < kRg; ++u) {
+                const int z = z0 + u, k = oz + z, e = e0 ^ (z & 1), i = i0 + e;
+                if (i > I || j > J || k > K) continue;
+                const int x = 2 * px + e;
+                const int o = ((z + 1) * (kRby + 2) + (y + 1)) * kRsx + x + 1;
+                const double cc = c[u];
+                const double tx = (xp[u] - 2.0 * cc) + xm[u];
+                const double ty = (yp[u] - 2.0 * cc) + ym[u];
+                const double tz = (zp[u] - 2.0 * cc) + zm[u];
+                const double r = (e ? rh[z][1] : rh[z][0]) - ((tx * idx2 + ty * idy2) + tz * idz2);
+                const double v = cc - (factor * r);
+                L[o] = v;
+                acc += (r * r);
+                // Neumann ghost faces (read by this cell only)
+                if (i == 1) L[o - 1] = v;
+                if (i == I) L[o + 1] = v;
+                if (j == 1) L[o - kRsx] = v;
+                if (j == J) L[o + kRsx] = v;
+                if (k == 1) L[o - kRsy] = v;
+                if (k == K) L[o + kRsy] = v;
+                // box-surface cells: the neighbours' shells
+                if (!(mode & 2) &&
+                    (x == 0 || x == kRbx - 1 || y == 0 || y == kRby - 1 || z == 0 || z == kRbz - 1))
+                    xstore(xch + (k * sxy + j * sx + i), v);
+            }
         }
     };
 
@@ -240,12 +295,13 @@ __global__ __launch_bounds__(kRthreads, 1) void k3_resident(G3 g, double* __rest
         const double s = rblock_sum(acc, sh);
         acc = 0.0;
         double* part = partials + (it & 1) * gridDim.x;
-        if (t == 0) part[b] = s;
+        if (t == 0) xstore(part + b, s);
         if (!(mode & 4) && !(ok = rgrid_sync(bar, ++nbar, &sh_flag, mode))) break;
-        if (!(mode & 2)) refresh(0);
-        // every workgroup: the same fixed-order sum of all partials
+        // every workgroup: the same fixed-order sum of all partials (loads
+        // issued together with the shell's)
         double q = 0.0;
-        for (int w = t; w < (int)gridDim.x; w += kRthreads) q += part[w];
+        for (int w = t; w < (int)gridDim.x; w += kRthreads) q += xload(part + w);
+        if (!(mode & 2)) refresh(0);
         const double S = rblock_sum(q, sh);
         res = (res + S) / cells;
         ++it;
@@ -292,16 +348,17 @@ int resident3_boxes(const G3& g) {
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(k3_resident),
                                                      kRthreads, 0) != hipSuccess)
         return 0;
-    return nb <= (long long)cus * per ? (int)nb : 0;
+    return nb <= (long long)cus * per && nb <= 256 ? (int)nb : 0;  // 256: partials slots
 }
 
-size_t resident3_bar_bytes() { return sizeof(Bar3); }
+size_t resident3_bar_bytes() { return 1024; }
+static_assert(sizeof(Bar3) <= 1024, "barrier state");
 
 // 0: launched; 1: the device refused the cooperative grid (the caller falls
 // back to the streaming sweep); < 0: error
 int launch3_resident(hipStream_t s, const G3& g, double* p, const double* rhs, double idx2,
                      double idy2, double idz2, double factor, double cells, double* partials,
-                     DevState* st, void* bar) {
+                     DevState* st, void* bar, double* mbox) {
     const int nb = resident3_boxes(g);
     if (nb == 0) return 1;
     int nbx = (g.I + kRbx - 1) / kRbx, nby = (g.J + kRby - 1) / kRby;
@@ -310,10 +367,11 @@ int launch3_resident(hipStream_t s, const G3& g, double* p, const double* rhs, d
     Bar3* b = static_cast<Bar3*>(bar);
     static int mode = [] {
         const char* e = getenv("MISOR3_RESIDENT_MODE");
-        return e ? atoi(e) : 1;
+        return e ? atoi(e) : 48;  // atomics for the exchange, two-level barrier
     }();
+    int md = mbox ? mode : (mode & ~8);
     void* args[] = {&ga, &p, const_cast<double**>(&rhs), &idx2, &idy2, &idz2, &factor, &cells,
-                    &partials, &st, &b, &nbx, &nby, &mode};
+                    &partials, &st, &b, &nbx, &nby, &md, &mbox};
     const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k3_resident),
                                                     dim3(nb), dim3(kRthreads), args, 0, s);
     if (e == hipSuccess) return 0;

@@ -282,10 +282,9 @@ def test_tuning_keys(golden):
         assert g.get_tuning(M.TUNE3_SWEEP) == 1 and g.get_tuning(M.TUNE3_ROWS) == 8
         assert g.get_tuning(M.TUNE3_KCHUNK) >= 8
         assert g.get_tuning(M.TUNE3_FOLD) == 1 and g.get_tuning(M.TUNE3_RHS_AHEAD) == 0
-        assert g.get_tuning(M.TUNE3_RESIDENT) == 0  # default: the streaming sweep
-        g.set_tuning(M.TUNE3_RESIDENT, -1)
-        assert g.get_tuning(M.TUNE3_RESIDENT) == 1  # 8^3 fits
+        assert g.get_tuning(M.TUNE3_RESIDENT) == 1  # default: resident when the grid fits
         g.set_tuning(M.TUNE3_RESIDENT, 0)
+        assert g.get_tuning(M.TUNE3_RESIDENT) == 0
         for key, bad in ((M.TUNE3_SWEEP, 2), (M.TUNE3_ROWS, 5), (M.TUNE3_KCHUNK, 2),
                          (M.TUNE3_RESIDENT, 2), (99, 0)):
             with pytest.raises(M.MisorError):

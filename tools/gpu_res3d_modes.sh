@@ -5,9 +5,12 @@ export TMPDIR=/tmp
 tag=$1
 mkdir -p gpurun_out
 o=gpurun_out/res3d_modes_$tag.txt; : > $o
-timeout -k 10 300 python -u -m pytest tests/test_ns3d_gpu.py -x -q --timeout 120 --timeout-method thread \
-    -k "resident or short_run or medium" > gpurun_out/res3d_tests_$tag.log 2>&1
-for m in 0 1 3 5 7; do
+for m in ${TMODES:-16}; do
+  MISOR3_RESIDENT_MODE=$m timeout -k 10 300 python -u -m pytest tests/test_ns3d_gpu.py -q --timeout 120 --timeout-method thread \
+    -k "resident or short_run or medium" > gpurun_out/res3d_tests_${tag}_m$m.log 2>&1 || rc=$?
+  rc=${rc:-0}; if [ $rc -gt 1 ]; then echo "mode $m: pytest rc $rc" >> $o; exit $rc; fi; rc=0
+done
+for m in ${MODES:-16 26 30}; do
   echo "mode $m" >> $o
   MISOR3_RESIDENT_MODE=$m timeout -k 10 100 python tools/tune3d.py --size 128 --iters 200 --configs 1,8,0,1,0,1 >> $o 2>&1
 done

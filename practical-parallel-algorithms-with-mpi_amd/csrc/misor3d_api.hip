@@ -90,7 +90,7 @@ struct misor_grid3 {
     int fold = 1;              // MISOR3_TUNE_FOLD: single rank, loop test inside the sweep
     int resident = -1;         // MISOR3_TUNE_RESIDENT: whole solve in one launch when it fits
     void* rbar = nullptr;      // its grid-barrier state and partials, uncached memory
-    double* rmbox = nullptr;   // its exchange mailbox (p's layout), uncached memory
+    double* rmbox = nullptr;   // its exchange mailboxes (2 x p's layout), uncached memory
     int rhs_ahead = 0;         // MISOR3_TUNE_RHS_AHEAD: fused sweep's rhs loads 1 or 2 steps
                                // ahead; 0: 2 on marches of >= 16 planes, else 1
     double dx = 0, dy = 0, dz = 0, dt = 0, dt_bound = 0;
@@ -652,7 +652,7 @@ int misor3_solve(misor_grid3* g, int* iters, double* res) {
                                           hipDeviceMallocUncached));
         if (!g->rmbox)
             HIPCHK3(hipExtMallocWithFlags(reinterpret_cast<void**>(&g->rmbox),
-                                          sizeof(double) * (size_t)g->nalloc,
+                                          2 * sizeof(double) * (size_t)g->nalloc,
                                           hipDeviceMallocUncached));
         double* const rpart =
             reinterpret_cast<double*>(static_cast<char*>(g->rbar) + resident3_bar_bytes());

@@ -343,6 +343,316 @@ __global__ __launch_bounds__(kRthreads, 1) void k3_resident(G3 g, double* __rest
     }
 }
 
+// ---------------------------------------------------------------------------
+// k3_resident1: ONE exchange and ONE grid barrier per iteration (mode bit 6).
+// The LDS holds the box and a two-cell shell (36 x 20 x 20 doubles, 115 KB).
+// Each iteration the workgroup also updates the red cells of the shell's
+// inner layer (its face-neighbours' cells) with the same arithmetic as their
+// owners, so the black pass finds every red neighbour locally; only black
+// cells cross box boundaries: after the black pass a box writes its black
+// cells within two of its surface to the mailbox of the iteration's parity,
+// and after the barrier it reads the black cells of its shell (both face
+// layers and the inner layer's edges).  Mailboxes alternate by iteration
+// (a box may write iteration n+1's cells while a slower neighbour still reads
+// iteration n's); p is only read at the start and written at the end.
+constexpr int kTsx = kRbx + 4, kTsy = (kRby + 4) * kTsx, kTcells = (kRbz + 4) * kTsy;
+constexpr int kTring = 2 * (kRby * kRbz + kRbx * kRbz + kRbx * kRby);  // inner-layer face cells
+constexpr int kTrq = kTring / kRthreads;
+constexpr int kTshell = 2 * kTring + 4 * (kRbx + kRby + kRbz);  // received positions
+constexpr int kTsq = (kTshell + kRthreads - 1) / kRthreads;
+static_assert(kTring % kRthreads == 0, "ring cells per thread");
+
+// shell position f (0 .. kTshell): face layers 0/1 and B+2/B+3, then the
+// inner layer's 12 edges; LDS coordinates (shell offset 2)
+__device__ __forceinline__ void shell_pos(int f, int& lx, int& ly, int& lz) {
+    constexpr int FX = kRby * kRbz, FY = kRbx * kRbz, FZ = kRbx * kRby;
+    if (f < 4 * FX) {
+        const int l = f / FX, r = f % FX;
+        lx = l < 2 ? l : kRbx + l;  // 0, 1, B+2, B+3
+        ly = 2 + r % kRby;
+        lz = 2 + r / kRby;
+    } else if (f < 4 * (FX + FY)) {
+        const int h = f - 4 * FX, l = h / FY, r = h % FY;
+        ly = l < 2 ? l : kRby + l;
+        lx = 2 + r % kRbx;
+        lz = 2 + r / kRbx;
+    } else if (f < 4 * (FX + FY + FZ)) {
+        const int h = f - 4 * (FX + FY), l = h / FZ, r = h % FZ;
+        lz = l < 2 ? l : kRbz + l;
+        lx = 2 + r % kRbx;
+        ly = 2 + r / kRbx;
+    } else {  // edges of the inner layer: two coordinates in {1, B+2}
+        const int h = f - 4 * (FX + FY + FZ);
+        if (h < 4 * kRbx) {
+            const int c = h / kRbx;
+            lx = 2 + h % kRbx;
+            ly = (c & 1) ? kRby + 2 : 1;
+            lz = (c & 2) ? kRbz + 2 : 1;
+        } else if (h < 4 * (kRbx + kRby)) {
+            const int q = h - 4 * kRbx, c = q / kRby;
+            ly = 2 + q % kRby;
+            lx = (c & 1) ? kRbx + 2 : 1;
+            lz = (c & 2) ? kRbz + 2 : 1;
+        } else {
+            const int q = h - 4 * (kRbx + kRby), c = q / kRbz;
+            lz = 2 + q % kRbz;
+            lx = (c & 1) ? kRbx + 2 : 1;
+            ly = (c & 2) ? kRby + 2 : 1;
+        }
+    }
+}
+
+// inner-layer face position f (0 .. kTring)
+__device__ __forceinline__ void ring_pos(int f, int& lx, int& ly, int& lz) {
+    constexpr int FX = kRby * kRbz, FY = kRbx * kRbz, FZ = kRbx * kRby;
+    if (f < 2 * FX) {
+        const int r = f % FX;
+        lx = f < FX ? 1 : kRbx + 2;
+        ly = 2 + r % kRby;
+        lz = 2 + r / kRby;
+    } else if (f < 2 * (FX + FY)) {
+        const int h = f - 2 * FX, r = h % FY;
+        ly = h < FY ? 1 : kRby + 2;
+        lx = 2 + r % kRbx;
+        lz = 2 + r / kRbx;
+    } else {
+        const int h = f - 2 * (FX + FY), r = h % FZ;
+        lz = h < FZ ? 1 : kRbz + 2;
+        lx = 2 + r % kRbx;
+        ly = 2 + r / kRbx;
+    }
+    (void)FZ;
+}
+
+__global__ __launch_bounds__(kRthreads, 1) void k3_resident1(G3 g, double* __restrict__ p,
+                                                             const double* __restrict__ rhs,
+                                                             double idx2, double idy2,
+                                                             double idz2, double factor,
+                                                             double cells,
+                                                             double* __restrict__ partials,
+                                                             DevState* __restrict__ st,
+                                                             Bar3* __restrict__ bar, int nbx,
+                                                             int nby, int mode,
+                                                             double* __restrict__ mbox,
+                                                             int mstride) {
+    __shared__ double L[kTcells];
+    __shared__ double sh[4];
+    __shared__ int sh_flag;
+    const int t = threadIdx.x;
+    const int b = blockIdx.x;
+    const int ox = 1 + (b % nbx) * kRbx;
+    const int oy = 1 + (b / nbx % nby) * kRby;
+    const int oz = 1 + b / (nbx * nby) * kRbz;
+    const int I = g.I, J = g.J, K = g.K;
+    const int sx = (int)g.sx, sxy = (int)g.sxy;
+    auto gof = [&](int i, int jj, int k) { return k * sxy + jj * sx + i; };
+    auto inner = [&](int i, int jj, int k) {
+        return i >= 1 && i <= I && jj >= 1 && jj <= J && k >= 1 && k <= K;
+    };
+    auto xload = [&](const double* a) {
+        return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    auto xstore = [&](double* a, double v) {
+        __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+
+    // p: the box and its two-cell shell (ghosts included; outside the array: 0)
+    for (int q = t; q < kTcells; q += kRthreads) {
+        const int lz = q / kTsy, ly = q / kTsx % (kRby + 4), lx = q % kTsx;
+        const int i = ox - 2 + lx, jj = oy - 2 + ly, k = oz - 2 + lz;
+        L[q] = (i >= 0 && jj >= 0 && k >= 0 && i <= I + 1 && jj <= J + 1 && k <= K + 1)
+                   ? p[gof(i, jj, k)]
+                   : 0.0;
+    }
+    const int px = t & 15, y = t >> 4;
+    const int i0 = ox + 2 * px, j = oy + y;
+    double rh[kRbz][2];
+#pragma unroll
+    for (int z = 0; z < kRbz; ++z) {
+        const int k = oz + z;
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+            rh[z][e] = (i0 + e <= I && j <= J && k <= K) ? rhs[gof(i0 + e, j, k)] : 0.0;
+    }
+    // the inner layer's red cells this thread updates: LDS index (-1: none) and rhs
+    int rl[kTrq];
+    double rr[kTrq];
+#pragma unroll
+    for (int m = 0; m < kTrq; ++m) {
+        int lx, ly, lz;
+        ring_pos(t + kRthreads * m, lx, ly, lz);
+        const int i = ox - 2 + lx, jj = oy - 2 + ly, k = oz - 2 + lz;
+        const bool red = inner(i, jj, k) && ((i + jj + k) & 1);
+        rl[m] = red ? (lz * (kRby + 4) + ly) * kTsx + lx : -1;
+        rr[m] = red ? rhs[gof(i, jj, k)] : 0.0;
+    }
+    // one update at LDS index o of cell (i, jj, k): returns r; ghost faces copied
+    auto upd = [&](int o, int i, int jj, int k, double rv, double c, double xm, double xp,
+                   double ym, double yp, double zm, double zp) {
+        const double tx = (xp - 2.0 * c) + xm;
+        const double ty = (yp - 2.0 * c) + ym;
+        const double tz = (zp - 2.0 * c) + zm;
+        const double r = rv - ((tx * idx2 + ty * idy2) + tz * idz2);
+        const double v = c - (factor * r);
+        L[o] = v;
+        if (i == 1) L[o - 1] = v;
+        if (i == I) L[o + 1] = v;
+        if (jj == 1) L[o - kTsx] = v;
+        if (jj == J) L[o + kTsx] = v;
+        if (k == 1) L[o - kTsy] = v;
+        if (k == K) L[o + kTsy] = v;
+        return r;
+    };
+    double acc = 0.0;
+    // the box's cells of colour col (1: red, i+j+k odd); black cells within two
+    // of the box surface go to the mailbox xm
+    auto pass = [&](int col, double* xm) {
+        const int e0 = ((i0 + j + oz) & 1) == col ? 0 : 1;
+#pragma unroll
+        for (int z0 = 0; z0 < kRbz; z0 += kRg) {
+            double c[kRg], am[kRg], ap[kRg], bm[kRg], bp[kRg], cm[kRg], cp[kRg];
+#pragma unroll
+            for (int u = 0; u < kRg; ++u) {
+                const int z = z0 + u, e = e0 ^ (z & 1);
+                const int o = ((z + 2) * (kRby + 4) + (y + 2)) * kTsx + 2 * px + e + 2;
+                c[u] = L[o];
+                am[u] = L[o - 1];
+                ap[u] = L[o + 1];
+                bm[u] = L[o - kTsx];
+                bp[u] = L[o + kTsx];
+                cm[u] = L[o - kTsy];
+                cp[u] = L[o + kTsy];
+            }
+#pragma unroll
+            for (int u = 0; u < kRg; ++u) {
+                const int z = z0 + u, k = oz + z, e = e0 ^ (z & 1), i = i0 + e;
+                if (i > I || j > J || k > K) continue;
+                const int x = 2 * px + e;
+                const int o = ((z + 2) * (kRby + 4) + (y + 2)) * kTsx + x + 2;
+                const double r = upd(o, i, j, k, e ? rh[z][1] : rh[z][0], c[u], am[u], ap[u],
+                                     bm[u], bp[u], cm[u], cp[u]);
+                acc += (r * r);
+                if (col == 0 && (x < 2 || x >= kRbx - 2 || y < 2 || y >= kRby - 2 || z < 2 ||
+                                 z >= kRbz - 2))
+                    xstore(xm + gof(i, j, k), L[o]);
+            }
+        }
+    };
+    auto ring_red = [&]() {
+        double c[kTrq], am[kTrq], ap[kTrq], bm[kTrq], bp[kTrq], cm[kTrq], cp[kTrq];
+#pragma unroll
+        for (int m = 0; m < kTrq; ++m) {
+            const int o = rl[m] < 0 ? kTsy + kTsx + 1 : rl[m];  // (a harmless inner index)
+            c[m] = L[o];
+            am[m] = L[o - 1];
+            ap[m] = L[o + 1];
+            bm[m] = L[o - kTsx];
+            bp[m] = L[o + kTsx];
+            cm[m] = L[o - kTsy];
+            cp[m] = L[o + kTsy];
+        }
+#pragma unroll
+        for (int m = 0; m < kTrq; ++m) {
+            if (rl[m] < 0) continue;
+            const int o = rl[m];
+            const int lz = o / kTsy, ly = o / kTsx % (kRby + 4), lx = o % kTsx;
+            (void)upd(o, ox - 2 + lx, oy - 2 + ly, oz - 2 + lz, rr[m], c[m], am[m], ap[m], bm[m],
+                      bp[m], cm[m], cp[m]);
+        }
+    };
+    // the shell's black cells of iteration parity q, with their ghost faces
+    auto receive = [&](const double* xm) {
+        double v[kTsq];
+        int o[kTsq];
+#pragma unroll
+        for (int m = 0; m < kTsq; ++m) {
+            const int f = t + kRthreads * m;
+            o[m] = -1;
+            v[m] = 0.0;
+            if (f < kTshell) {
+                int lx, ly, lz;
+                shell_pos(f, lx, ly, lz);
+                const int i = ox - 2 + lx, jj = oy - 2 + ly, k = oz - 2 + lz;
+                if (inner(i, jj, k) && !((i + jj + k) & 1)) {
+                    o[m] = (lz * (kRby + 4) + ly) * kTsx + lx;
+                    v[m] = xload(xm + gof(i, jj, k));
+                }
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < kTsq; ++m) {
+            if (o[m] < 0) continue;
+            const int q = o[m];
+            L[q] = v[m];
+            // ghost faces of the inner layer's cells (read by the red update of
+            // that cell next iteration); the outer layer's are never read
+            const int lz = q / kTsy, ly = q / kTsx % (kRby + 4), lx = q % kTsx;
+            if (lx == 0 || lx == kRbx + 3 || ly == 0 || ly == kRby + 3 || lz == 0 ||
+                lz == kRbz + 3)
+                continue;
+            const int i = ox - 2 + lx, jj = oy - 2 + ly, k = oz - 2 + lz;
+            if (i == 1) L[q - 1] = v[m];
+            if (i == I) L[q + 1] = v[m];
+            if (jj == 1) L[q - kTsx] = v[m];
+            if (jj == J) L[q + kTsx] = v[m];
+            if (k == 1) L[q - kTsy] = v[m];
+            if (k == K) L[q + kTsy] = v[m];
+        }
+    };
+
+    double res = st->res;
+    int it = st->it, done = st->done;
+    const double epssq = st->epssq;
+    const int itermax = st->itermax;
+    unsigned nbar = 0;
+    bool ok = true;
+    __syncthreads();
+    while (!done) {
+        double* const xm = mbox + (it & 1) * (long long)mstride;
+        ring_red();  // the neighbours' red cells next to the box
+        pass(1, xm);
+        __syncthreads();
+        pass(0, xm);
+        const double s = rblock_sum(acc, sh);
+        acc = 0.0;
+        double* part = partials + (it & 1) * gridDim.x;
+        if (t == 0) xstore(part + b, s);
+        if (!(ok = rgrid_sync(bar, ++nbar, &sh_flag, mode))) break;
+        double q = 0.0;
+        for (int w = t; w < (int)gridDim.x; w += kRthreads) q += xload(part + w);
+        receive(xm);
+        const double S = rblock_sum(q, sh);
+        res = (res + S) / cells;
+        ++it;
+        done = !((res >= epssq) && (it < itermax));
+        __syncthreads();
+    }
+    if (!ok) return;
+#pragma unroll
+    for (int z = 0; z < kRbz; ++z) {
+        const int k = oz + z;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int i = i0 + e;
+            if (i > I || j > J || k > K) continue;
+            const int o = ((z + 2) * (kRby + 4) + (y + 2)) * kTsx + 2 * px + e + 2;
+            const int go = gof(i, j, k);
+            p[go] = L[o];
+            if (i == 1) p[go - 1] = L[o - 1];
+            if (i == I) p[go + 1] = L[o + 1];
+            if (j == 1) p[go - sx] = L[o - kTsx];
+            if (j == J) p[go + sx] = L[o + kTsx];
+            if (k == 1) p[go - sxy] = L[o - kTsy];
+            if (k == K) p[go + sxy] = L[o + kTsy];
+        }
+    }
+    if (b == 0 && t == 0) {
+        st->it = it;
+        st->res = res;
+        st->done = done;
+    }
+}
+
 // boxes of the resident solve for this grid, or 0 if it cannot run here
 int resident3_boxes(const G3& g) {
     if (g.koff != 0 || !g.lo_phys || !g.hi_phys) return 0;  // single domain only
@@ -380,8 +690,13 @@ int launch3_resident(hipStream_t s, const G3& g, double* p, const double* rhs, d
     int md = mbox ? mode : (mode & ~8);
     void* args[] = {&ga, &p, const_cast<double**>(&rhs), &idx2, &idy2, &idz2, &factor, &cells,
                     &partials, &st, &b, &nbx, &nby, &md, &mbox};
-    const hipError_t e = hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k3_resident),
-                                                    dim3(nb), dim3(kRthreads), args, 0, s);
+    int mstride = (int)((g.K + 4) * g.sxy);  // the host's mailboxes: two buffers of p's size
+    void* args1[] = {&ga, &p, const_cast<double**>(&rhs), &idx2, &idy2, &idz2, &factor, &cells,
+                     &partials, &st, &b, &nbx, &nby, &md, &mbox, &mstride};
+    const bool one = (md & 64) && mbox;
+    const hipError_t e = hipLaunchCooperativeKernel(
+        one ? reinterpret_cast<const void*>(k3_resident1) : reinterpret_cast<const void*>(k3_resident),
+        dim3(nb), dim3(kRthreads), one ? args1 : args, 0, s);
     if (e == hipSuccess) return 0;
     (void)hipGetLastError();  // clear the refusal
     return 1;

@@ -685,7 +685,7 @@ int launch3_resident(hipStream_t s, const G3& g, double* p, const double* rhs, d
     Bar3* b = static_cast<Bar3*>(bar);
     static int mode = [] {
         const char* e = getenv("MISOR3_RESIDENT_MODE");
-        return e ? atoi(e) : 48;  // atomics for the exchange, two-level barrier
+        return e ? atoi(e) : 112;  // one barrier per iteration, atomics, two-level barrier
     }();
     int md = mbox ? mode : (mode & ~8);
     void* args[] = {&ga, &p, const_cast<double**>(&rhs), &idx2, &idy2, &idz2, &factor, &cells,

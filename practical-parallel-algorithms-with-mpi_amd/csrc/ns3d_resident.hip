@@ -361,6 +361,8 @@ constexpr int kTrq = kTring / kRthreads;
 constexpr int kTshell = 2 * kTring + 4 * (kRbx + kRby + kRbz);  // received positions
 constexpr int kTsq = (kTshell + kRthreads - 1) / kRthreads;
 static_assert(kTring % kRthreads == 0, "ring cells per thread");
+constexpr int kTrx = kTshell / 2 + 128;  // black cells of the shell, at most
+constexpr int kTrxq = (kTrx + kRthreads - 1) / kRthreads;
 
 // shell position f (0 .. kTshell): face layers 0/1 and B+2/B+3, then the
 // inner layer's 12 edges; LDS coordinates (shell offset 2)
@@ -438,6 +440,13 @@ __global__ __launch_bounds__(kRthreads, 1) void k3_resident1(G3 g, double* __res
     __shared__ double L[kTcells];
     __shared__ double sh[4];
     __shared__ int sh_flag;
+    // built once: the shell's black cells to receive (LDS index | ghost-face bits
+    // << 16, global offset) and the inner layer's red cells (LDS index | ghost
+    // bits << 16, rhs) -- the loops below then touch only real cells
+    __shared__ int2 rx_list[kTrx];
+    __shared__ int ring_o[kTring / 2 + 64];
+    __shared__ double ring_r[kTring / 2 + 64];
+    __shared__ int n_rx, n_ring;
     const int t = threadIdx.x;
     const int b = blockIdx.x;
     const int ox = 1 + (b % nbx) * kRbx;
@@ -474,18 +483,46 @@ __global__ __launch_bounds__(kRthreads, 1) void k3_resident1(G3 g, double* __res
         for (int e = 0; e < 2; ++e)
             rh[z][e] = (i0 + e <= I && j <= J && k <= K) ? rhs[gof(i0 + e, j, k)] : 0.0;
     }
-    // the inner layer's red cells this thread updates: LDS index (-1: none) and rhs
-    int rl[kTrq];
-    double rr[kTrq];
-#pragma unroll
-    for (int m = 0; m < kTrq; ++m) {
+    auto gbits = [&](int i, int jj, int k) {
+        return (i == 1 ? 1 : 0) | (i == I ? 2 : 0) | (jj == 1 ? 4 : 0) | (jj == J ? 8 : 0) |
+               (k == 1 ? 16 : 0) | (k == K ? 32 : 0);
+    };
+    if (t == 0) n_rx = n_ring = 0;
+    __syncthreads();
+    for (int f = t; f < kTring; f += kRthreads) {
         int lx, ly, lz;
-        ring_pos(t + kRthreads * m, lx, ly, lz);
+        ring_pos(f, lx, ly, lz);
         const int i = ox - 2 + lx, jj = oy - 2 + ly, k = oz - 2 + lz;
-        const bool red = inner(i, jj, k) && ((i + jj + k) & 1);
-        rl[m] = red ? (lz * (kRby + 4) + ly) * kTsx + lx : -1;
-        rr[m] = red ? rhs[gof(i, jj, k)] : 0.0;
+        if (inner(i, jj, k) && ((i + jj + k) & 1)) {
+            const int q = atomicAdd(&n_ring, 1);
+            ring_o[q] = ((lz * (kRby + 4) + ly) * kTsx + lx) | (gbits(i, jj, k) << 16);
+            ring_r[q] = rhs[gof(i, jj, k)];
+        }
     }
+    for (int f = t; f < kTshell; f += kRthreads) {
+        int lx, ly, lz;
+        shell_pos(f, lx, ly, lz);
+        const int i = ox - 2 + lx, jj = oy - 2 + ly, k = oz - 2 + lz;
+        if (inner(i, jj, k) && !((i + jj + k) & 1)) {
+            const int q = atomicAdd(&n_rx, 1);
+            // ghost faces only for the inner layer's cells (the outer layer's are never read)
+            const bool outer = lx == 0 || lx == kRbx + 3 || ly == 0 || ly == kRby + 3 || lz == 0 ||
+                               lz == kRbz + 3;
+            rx_list[q] = make_int2(((lz * (kRby + 4) + ly) * kTsx + lx) |
+                                       ((outer ? 0 : gbits(i, jj, k)) << 16),
+                                   gof(i, jj, k));
+        }
+    }
+    __syncthreads();
+    const int nring = n_ring, nrx = n_rx;
+    auto ghosts = [&](int o, int gb, double v) {
+        if (gb & 1) L[o - 1] = v;
+        if (gb & 2) L[o + 1] = v;
+        if (gb & 4) L[o - kTsx] = v;
+        if (gb & 8) L[o + kTsx] = v;
+        if (gb & 16) L[o - kTsy] = v;
+        if (gb & 32) L[o + kTsy] = v;
+    };
     // one update at LDS index o of cell (i, jj, k): returns r; ghost faces copied
     auto upd = [&](int o, int i, int jj, int k, double rv, double c, double xm, double xp,
                    double ym, double yp, double zm, double zp) {
@@ -539,10 +576,14 @@ __global__ __launch_bounds__(kRthreads, 1) void k3_resident1(G3 g, double* __res
         }
     };
     auto ring_red = [&]() {
-        double c[kTrq], am[kTrq], ap[kTrq], bm[kTrq], bp[kTrq], cm[kTrq], cp[kTrq];
+        constexpr int RQ = (kTring / 2 + 64 + kRthreads - 1) / kRthreads;
+        double c[RQ], am[RQ], ap[RQ], bm[RQ], bp[RQ], cm[RQ], cp[RQ];
+        int oo[RQ];
 #pragma unroll
-        for (int m = 0; m < kTrq; ++m) {
-            const int o = rl[m] < 0 ? kTsy + kTsx + 1 : rl[m];  // (a harmless inner index)
+        for (int m = 0; m < RQ; ++m) {
+            const int q = t + kRthreads * m;
+            oo[m] = q < nring ? ring_o[q] : -1;
+            const int o = oo[m] < 0 ? kTsy + kTsx + 1 : (oo[m] & 0xffff);
             c[m] = L[o];
             am[m] = L[o - 1];
             ap[m] = L[o + 1];
@@ -552,51 +593,34 @@ __global__ __launch_bounds__(kRthreads, 1) void k3_resident1(G3 g, double* __res
             cp[m] = L[o + kTsy];
         }
 #pragma unroll
-        for (int m = 0; m < kTrq; ++m) {
-            if (rl[m] < 0) continue;
-            const int o = rl[m];
-            const int lz = o / kTsy, ly = o / kTsx % (kRby + 4), lx = o % kTsx;
-            (void)upd(o, ox - 2 + lx, oy - 2 + ly, oz - 2 + lz, rr[m], c[m], am[m], ap[m], bm[m],
-                      bp[m], cm[m], cp[m]);
+        for (int m = 0; m < RQ; ++m) {
+            if (oo[m] < 0) continue;
+            const int o = oo[m] & 0xffff;
+            const double tx = (ap[m] - 2.0 * c[m]) + am[m];
+            const double ty = (bp[m] - 2.0 * c[m]) + bm[m];
+            const double tz = (cp[m] - 2.0 * c[m]) + cm[m];
+            const double r = ring_r[t + kRthreads * m] - ((tx * idx2 + ty * idy2) + tz * idz2);
+            const double v = c[m] - (factor * r);
+            L[o] = v;
+            ghosts(o, oo[m] >> 16, v);
         }
     };
-    // the shell's black cells of iteration parity q, with their ghost faces
+    // the shell's black cells from mailbox xm, with their ghost faces
     auto receive = [&](const double* xm) {
-        double v[kTsq];
-        int o[kTsq];
+        double v[kTrxq];
+        int2 e[kTrxq];
 #pragma unroll
-        for (int m = 0; m < kTsq; ++m) {
-            const int f = t + kRthreads * m;
-            o[m] = -1;
-            v[m] = 0.0;
-            if (f < kTshell) {
-                int lx, ly, lz;
-                shell_pos(f, lx, ly, lz);
-                const int i = ox - 2 + lx, jj = oy - 2 + ly, k = oz - 2 + lz;
-                if (inner(i, jj, k) && !((i + jj + k) & 1)) {
-                    o[m] = (lz * (kRby + 4) + ly) * kTsx + lx;
-                    v[m] = xload(xm + gof(i, jj, k));
-                }
-            }
+        for (int m = 0; m < kTrxq; ++m) {
+            const int q = t + kRthreads * m;
+            e[m] = q < nrx ? rx_list[q] : make_int2(-1, 0);
+            v[m] = e[m].x >= 0 ? xload(xm + e[m].y) : 0.0;
         }
 #pragma unroll
-        for (int m = 0; m < kTsq; ++m) {
-            if (o[m] < 0) continue;
-            const int q = o[m];
-            L[q] = v[m];
-            // ghost faces of the inner layer's cells (read by the red update of
-            // that cell next iteration); the outer layer's are never read
-            const int lz = q / kTsy, ly = q / kTsx % (kRby + 4), lx = q % kTsx;
-            if (lx == 0 || lx == kRbx + 3 || ly == 0 || ly == kRby + 3 || lz == 0 ||
-                lz == kRbz + 3)
-                continue;
-            const int i = ox - 2 + lx, jj = oy - 2 + ly, k = oz - 2 + lz;
-            if (i == 1) L[q - 1] = v[m];
-            if (i == I) L[q + 1] = v[m];
-            if (jj == 1) L[q - kTsx] = v[m];
-            if (jj == J) L[q + kTsx] = v[m];
-            if (k == 1) L[q - kTsy] = v[m];
-            if (k == K) L[q + kTsy] = v[m];
+        for (int m = 0; m < kTrxq; ++m) {
+            if (e[m].x < 0) continue;
+            const int o = e[m].x & 0xffff;
+            L[o] = v[m];
+            ghosts(o, e[m].x >> 16, v[m]);
         }
     };
 

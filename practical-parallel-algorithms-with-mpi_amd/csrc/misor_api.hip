@@ -137,6 +137,7 @@ struct misor_grid {
 
     // temporally blocked sweep (sor_tb.hip): T iterations per pass over HBM
     int tsteps = kDefaultTsteps;  // requested T (1: single-iteration kernel)
+    bool tsteps_set = false;      // T requested by MISOR_TUNE_TSTEPS (else the default rule)
     SweepParams tp{};             // its launch geometry (for T = tsteps)
     int tb_nparts = 0;
     int tb_rows_req = 0;          // MISOR_TUNE_TB_ROWS (0: automatic)
@@ -649,6 +650,13 @@ static bool chain_on(const misor_grid* g, int variant) {
     return want && g->tb_persistent && variant == kDefaultTbVariant;
 }
 
+// T when none was requested: 8 on large local blocks; on small ones 8 with
+// chained passes (the default there), 7 without (misor_internal.h)
+static int default_tsteps(const misor_grid* g, int variant) {
+    const long long cells = (long long)g->loc.ni * g->loc.nj;
+    return cells >= kTsteps8Cells || chain_on(g, variant) ? kDefaultTsteps : kSmallBlockTsteps;
+}
+
 // residual partials per stage of a pass: one per block, or one per block and
 // wave for a chained pass (sor_tb.h chain_block_end)
 static int tb_parts(const SweepParams& tp) {
@@ -1120,11 +1128,7 @@ int misor_create(misor_grid** out, const misor_desc* d) {
         e = getenv("MISOR_NS_FUSE");  // A/B switch (bench.py --workload ns)
         g->ns_fuse = !(e && e[0] == '0');
     }
-    // T: 8 on large local blocks; on small ones 8 with chained passes (the
-    // default there), 7 without (misor_internal.h)
-    const long long cells = (long long)g->loc.ni * g->loc.nj;
-    const int T0 = cells >= kTsteps8Cells || g->tb_chain != 0 ? kDefaultTsteps : kSmallBlockTsteps;
-    if (configure_tb(g, T0, kDefaultTbVariant, 0) != MISOR_OK)
+    if (configure_tb(g, default_tsteps(g, kDefaultTbVariant), kDefaultTbVariant, 0) != MISOR_OK)
         CREATE_FAIL(MISOR_ENOMEM, "%s", g_err.c_str());
     if (hipStreamSynchronize(g->stream) != hipSuccess)
         CREATE_FAIL(MISOR_EHIP, "hipStreamSynchronize failed");
@@ -2076,15 +2080,20 @@ int misor_set_tuning(misor_grid* g, int key, int value) {
         return configure_sweep(g, g->sp.variant, g->sp.rows_per_block, value != 0);
     case MISOR_TUNE_SMALL_SOLVE: g->small_solve = value != 0; return MISOR_OK;
     case MISOR_TUNE_OVERLAP: g->overlap = value != 0; return MISOR_OK;
-    case MISOR_TUNE_TSTEPS: return configure_tb(g, value, g->tp.variant, g->tb_rows_req);
+    case MISOR_TUNE_TSTEPS:
+        g->tsteps_set = true;
+        return configure_tb(g, value, g->tp.variant, g->tb_rows_req);
     case MISOR_TUNE_TB_VARIANT: return configure_tb(g, g->tsteps, value, g->tb_rows_req);
     case MISOR_TUNE_TB_ROWS: return configure_tb(g, g->tsteps, g->tp.variant, value);
     case MISOR_TUNE_TB_PERSISTENT:
         g->tb_persistent = value != 0;
         return configure_tb(g, g->tsteps, g->tp.variant, g->tb_rows_req);
     case MISOR_TUNE_TB_CHAIN:
+        // without an explicit T request the default rule re-picks T (chained
+        // small blocks run T = 8, unchained ones T = 7)
         g->tb_chain = value < 0 ? -1 : value != 0;
-        return configure_tb(g, g->tsteps, g->tp.variant, g->tb_rows_req);
+        return configure_tb(g, g->tsteps_set ? g->tsteps : default_tsteps(g, g->tp.variant),
+                            g->tp.variant, g->tb_rows_req);
     case MISOR_TUNE_NS_FUSE: g->ns_fuse = value != 0; return MISOR_OK;
     case MISOR_TUNE_FINISH2: g->finish2 = value != 0; return MISOR_OK;
     case MISOR_TUNE_TB_RESERVE:

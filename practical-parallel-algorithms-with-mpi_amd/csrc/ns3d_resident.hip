@@ -88,6 +88,26 @@ __device__ __forceinline__ double rblock_sum(double v, double* sh) {
 // grid barrier number n (1-based): returns false if the solve was aborted.
 // mode (experiments, MISOR3_RESIDENT_MODE): bit 0 = the agent-scope fences by
 // thread 0 only (after a workgroup-scope release by every wave)
+//
+// The default hand-off (mode bits 4 + 5, no agent-scope fence) is the
+// "sc1 stores drained, sc1 loads" form of MI355X_MICROARCH.md (Workgroup
+// dispatch ... Valid forms, table row 1), a gfx950 property measured there and
+// not an architectural guarantee of the HIP memory model; the library is built
+// for gfx950 only.  The conditions it rests on, all held here:
+//  (1) every load of exchanged data (mailbox cells, partials) is a relaxed
+//      agent-scope atomic load (global_load ... sc1), never a plain load
+//      (mode 8 with plain loads read stale lines);
+//  (2) every store of it is a relaxed agent-scope atomic store (sc1);
+//  (3) every storing wave waits for its stores (s_waitcnt 0) before the
+//      workgroup barrier, and only then does ONE lane (thread 0) add to the
+//      arrival counter -- in the two-level form the group's last arriver,
+//      told by the value its own add returned, adds to the global counter;
+//  (4) the consumer polls the counter with sc1 loads (relaxed agent-scope
+//      atomic loads) from one lane and the other waves load only after the
+//      workgroup barrier that lane joins.
+// Agent-scope release / acquire fences instead (mode 0 / 1) are correct by
+// the memory model and cost an L2 write-back + invalidate per barrier: 41-69
+// us per iteration against 16.4 (profiles/r03_res3d_modes.txt).
 __device__ bool rgrid_sync(Bar3* bar, unsigned n, int* sh_flag, int mode) {
     if (mode & 24) {  // exchange data and partials by agent-scope atomics: no cache upkeep
         __builtin_amdgcn_s_waitcnt(0);  // this wave's stores acknowledged by memory
@@ -684,12 +704,18 @@ int resident3_boxes(const G3& g) {
     const int nbx = (g.I + kRbx - 1) / kRbx, nby = (g.J + kRby - 1) / kRby,
               nbz = (g.K + kRbz - 1) / kRbz;
     const long long nb = (long long)nbx * nby * nbz;
-    int dev = 0, cus = 0, per = 0;
+    // residency of BOTH resident kernels (the default mode launches
+    // k3_resident1, ~154 KB of LDS; k3_resident ~88 KB): the smaller answer, so
+    // the count reported here is one the launched kernel is admitted with
+    int dev = 0, cus = 0, per0 = 0, per1 = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(k3_resident),
-                                                     kRthreads, 0) != hipSuccess)
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per0, reinterpret_cast<const void*>(k3_resident),
+                                                     kRthreads, 0) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per1, reinterpret_cast<const void*>(k3_resident1), kRthreads, 0) != hipSuccess)
         return 0;
+    const int per = per0 < per1 ? per0 : per1;
     return nb <= (long long)cus * per && nb <= 256 ? (int)nb : 0;  // 256: partials slots
 }
 

@@ -40,8 +40,11 @@ region launches (T and the remainder steps % T) runs once before timing.
 
 cpu_baseline: the reference's own solveRB (assignment-4/src/solver.c:179-238,
 compiled in place by oracle/Makefile into oracle/_ref/libref.so) on one host
-core, on a bounded sample (8192^2 grid, 40 sweeps); falls back to the C
+core, on the bench's own 32768^2 grid (the device's fields after the timed
+solve), 3 sweeps, the solve timed alone; falls back to the C
 restatement (oracle/liboracle.so, kind "port") when _ref is absent.
+cpu_baseline_multicore: the restatement over every core of the affinity mask
+(pthreads over row bands), same grid, 10 sweeps.
 """
 from __future__ import annotations
 
@@ -65,36 +68,31 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(n=8192, sweeps=40, reps=3):
-    """Reference solveRB on 1 core, bounded sample, best of `reps` (median
-    reported beside it); returns the JSON object."""
-    import numpy as np
+def cpu_baseline(p, rhs, sweeps=3):
+    """The reference's own solveRB (assignment-4/src/solver.c:179-238, compiled
+    in place by oracle/Makefile into oracle/_ref/libref.so) on one host core,
+    on the bench's own grid: the fields the GPU holds after the timed solve,
+    `sweeps` iterations, the solve timed alone (init excluded, as
+    assignment-4/src/main.c:33-35 times solve()).  Falls back to the C
+    restatement (oracle/liboracle.so, kind "port") when _ref is absent."""
     import orc
 
-    kind = "reference" if orc.have_ref() else "port"
-    times = []
-    for _ in range(reps):
-        if kind == "reference":
-            R = orc.ref()
-            # refa4_run does init + solve; time init separately by a 0-sweep call
-            t0 = time.perf_counter()
-            R.refa4_run(n, n, 1.0, 1.0, 0, 1e-300, 1.9, 2, 1, None, None, None)
-            t1 = time.perf_counter()
-            it = R.refa4_run(n, n, 1.0, 1.0, sweeps, 1e-300, 1.9, 2, 1, None, None, None)
-            t2 = time.perf_counter()
-            times.append((t2 - t1) - (t1 - t0))
-        else:
-            p, rhs = orc.poisson_init(n, n)
-            t1 = time.perf_counter()
-            it, _ = orc.solve_rb(p, rhs, 1.0 / n, 1.0 / n, 1.9, 1e-300, sweeps)
-            times.append(time.perf_counter() - t1)
-        assert it == sweeps
-    best, med = min(times), float(np.median(times))
-    lup = float(n) * n * sweeps
-    return {"value": round(lup / best / 1e6, 2), "unit": "MLUP/s", "cores": 1, "kind": kind,
-            "median": round(lup / med / 1e6, 2), "cpu": cpu_model(),
-            "sample": "solveRB %dx%d, %d sweeps, best of %d (%.2f s solve, init excluded), "
-                      "1 host core" % (n, n, sweeps, reps, best)}
+    n = p.shape[1] - 2
+    if orc.have_ref():
+        kind = "reference"
+        it, sec = orc.ref_solve_rb_arrays(p, rhs, 1.0 / n, 1.0 / n, 1.9, 1e-300, sweeps)
+    else:
+        kind = "port"
+        t1 = time.perf_counter()
+        it, _ = orc.solve_rb(p, rhs, 1.0 / n, 1.0 / n, 1.9, 1e-300, sweeps)
+        sec = time.perf_counter() - t1
+    assert it == sweeps
+    lup = float(n) * (p.shape[0] - 2) * sweeps
+    return {"value": round(lup / sec / 1e6, 2), "unit": "MLUP/s", "cores": 1, "kind": kind,
+            "cpu": cpu_model(),
+            "sample": "solveRB on the bench's %dx%d grid (its fields after the timed solve), "
+                      "%d sweeps, one run (%.2f s solve, init excluded), 1 host core"
+                      % (n, p.shape[0] - 2, sweeps, sec)}
 
 
 def cpu_model():
@@ -107,28 +105,27 @@ def cpu_model():
     return None
 
 
-def cpu_baseline_multicore(n=8192, sweeps=40, reps=3):
-    """solveRB on all the host cores this job may use (no MPI on
-    the box, so pthreads over row bands, oracle/oracle_mt.c -- the restatement,
-    p bit-identical to the single-core solve); bounded sample, best of `reps`"""
-    import numpy as np
+def cpu_baseline_multicore(p, rhs, sweeps=10):
+    """solveRB on every host core the affinity mask allows (no MPI
+    on the box, so pthreads over row bands, oracle/oracle_mt.c -- the
+    restatement, p bit-identical to the single-core solve), on the bench's own
+    grid; one run of `sweeps` iterations"""
     import orc
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
-    times = []
-    for _ in range(reps):
-        p, rhs = orc.poisson_init(n, n)
-        t1 = time.perf_counter()
-        it, _ = orc.solve_rb_mt(p, rhs, 1.0 / n, 1.0 / n, 1.9, 1e-300, sweeps, threads)
-        times.append(time.perf_counter() - t1)
-        assert it == sweeps
-    best, med = min(times), float(np.median(times))
-    lup = float(n) * n * sweeps
-    return {"value": round(lup / best / 1e6, 1), "unit": "MLUP/s", "cores": threads,
-            "kind": "port", "median": round(lup / med / 1e6, 1), "cpu": cpu_model(),
-            "nproc": os.cpu_count(),
-            "sample": "solveRB %dx%d, %d sweeps, best of %d (%.2f s solve), %d threads over "
-                      "row bands (oracle/oracle_mt.c)" % (n, n, sweeps, reps, best, threads)}
+    n = p.shape[1] - 2
+    aff = len(os.sched_getaffinity(0))
+    threads = min(aff, 256)
+    t1 = time.perf_counter()
+    it, _ = orc.solve_rb_mt(p, rhs, 1.0 / n, 1.0 / n, 1.9, 1e-300, sweeps, threads)
+    sec = time.perf_counter() - t1
+    assert it == sweeps
+    lup = float(n) * (p.shape[0] - 2) * sweeps
+    return {"value": round(lup / sec / 1e6, 1), "unit": "MLUP/s", "cores": threads,
+            "kind": "port", "cpu": cpu_model(), "nproc": os.cpu_count(), "affinity": aff,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "sample": "solveRB on the bench's %dx%d grid, %d sweeps, one run (%.2f s), %d "
+                      "threads over row bands (oracle/oracle_mt.c)"
+                      % (n, p.shape[0] - 2, sweeps, sec, threads)}
 
 
 def pmc_summary(size, nranks, T, chain):
@@ -506,6 +503,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--tsteps", type=int, default=0,
                     help="iterations per kernel launch (0: library default)")
+    ap.add_argument("--tb-variant", type=int, default=-1,
+                    help="temporally blocked kernel variant (-1: library default)")
     ap.add_argument("--workload", choices=("poisson", "ns", "ns3d"), default="poisson",
                     help="poisson: the headline metric (config 4); ns: config 5, "
                          "dcavity NS weak scaling (--size cells^2 per GPU); ns3d: "
@@ -574,6 +573,8 @@ def main():
         comm_id = obj[0]
     g = M.Grid(imax, jmax, 1.0 / n, 1.0 / n, 1.9, 1e-300, args.steps, device=local_rank,
                nranks=world, rank=rank, comm_id=comm_id)
+    if args.tb_variant >= 0:
+        g.set_tuning(M.TUNE_TB_VARIANT, args.tb_variant)
     if args.tsteps > 0:
         g.set_tuning(M.TUNE_TSTEPS, args.tsteps)
     g.poisson_init(float(pdims[0]), float(pdims[1]), 2)
@@ -718,14 +719,17 @@ def main():
         # (SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES per wave, 2 waves per SIMD)
         out["roofline"]["valu"] = valu
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # the bench's own grid: the fields the device holds after the timed solve
+        hp, hrhs = g.download(M.P), g.download(M.RHS)
         try:
-            out["cpu_baseline"] = cpu_baseline()
+            out["cpu_baseline"] = cpu_baseline(hp, hrhs)
         except Exception as e:  # reported, never fatal for the GPU number
             out["cpu_baseline"] = {"value": None, "error": repr(e)}
         try:
-            out["cpu_baseline_multicore"] = cpu_baseline_multicore()
+            out["cpu_baseline_multicore"] = cpu_baseline_multicore(hp, hrhs)
         except Exception as e:
             out["cpu_baseline_multicore"] = {"value": None, "error": repr(e)}
+        del hp, hrhs
         for key in ("cpu_baseline", "cpu_baseline_multicore"):
             cb = out[key]
             out["config"][key + "_sample"] = "%s; %s cores (%s)" % (

@@ -65,13 +65,19 @@ int sweep_waves(int variant);
 // SIMD) or 4 (256-column strips, rhs ring in LDS, 1 wave per SIMD; T <= kMaxQuadT)
 // quad variants: sched = how far the compiler may interleave steps (sor_tb.h
 // qstep), max_t = the largest T whose LDS ring fits (2T + D (+1) rows of 2 KB per wave)
+// xch: the strips of a workgroup exchange their edge columns through LDS
+// (sor_tbx.h rb_tbx_kernel): the workgroup loads 128 W columns and owns
+// 128 W - 4T of them; its rhs ring is in LDS (max_t: two workgroups per CU)
 struct TbVariant {
-    int waves, ahead, cols, sched, max_t;
+    int waves, ahead, cols, sched, max_t, xch;
 };
-constexpr TbVariant kTbVariants[] = {{4, 2, 2, 0, kMaxT}, {8, 2, 2, 0, kMaxT}, {2, 2, 2, 0, kMaxT},
-                                     {1, 2, 2, 0, kMaxT}, {4, 3, 2, 0, kMaxT}, {4, 2, 4, 0, 8}};
-constexpr int kNumTbVariants = 6;
+constexpr TbVariant kTbVariants[] = {{4, 2, 2, 0, kMaxT, 0}, {8, 2, 2, 0, kMaxT, 0},
+                                     {2, 2, 2, 0, kMaxT, 0}, {1, 2, 2, 0, kMaxT, 0},
+                                     {4, 3, 2, 0, kMaxT, 0}, {4, 2, 4, 0, 8, 0},
+                                     {4, 2, 2, 0, 10, 1},    {8, 2, 2, 0, 10, 1}};
+constexpr int kNumTbVariants = 8;
 constexpr int kQuadTbVariant = 5;
+constexpr int kXchTbVariant = 6;
 // iterations per pass: 8 on large local blocks, 7 below kTsteps8Cells cells
 // (32768^2 0.744 vs 0.785 ms/iteration, profiles/r02_tune_t789.txt; one rank's
 // 8192 x 16384 block at 8 GPUs 0.118-0.122 at T = 7 vs 0.125 at T = 8,
@@ -94,6 +100,7 @@ int tb_resident(int T, int variant);
 int tb_cols(int variant);
 int tb_max_t(int variant);
 int tb_out_width(int T, int variant);           // owned columns of one wave's strip
+int tb_xch(int variant);                        // the exchange kernel (sor_tbx.h)
 int tb_nbx(int ni, int T, int variant);         // block columns of a pass of T iterations
 
 // Solver state that lives on the device between launches.  Written only by

@@ -3,6 +3,7 @@
 #include <algorithm>
 
 #include "sor_tb.h"
+#include "sor_tbx.h"
 
 #ifndef MISOR_TB_T
 #error "compile with -DMISOR_TB_T=<iterations per pass>"
@@ -34,6 +35,36 @@ static int resident_chain() {
     static int n = 0;
     if (n == 0) n = persistent_grid(rb_tbc_kernel<T, W, D, P2, E>, kLanes * W);
     return n;
+}
+
+template <int T, int W, int D, bool P2>
+static int residentx() {
+    static int n = 0;
+    if (n == 0) n = persistent_grid(rb_tbx_kernel<T, W, D, P2>, kLanes * W);
+    return n;
+}
+
+// the exchange variant exists for T = 1 .. 10 (its LDS ring: sor_tbx.h); the
+// templates keep the other units from instantiating it
+template <int TT>
+static int residentx_of(int variant) {
+    if constexpr (TT >= 1 && TT <= 10)
+        return variant == 7 ? residentx<TT, 8, 2, false>() : residentx<TT, 4, 2, false>();
+    else
+        return 0;
+}
+
+template <int TT, class Go>
+static void launchx(const SweepParams& prm, Go&& go) {
+    if constexpr (TT >= 1 && TT <= 10) {
+        if (prm.variant == 7) {
+            if (prm.pow2) go(rb_tbx_kernel<TT, 8, 2, true>, kLanes * 8, residentx<TT, 8, 2, true>());
+            else go(rb_tbx_kernel<TT, 8, 2, false>, kLanes * 8, residentx<TT, 8, 2, false>());
+        } else {
+            if (prm.pow2) go(rb_tbx_kernel<TT, 4, 2, true>, kLanes * 4, residentx<TT, 4, 2, true>());
+            else go(rb_tbx_kernel<TT, 4, 2, false>, kLanes * 4, residentx<TT, 4, 2, false>());
+        }
+    }
 }
 
 template <int T, int W, int D, int SC>
@@ -86,6 +117,10 @@ void MISOR_CAT(launch_tb_t, MISOR_TB_T)(hipStream_t s, const SweepParams& prm,
     };
 #define TB(W, DD) go(rb_tb_kernel<kT, W, DD, false>, kLanes * W, resident2<kT, W, DD, false>())
     // must match kTbVariants (misor_internal.h)
+    if (tb_xch(prm.variant)) {  // configure_tb keeps T within 2 .. max_t (10)
+        launchx<kT>(prm, go);
+        return;
+    }
     switch (prm.variant) {
     case 1: TB(8, 2); break;
     case 2:  // 2 strips per workgroup (finer slots for small rank blocks)
@@ -118,6 +153,8 @@ int MISOR_CAT(tb_resident_t, MISOR_TB_T)(int variant) {
     case 2: return resident2<kT, 2, 2, false>();
     case 3: return resident2<kT, 1, 2, false>();
     case 4: return resident2<kT, 4, 3, false>();
+    case 6:
+    case 7: return residentx_of<kT>(variant);
 #define Q4(V)                                                                             \
     case V:                                                                               \
         if constexpr (quad_ok<V>())                                                       \

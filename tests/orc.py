@@ -218,6 +218,9 @@ def ref():
                                 _dp, _dp, _dp]
         R.refns_run.restype = C.c_int
         R.refa4_read_parameter.argtypes = [C.c_char_p, _ip, _ip, _ip, _dp, _dp, _dp, _dp]
+        R.refa4_solve_rb_arrays.argtypes = [C.c_int, C.c_int, C.c_double, C.c_double,
+                                            C.c_double, C.c_double, C.c_int, _dp, _dp, _dp]
+        R.refa4_solve_rb_arrays.restype = C.c_int
         _ref = R
     return _ref
 
@@ -230,6 +233,16 @@ def ref_a4(imax, jmax, which="rb", itermax=1000000, eps=1e-6, omg=1.9, xlength=1
     it = ref().refa4_run(imax, jmax, xlength, ylength, itermax, eps, omg, problem, w,
                          _ptr(init_p), _ptr(p), _ptr(rhs))
     return it, p, rhs
+
+
+def ref_solve_rb_arrays(p, rhs, dx, dy, omega, eps, itermax):
+    """the reference's solveRB in place on p (assignment-4/src/solver.c:179-238);
+    returns (iterations, seconds of the solve alone)"""
+    jmax, imax = p.shape[0] - 2, p.shape[1] - 2
+    sec = C.c_double(0.0)
+    it = ref().refa4_solve_rb_arrays(imax, jmax, dx, dy, omega, eps, itermax, _ptr(p),
+                                     _ptr(rhs), C.byref(sec))
+    return it, sec.value
 
 
 def ref_ns(par, te=-1.0, max_steps=-1, solver=1, cap=1 << 20):

@@ -225,12 +225,19 @@ enum {
     MISOR_TUNE_TB_RESERVE = 12,    /* decomposed, overlapped: workgroup slots the persistent
                                     * interior launch leaves to the exchange / all-reduce /
                                     * edge-block streams (default 16) */
-    MISOR_TUNE_TB_CHAIN = 13       /* temporally blocked kernel, persistent, default variant:
+    MISOR_TUNE_TB_CHAIN = 13,      /* temporally blocked kernel, persistent, default variant:
                                     * 1 = chained vertical runs of short blocks with work
                                     * stealing (no warm-up rows between the blocks of a
                                     * run); 0 = one block per work item; -1 (default) =
                                     * chained on local blocks below 2^28 cells.  Get: 1 if
                                     * chained passes are in effect */
+    MISOR_TUNE_NEAR_BAND = 14      /* solveRB's loop test near its threshold: when an
+                                    * iteration's res lies within a relative 10^-value of
+                                    * eps^2, that iteration and the rest of the solve are
+                                    * recomputed one sweep at a time with an exact
+                                    * (order-independent) sum of r^2, so the iteration count
+                                    * and res do not depend on the partition.  Default 10;
+                                    * >= 300: off (set by tests to force the path: -30) */
 };
 int misor_set_tuning(misor_grid* g, int key, int value);
 int misor_get_tuning(const misor_grid* g, int key, int* value);

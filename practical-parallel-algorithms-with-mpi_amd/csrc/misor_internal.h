@@ -109,9 +109,11 @@ struct DevState {
     int it;        // iterations completed
     int done;      // 1 once (res >= eps^2 && it < itermax) is false
     int itermax;   // cap of the current solve call
-    int pad;
+    int near;      // 1: stopped before iteration it+1, whose res fell within nband of
+                   // eps^2 (misor_api.hip exact_tail recomputes from there)
     double res;    // residual of the last iteration
     double epssq;
+    double nband;  // |res - eps^2| <= nband: near the threshold (0: never)
     double sum[kMaxT];  // sum r^2 of each iteration of the last pass (this rank,
                         // then all-reduced)
 };
@@ -191,6 +193,9 @@ struct NsParams {
 // kernel launchers (sor_kernels.hip, ns_kernels.hip)
 void launch_sweep(hipStream_t s, const SweepParams& prm, const double* src, double* dst,
                   const double* rhs, double* partials, const DevState* st);
+// the same sweep (default variant's geometry) storing r^2 of every counted cell into rsq
+void launch_sweep_rsq(hipStream_t s, const SweepParams& prm, const double* src, double* dst,
+                      const double* rhs, double* partials, const DevState* st, double* rsq);
 // T iterations per pass: partials[t * nparts + block]
 void launch_finish(hipStream_t s, const double* partials, int nparts, int T, DevState* st,
                    double cells, int decide);

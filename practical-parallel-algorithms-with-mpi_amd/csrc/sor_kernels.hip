@@ -70,11 +70,13 @@ __device__ __forceinline__ void stv(double* p, d2 v) {
 
 // WAVES: strips per workgroup; D: rows of p / rhs kept in flight ahead of the
 // row being updated; NT: non-temporal stores of the new p (write-once stream)
-template <int WAVES, int D, bool NT, bool LNT>
+// RSQ: also store r^2 of every cell this block counts into rsq (same layout as
+// p) -- the exact, order-independent residual of misor_api.hip exact_tail
+template <int WAVES, int D, bool NT, bool LNT, bool RSQ = false>
 __global__ __launch_bounds__(kLanes* WAVES) void rb_sweep_kernel(
     SweepParams prm, const double* __restrict__ src, double* __restrict__ dst,
     const double* __restrict__ rhs, double* __restrict__ partials,
-    const DevState* __restrict__ st) {
+    const DevState* __restrict__ st, double* __restrict__ rsq = nullptr) {
     __shared__ double wsum[WAVES];
     if (st->done) return;  // converged or capped: the whole grid exits
 
@@ -141,6 +143,7 @@ __global__ __launch_bounds__(kLanes* WAVES) void rb_sweep_kernel(
         const double* sp = src + (long long)kYOff * pitch + kXOff + ia;
         const double* rp = rhs + (long long)kYOff * pitch + kXOff + ia;
         double* dp = dst + (long long)kYOff * pitch + kXOff + ia;
+        double* qp = RSQ ? rsq + (long long)kYOff * pitch + kXOff + ia : nullptr;
 
         auto ldp = [&](int j) { return ldv<LNT>(sp + (long long)j * pitch); };
         auto ldr = [&](int j) { return ldv<LNT>(rp + (long long)j * pitch); };
@@ -191,6 +194,7 @@ __global__ __launch_bounds__(kLanes* WAVES) void rb_sweep_kernel(
                                               ((Up.x - 2.0 * c) + Mm1.x) * idy2);
                     if (red_a) Mr.x = c - coef * rr;
                     if (in_a && own) acc += rr * rr;
+                    if (RSQ && in_a && own) qp[(long long)r * pitch] = rr * rr;
                     // right halo column c0+128 is red too (same parity as ia)
                     if (hr && in_h) {
                         const double ch = Hc.x;
@@ -207,6 +211,7 @@ __global__ __launch_bounds__(kLanes* WAVES) void rb_sweep_kernel(
                                               ((Up.y - 2.0 * c) + Mm1.y) * idy2);
                     if (red_b) Mr.y = c - coef * rr;
                     if (in_b && own) acc += rr * rr;
+                    if (RSQ && in_b && own) qp[(long long)r * pitch + 1] = rr * rr;
                     // left halo column c0-1 is red (same parity as ib)
                     if (hl && in_h) {
                         const double ch = Hc.y;
@@ -231,6 +236,7 @@ __global__ __launch_bounds__(kLanes* WAVES) void rb_sweep_kernel(
                     if (in_a) {
                         F.x = c - coef * rr;
                         acc += rr * rr;
+                        if (RSQ) qp[(long long)jw * pitch] = rr * rr;
                     }
                 } else {
                     // row r-1 has q' = 0: column ib black
@@ -242,6 +248,7 @@ __global__ __launch_bounds__(kLanes* WAVES) void rb_sweep_kernel(
                     if (in_b) {
                         F.y = c - coef * rr;
                         acc += rr * rr;
+                        if (RSQ) qp[(long long)jw * pitch + 1] = rr * rr;
                     }
                 }
 
@@ -377,6 +384,11 @@ __global__ __launch_bounds__(kFinishThreads) void rb_finish_kernel(
                 st->sum[g] = tot[g];  // decomposed: all-reduce, then decide
             } else if (!st->done) {
                 const double res = tot[g] / cells;
+                if (fabs(res - st->epssq) <= st->nband) {  // near: stop before it
+                    st->near = 1;
+                    st->done = 1;
+                    continue;
+                }
                 const int it = st->it + 1;
                 st->res = res;
                 st->it = it;
@@ -463,6 +475,14 @@ void launch_sweep(hipStream_t s, const SweepParams& prm, const double* src, doub
 #undef SWEEP
 }
 
+void launch_sweep_rsq(hipStream_t s, const SweepParams& prm, const double* src, double* dst,
+                      const double* rhs, double* partials, const DevState* st, double* rsq) {
+    // the default sweep variant's geometry (kDefaultSweepVariant: 8 strips, 2 rows
+    // in flight, nt stores); the exact tail sets up prm with it
+    hipLaunchKernelGGL((rb_sweep_kernel<8, 2, true, false, true>), dim3(prm.nblocks),
+                       dim3(kLanes * 8), 0, s, prm, src, dst, rhs, partials, st, rsq);
+}
+
 void launch_finish(hipStream_t s, const double* partials, int nparts, int T, DevState* st,
                    double cells, int decide) {
     hipLaunchKernelGGL(rb_finish_kernel, dim3(1), dim3(kFinishThreads), 0, s, partials, nparts, T, st,
@@ -477,18 +497,24 @@ __global__ void rb_decide_kernel(DevState* st, int T, double cells) {
     double sum[kMaxT];
 #pragma unroll
     for (int g = 0; g < kMaxT; ++g) sum[g] = g < T ? st->sum[g] : 0.0;
-    const double epssq = st->epssq;
+    const double epssq = st->epssq, nband = st->nband;
     const int itermax = st->itermax;
-    int it = st->it, done = 0;
+    int it = st->it, done = 0, near = 0;
     double res = st->res;
     for (int g = 0; g < T && !done; ++g) {
-        res = sum[g] / cells;
+        const double r = sum[g] / cells;
+        if (fabs(r - epssq) <= nband) {  // near the threshold: stop before this iteration
+            near = done = 1;
+            break;
+        }
+        res = r;
         ++it;
         done = !((res >= epssq) && (it < itermax));
     }
     st->res = res;
     st->it = it;
     st->done = done;
+    st->near = near;
 }
 
 void launch_decide(hipStream_t s, DevState* st, int T, double cells) {
@@ -556,10 +582,10 @@ __global__ __launch_bounds__(kSmallThreads) void rb_solve_small_kernel(
     }
     __syncthreads();
 
-    const double epssq = st->epssq;
+    const double epssq = st->epssq, nband = st->nband;
     const int itermax = st->itermax;
-    double res = 1.0;
-    int it = 0;
+    double res = st->res;
+    int it = st->it, near = 0;
     while ((res >= epssq) && (it < itermax)) {
         double acc = 0.0;
 #pragma unroll
@@ -597,18 +623,26 @@ __global__ __launch_bounds__(kSmallThreads) void rb_solve_small_kernel(
             red[16] = s;
         }
         __syncthreads();
-        res = red[16] / cells;
+        const double rn = red[16] / cells;
+        if (fabs(rn - epssq) <= nband) {  // near the threshold: p is left as it was;
+            near = 1;                      // the host reruns up to it iterations
+            break;
+        }
+        res = rn;
         ++it;
     }
 
-    for (long long k = t; k < ncell; k += kSmallThreads) {
-        const int i = (int)(k % W), j = (int)(k / W);
-        p_glob[(long long)(j + kYOff) * pitch + (i + kXOff)] = P[k];
+    if (!near) {
+        for (long long k = t; k < ncell; k += kSmallThreads) {
+            const int i = (int)(k % W), j = (int)(k / W);
+            p_glob[(long long)(j + kYOff) * pitch + (i + kXOff)] = P[k];
+        }
     }
     if (t == 0) {
         st->it = it;
         st->res = res;
         st->done = 1;
+        st->near = near;
     }
 }
 

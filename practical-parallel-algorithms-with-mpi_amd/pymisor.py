@@ -26,7 +26,7 @@ SOLVE_RB, SOLVE_RBA = 0, 1
 LEX_A4, LEX_SEQ = 0, 1
 (TUNE_SWEEP_VARIANT, TUNE_ROWS_PER_BLOCK, TUNE_XCD_REMAP, TUNE_SMALL_SOLVE, TUNE_OVERLAP,
  TUNE_TSTEPS, TUNE_TB_VARIANT, TUNE_TB_ROWS, TUNE_TB_PERSISTENT, TUNE_NS_FUSE,
- TUNE_FINISH2, TUNE_TB_RESERVE, TUNE_TB_CHAIN) = 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13
+ TUNE_FINISH2, TUNE_TB_RESERVE, TUNE_TB_CHAIN, TUNE_NEAR_BAND) = range(1, 15)
 COMM_ID_BYTES = 128
 # 3D field ids (misor3_*)
 P3, RHS3, U3, V3, W3, F3, G3, H3 = range(8)

@@ -24,7 +24,10 @@ def child(a):
     if a.lib:
         M.LIBPATH = os.path.abspath(a.lib)
     n, T = a.size, a.tsteps
-    g = M.Grid(n, n, 1.0 / n, 1.0 / n, 1.9, 1e-300, 1 << 20, device=0)
+    ni, nj = a.ni or n, a.nj or n
+    g = M.Grid(ni, nj, 1.0 / n, 1.0 / n, 1.9, 1e-300, 1 << 20, device=0)
+    if a.variant >= 0:
+        g.set_tuning(M.TUNE_TB_VARIANT, a.variant)
     g.set_tuning(M.TUNE_TSTEPS, T)
     if a.rows:
         g.set_tuning(M.TUNE_TB_ROWS, a.rows)
@@ -48,6 +51,9 @@ def main():
     ap.add_argument("--size", type=int, default=32768)
     ap.add_argument("--tsteps", type=int, default=7)
     ap.add_argument("--rows", type=int, default=0)
+    ap.add_argument("--ni", type=int, default=0, help="grid columns (default --size)")
+    ap.add_argument("--nj", type=int, default=0, help="grid rows (default --size)")
+    ap.add_argument("--variant", type=int, default=-1, help="TB variant (-1: default)")
     ap.add_argument("--passes", type=int, default=6)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--child", action="store_true")
@@ -59,7 +65,8 @@ def main():
         for v in a.values.split(","):
             env = dict(os.environ, **{a.var: v})
             cmd = [sys.executable, __file__, "--child", "--size", str(a.size), "--tsteps",
-                   str(a.tsteps), "--rows", str(a.rows), "--passes", str(a.passes)]
+                   str(a.tsteps), "--rows", str(a.rows), "--passes", str(a.passes),
+                   "--ni", str(a.ni), "--nj", str(a.nj), "--variant", str(a.variant)]
             if a.lib:
                 cmd += ["--lib", a.lib]
             out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
@@ -74,7 +81,7 @@ def main():
         ms = sorted(d["ms_iter"] for d in res[v])
         print("%s=%s rows=%d ms/iter med %.4f min %.4f  MLUP/s %.0f" % (
             a.var, v, res[v][0]["rows"], ms[len(ms) // 2], ms[0],
-            float(a.size) ** 2 / (ms[len(ms) // 2] * 1e-3) / 1e6))
+            float(a.ni or a.size) * (a.nj or a.size) / (ms[len(ms) // 2] * 1e-3) / 1e6))
     print("identical p across settings: %s" % (len(hashes) == 1))
 
 

@@ -1587,7 +1587,9 @@ static int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* 
     s0.res = res0;
     s0.epssq = epssq;
     s0.itermax = itermax;
-    s0.nband = g->near_rel > 0.0 ? g->near_rel * epssq : -1.0;
+    // (eps^2 = 0 -- e.g. eps = 1e-300 -- has no threshold to come near: res >= 0
+    // always continues the loop)
+    s0.nband = g->near_rel > 0.0 && epssq > 0.0 ? g->near_rel * epssq : -1.0;
     s0.done = !((res0 >= epssq) && (it0 < itermax));  // loop test of solver.c:197
     if (s0.done) {
         if (iters) *iters = it0;

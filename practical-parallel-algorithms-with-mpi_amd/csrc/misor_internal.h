@@ -74,8 +74,9 @@ struct TbVariant {
 constexpr TbVariant kTbVariants[] = {{4, 2, 2, 0, kMaxT, 0}, {8, 2, 2, 0, kMaxT, 0},
                                      {2, 2, 2, 0, kMaxT, 0}, {1, 2, 2, 0, kMaxT, 0},
                                      {4, 3, 2, 0, kMaxT, 0}, {4, 2, 4, 0, 8, 0},
-                                     {4, 2, 2, 0, 10, 1},    {8, 2, 2, 0, 10, 1}};
-constexpr int kNumTbVariants = 8;
+                                     {4, 2, 2, 0, 10, 1},    {8, 2, 2, 0, 10, 1},
+                                     {2, 2, 2, 0, 10, 1}};
+constexpr int kNumTbVariants = 9;
 constexpr int kQuadTbVariant = 5;
 constexpr int kXchTbVariant = 6;
 // iterations per pass: 8 on large local blocks, 7 below kTsteps8Cells cells

@@ -49,7 +49,9 @@ static int residentx() {
 template <int TT>
 static int residentx_of(int variant) {
     if constexpr (TT >= 1 && TT <= 10)
-        return variant == 7 ? residentx<TT, 8, 2, false>() : residentx<TT, 4, 2, false>();
+        return variant == 7   ? residentx<TT, 8, 2, false>()
+               : variant == 8 ? residentx<TT, 2, 2, false>()
+                              : residentx<TT, 4, 2, false>();
     else
         return 0;
 }
@@ -60,6 +62,9 @@ static void launchx(const SweepParams& prm, Go&& go) {
         if (prm.variant == 7) {
             if (prm.pow2) go(rb_tbx_kernel<TT, 8, 2, true>, kLanes * 8, residentx<TT, 8, 2, true>());
             else go(rb_tbx_kernel<TT, 8, 2, false>, kLanes * 8, residentx<TT, 8, 2, false>());
+        } else if (prm.variant == 8) {
+            if (prm.pow2) go(rb_tbx_kernel<TT, 2, 2, true>, kLanes * 2, residentx<TT, 2, 2, true>());
+            else go(rb_tbx_kernel<TT, 2, 2, false>, kLanes * 2, residentx<TT, 2, 2, false>());
         } else {
             if (prm.pow2) go(rb_tbx_kernel<TT, 4, 2, true>, kLanes * 4, residentx<TT, 4, 2, true>());
             else go(rb_tbx_kernel<TT, 4, 2, false>, kLanes * 4, residentx<TT, 4, 2, false>());

@@ -70,6 +70,9 @@ namespace {
 #ifndef XLA
 #define XLA 2   // stages of LDS reads in flight ahead of the computing stage
 #endif
+#ifndef XEARLY
+#define XEARLY 1  // publish a stage's edge values right after the stage, not at the step's end
+#endif
 
 // LDS ring slots (rows of rhs for stages 1 .. T-1) and the warm-up length
 template <int T>
@@ -197,24 +200,29 @@ __device__ __forceinline__ d2 xstage(const XLane& c, int t, int rin, d2 In, d2& 
 
 // the LDS traffic of a step's end: this step's edge values for the neighbours'
 // next step (colour 1 - Q), rhs row n-1 into its ring slot; then the barrier
-template <int T, int D, int Q>
-__device__ __forceinline__ void xpublish(XMarch<T, D>& m, double* xw, double* ringslot, int lane) {
+// stage t's edge values (its A and M1 after the stage) for the neighbours' next step
+template <int Q>
+__device__ __forceinline__ void xpub_stage(const d2& A, const d2& M1, double* xw, int t,
+                                           int lane) {
     if (Q == 1) {  // next step is colour 0: the right neighbour reads lane 63's .y
         if (lane == kLanes - 1) {
-#pragma unroll
-            for (int t = 0; t < T; ++t) {
-                xw[2 * t] = m.A[t].y;
-                xw[2 * t + 1] = m.M1[t].y;
-            }
+            xw[2 * t] = A.y;
+            xw[2 * t + 1] = M1.y;
         }
     } else {  // next step is colour 1: the left neighbour reads lane 0's .x
         if (lane == 0) {
-#pragma unroll
-            for (int t = 0; t < T; ++t) {
-                xw[2 * t] = m.A[t].x;
-                xw[2 * t + 1] = m.M1[t].x;
-            }
+            xw[2 * t] = A.x;
+            xw[2 * t + 1] = M1.x;
         }
+    }
+}
+
+template <int T, int D, int Q>
+__device__ __forceinline__ void xpublish(XMarch<T, D>& m, double* xw, double* ringslot, int lane,
+                                         bool stages = true) {
+    if (stages) {
+#pragma unroll
+        for (int t = 0; t < T; ++t) xpub_stage<Q>(m.A[t], m.M1[t], xw, t, lane);
     }
     ringslot[lane] = m.R1.x;
     ringslot[kLanes + lane] = m.R1.y;
@@ -288,19 +296,31 @@ __device__ __forceinline__ void xsteady_step(XMarch<T, D>& m, const XLane& c, co
 #pragma unroll
     for (int t = 0; t <= LA; ++t) issue(t);
     if (XHOIST) __builtin_amdgcn_sched_barrier(0);
+    double* const xw = &sh.xch[PAR][wave + 1][0][0];
+    double* const rslot = &sh.ring[wave][(PH - 1 + S) % S][0][0];
     d2 v = m.Pq[0];
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         v = xstage<T, Q, kSteady, P2>(c, t, 0, v, m.A[t], m.M1[t], m.M2[t], rr[t], rb[t], nA[t],
                                       nM[t], io.idx2, io.idy2, io.coef, m.acc[t]);
+        // XEARLY: the stage's edge values go out at once, so the step's closing
+        // wait covers the last stage's write only; rhs row n-1 goes into its slot
+        // once the last read of that slot (stage T-1's black, in this step) is
+        // issued (a wave's LDS operations complete in order)
+        if (XEARLY) xpub_stage<Q>(m.A[t], m.M1[t], xw, t, lane);
         if (t + LA + 1 < T) {
             issue(t + LA + 1);
+            if (XEARLY && t + LA + 1 == T - 1) {
+                rslot[lane] = m.R1.x;
+                rslot[kLanes + lane] = m.R1.y;
+            }
             if (XHOIST) __builtin_amdgcn_sched_barrier(0);
         }
     }
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), io.d, io.st_lane, so, 2);
-    xpublish<T, D, Q>(m, &sh.xch[PAR][wave + 1][0][0],
-                      &sh.ring[wave][(PH - 1 + S) % S][0][0], lane);
+    if (!XEARLY || LA + 1 >= T) {  // (LA + 1 >= T: every read was issued at the start)
+        xpublish<T, D, Q>(m, xw, rslot, lane, !XEARLY);
+    }
     // the store reads its data VGPRs after it issues (sor_tb.h steady_step)
     asm volatile("" ::"v"(m.keep[0]));
     m.keep[0] = m.keep[1];

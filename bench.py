@@ -105,6 +105,15 @@ def cpu_model():
     return None
 
 
+def cgroup_cpus():
+    """CPUs granted by the cgroup v2 quota (cpu.max "quota period"), or None"""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline_multicore(p, rhs, sweeps=10):
     """solveRB on every host core the affinity mask allows (no MPI
     on the box, so pthreads over row bands, oracle/oracle_mt.c -- the
@@ -114,7 +123,13 @@ def cpu_baseline_multicore(p, rhs, sweeps=10):
 
     n = p.shape[1] - 2
     aff = len(os.sched_getaffinity(0))
-    threads = min(aff, 256)
+    quota = cgroup_cpus()
+    # threads: the cores this process may actually run on at once -- the
+    # affinity mask, capped by a cgroup CPU quota and by OMP_NUM_THREADS (the
+    # GPU box shows its whole machine in the mask but grants a share of it,
+    # which it states in OMP_NUM_THREADS; 256 threads there ran at 1.8x one)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    threads = max(1, min(aff, 256, quota or 256, int(omp) if omp.isdigit() and int(omp) > 0 else 256))
     t1 = time.perf_counter()
     it, _ = orc.solve_rb_mt(p, rhs, 1.0 / n, 1.0 / n, 1.9, 1e-300, sweeps, threads)
     sec = time.perf_counter() - t1
@@ -122,6 +137,7 @@ def cpu_baseline_multicore(p, rhs, sweeps=10):
     lup = float(n) * (p.shape[0] - 2) * sweeps
     return {"value": round(lup / sec / 1e6, 1), "unit": "MLUP/s", "cores": threads,
             "kind": "port", "cpu": cpu_model(), "nproc": os.cpu_count(), "affinity": aff,
+            "cgroup_cpus": quota,
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
             "sample": "solveRB on the bench's %dx%d grid, %d sweeps, one run (%.2f s), %d "
                       "threads over row bands (oracle/oracle_mt.c)"

@@ -20,9 +20,10 @@ namespace misor {
 //  - kXOff = 15 puts the first interior column i = 1 on a 128-byte boundary,
 //    so every wave's 16-byte-per-lane row segment of 128 cells starts a cache
 //    line; the ghost column i = 0 is the last double of the preceding line.
-//  - kYOff = 2 * kMaxT + 2 rows below row 0 and as many (+ prefetch run-out)
+//  - kYOff = 2 * kMaxT + 16 rows below row 0 and as many (+ prefetch run-out)
 //    above row nj+1: a block of the temporally blocked sweep streams rows
-//    j0-2T-1 .. j1-1+2T (+ rows in flight) without clamping, and its first
+//    j0-2T-1 .. j1-1+2T (+ rows in flight; the split-ring march up to 14
+//    more warm-up rows below, sor_tbh.h) without clamping, and its first
 //    strip's columns from 1 - 2T (the tail of the row below, in the
 //    allocation: a left halo of depth 2 kMaxT too).
 //  - pitch = 160 + round_up(ni, kStripCells * kMaxWavesX): left pad line, the
@@ -32,7 +33,7 @@ namespace misor {
 // ---------------------------------------------------------------------------
 constexpr int kXOff = 15;
 constexpr int kMaxT = 12;                // iterations per temporally blocked pass (max)
-constexpr int kYOff = 2 * kMaxT + 2;
+constexpr int kYOff = 2 * kMaxT + 16;
 constexpr int kLanes = 64;                 // wavefront
 constexpr int kStripCells = 2 * kLanes;    // 128 columns per wave (2 per lane)
 constexpr int kMaxWavesX = 16;             // strips per sweep workgroup (max)
@@ -68,15 +69,23 @@ int sweep_waves(int variant);
 // xch: the strips of a workgroup exchange their edge columns through LDS
 // (sor_tbx.h rb_tbx_kernel): the workgroup loads 128 W columns and owns
 // 128 W - 4T of them; its rhs ring is in LDS (max_t: two workgroups per CU)
+// skew: the steady march in two independent stage chains per step (sor_tb.h
+// skew_step); lds: rows in flight per array through an LDS queue (sor_tb.h
+// steady_step DL); hr: the split rhs ring, registers + LDS (sor_tbh.h)
 struct TbVariant {
-    int waves, ahead, cols, sched, max_t, xch;
+    int waves, ahead, cols, sched, max_t, xch, skew, lds, hr;
 };
 constexpr TbVariant kTbVariants[] = {{4, 2, 2, 0, kMaxT, 0}, {8, 2, 2, 0, kMaxT, 0},
                                      {2, 2, 2, 0, kMaxT, 0}, {1, 2, 2, 0, kMaxT, 0},
                                      {4, 3, 2, 0, kMaxT, 0}, {4, 2, 4, 0, 8, 0},
                                      {4, 2, 2, 0, 10, 1},    {8, 2, 2, 0, 10, 1},
-                                     {2, 2, 2, 0, 10, 1}};
-constexpr int kNumTbVariants = 9;
+                                     {2, 2, 2, 0, 10, 1},    {4, 2, 2, 0, kMaxT, 0, 1},
+                                     {4, 2, 2, 0, kMaxT, 0, 0, 8}, {4, 2, 2, 0, kMaxT, 0, 0, 4},
+                                     {4, 2, 2, 0, kMaxT, 0, 0, 0, 1}, {4, 2, 2, 0, kMaxT, 0, 1, 0, 1}};
+constexpr int kNumTbVariants = 14;
+constexpr int kHrTbVariant = 12;   // 13: skewed (T >= 2; T = 1 as 12)
+constexpr int kSkewTbVariant = 9;
+constexpr int kLdsTbVariant = 10;  // 8 rows in flight; 11: 4
 constexpr int kQuadTbVariant = 5;
 constexpr int kXchTbVariant = 6;
 // iterations per pass: 8 on large local blocks, 7 below kTsteps8Cells cells
@@ -94,6 +103,25 @@ constexpr int kTbSmallRows = 32;       // short block rows the work order takes 
 constexpr int kTbSmallRounds = 2;      // ... about this many resident rounds of them
 constexpr int kTbReserve = 16;         // slots a pipelined interior launch leaves free
 int tb_waves(int variant);
+// the split rhs ring (sor_tbh.h): stages 0 .. K-1 read registers, the rest LDS;
+// both rings have S slots, S = max(2K + D, 2(T - K) + 1) rounded up to even.
+// K: as few register stages as the LDS allows -- S <= kHrMaxSlots rows of 1 KB
+// per wave (two workgroups of four waves: 144 KB of the CU's 160)
+constexpr int kHrMaxSlots = 18;
+// The skewed form (sk = 1) keeps one more row in each ring.
+__host__ __device__ constexpr int hr_cost(int T, int D, int k, int sk = 0) {
+    const int a = 2 * k + D + sk, b = 2 * (T - k) + 1 + sk;
+    const int s = a > b ? a : b;
+    return s + (s & 1);
+}
+__host__ __device__ constexpr int hr_k(int T, int D, int sk = 0) {
+    for (int k = 0; k <= T; ++k)
+        if (hr_cost(T, D, k, sk) <= kHrMaxSlots) return k;
+    return T;
+}
+__host__ __device__ constexpr int hr_slots(int T, int D, int sk = 0) {
+    return hr_cost(T, D, hr_k(T, D, sk), sk);
+}
 // rhs ring slots of the steady march: interior block heights are multiples of it
 int tb_ring_slots(int T, int variant);
 // workgroups of a persistent pass resident on the device at once

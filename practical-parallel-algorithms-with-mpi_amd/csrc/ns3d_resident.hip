@@ -42,6 +42,7 @@
 // lines were still cached.
 
 #include <cstdlib>
+#include <type_traits>
 
 #include "misor_internal.h"
 
@@ -75,14 +76,18 @@ __device__ __forceinline__ double rwave_sum(double v) {
     return v;
 }
 
-// fixed-order sum over the workgroup (wave trees, then waves 0..3 in order);
-// every thread gets the result
+// fixed-order sum over the workgroup (wave trees, then waves 0..NW-1 in
+// order); every thread gets the result
+template <int NW = 4>
 __device__ __forceinline__ double rblock_sum(double v, double* sh) {
     v = rwave_sum(v);
     __syncthreads();
     if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
     __syncthreads();
-    return ((sh[0] + sh[1]) + sh[2]) + sh[3];
+    double s = sh[0];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) s += sh[w];
+    return s;
 }
 
 // grid barrier number n (1-based): returns false if the solve was aborted.
@@ -158,6 +163,55 @@ __device__ bool rgrid_sync(Bar3* bar, unsigned n, int* sh_flag, int mode) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     else if (!(mode & 1))
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    return *sh_flag == 0;
+}
+
+// rgrid_sync in two halves (the exchange-by-atomics modes, bits 3 / 4): arrive
+// (every wave's stores acknowledged, then thread 0 counts the workgroup in)
+// and wait; the workgroup may compute in between anything that reads no
+// exchanged data and writes none
+__device__ void rgrid_arrive(Bar3* bar, unsigned n, int mode) {
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (mode & 32) {
+            const unsigned x = blockIdx.x & 7, nb = gridDim.x;
+            const unsigned cx = (nb - x + 7) / 8;
+            const unsigned old = __hip_atomic_fetch_add(&bar->xcd[16 * x], 1u, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+            if (old + 1 == n * cx)
+                __hip_atomic_fetch_add(&bar->count, 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_fetch_add(&bar->count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+__device__ bool rgrid_wait(Bar3* bar, unsigned n, int* sh_flag, int mode) {
+    if (threadIdx.x == 0) {
+        const unsigned nb = gridDim.x;
+        const unsigned target = (mode & 32) ? n * (nb < 8 ? nb : 8) : n * nb;
+        int ab = 0;
+        long long polls = 0;
+        while (__hip_atomic_load(&bar->count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+               target) {
+            if (__hip_atomic_load(&bar->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                ab = 1;
+                break;
+            }
+            if (++polls > kSpinLimit) {
+                __hip_atomic_store(&bar->abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ab = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        *sh_flag = ab;
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     return *sh_flag == 0;
 }
 
@@ -377,12 +431,8 @@ __global__ __launch_bounds__(kRthreads, 1) void k3_resident(G3 g, double* __rest
 // iteration n's); p is only read at the start and written at the end.
 constexpr int kTsx = kRbx + 4, kTsy = (kRby + 4) * kTsx, kTcells = (kRbz + 4) * kTsy;
 constexpr int kTring = 2 * (kRby * kRbz + kRbx * kRbz + kRbx * kRby);  // inner-layer face cells
-constexpr int kTrq = kTring / kRthreads;
 constexpr int kTshell = 2 * kTring + 4 * (kRbx + kRby + kRbz);  // received positions
-constexpr int kTsq = (kTshell + kRthreads - 1) / kRthreads;
-static_assert(kTring % kRthreads == 0, "ring cells per thread");
 constexpr int kTrx = kTshell / 2 + 128;  // black cells of the shell, at most
-constexpr int kTrxq = (kTrx + kRthreads - 1) / kRthreads;
 
 // shell position f (0 .. kTshell): face layers 0/1 and B+2/B+3, then the
 // inner layer's 12 edges; LDS coordinates (shell offset 2)
@@ -446,19 +496,24 @@ __device__ __forceinline__ void ring_pos(int f, int& lx, int& ly, int& lz) {
     (void)FZ;
 }
 
-__global__ __launch_bounds__(kRthreads, 1) void k3_resident1(G3 g, double* __restrict__ p,
-                                                             const double* __restrict__ rhs,
-                                                             double idx2, double idy2,
-                                                             double idz2, double factor,
-                                                             double cells,
-                                                             double* __restrict__ partials,
-                                                             DevState* __restrict__ st,
-                                                             Bar3* __restrict__ bar, int nbx,
-                                                             int nby, int mode,
-                                                             double* __restrict__ mbox,
-                                                             int mstride) {
+// NT threads per box: thread t owns the column pair t & 15 of row (t >> 4) & 15
+// in the PZ = 16 * 256 / NT planes from (t >> 8) * PZ (NT = 1024: four waves
+// per SIMD to cover the LDS and FP64 latency of the passes)
+// REG: every box lies wholly inside the domain (I, J, K multiples of the box:
+// the reference's 128^3) -- the register form of the passes (below)
+template <int NT, bool REG = false>
+__global__ __launch_bounds__(NT, 1) void k3_resident1(G3 g, double* __restrict__ p,
+                                                      const double* __restrict__ rhs, double idx2,
+                                                      double idy2, double idz2, double factor,
+                                                      double cells, double* __restrict__ partials,
+                                                      DevState* __restrict__ st,
+                                                      Bar3* __restrict__ bar, int nbx, int nby,
+                                                      int mode, double* __restrict__ mbox,
+                                                      int mstride) {
+    constexpr int NW = NT / 64, PZ = kRbz * 256 / NT, G = NT >= 1024 ? 2 : (PZ < kRg ? PZ : kRg);
+    static_assert(NT % 256 == 0 && PZ % 2 == 0 && PZ % G == 0 && G % 2 == 0, "thread layout");
     __shared__ double L[kTcells];
-    __shared__ double sh[4];
+    __shared__ double sh[NW];
     __shared__ int sh_flag;
     // built once: the shell's black cells to receive (LDS index | ghost-face bits
     // << 16, global offset) and the inner layer's red cells (LDS index | ghost
@@ -486,19 +541,19 @@ __global__ __launch_bounds__(kRthreads, 1) void k3_resident1(G3 g, double* __res
     };
 
     // p: the box and its two-cell shell (ghosts included; outside the array: 0)
-    for (int q = t; q < kTcells; q += kRthreads) {
+    for (int q = t; q < kTcells; q += NT) {
         const int lz = q / kTsy, ly = q / kTsx % (kRby + 4), lx = q % kTsx;
         const int i = ox - 2 + lx, jj = oy - 2 + ly, k = oz - 2 + lz;
         L[q] = (i >= 0 && jj >= 0 && k >= 0 && i <= I + 1 && jj <= J + 1 && k <= K + 1)
                    ? p[gof(i, jj, k)]
                    : 0.0;
     }
-    const int px = t & 15, y = t >> 4;
+    const int px = t & 15, y = (t >> 4) & 15, zb = (t >> 8) * PZ;
     const int i0 = ox + 2 * px, j = oy + y;
-    double rh[kRbz][2];
+    double rh[PZ][2];  // rh[z - zb]
 #pragma unroll
-    for (int z = 0; z < kRbz; ++z) {
-        const int k = oz + z;
+    for (int z = 0; z < PZ; ++z) {
+        const int k = oz + zb + z;
 #pragma unroll
         for (int e = 0; e < 2; ++e)
             rh[z][e] = (i0 + e <= I && j <= J && k <= K) ? rhs[gof(i0 + e, j, k)] : 0.0;
@@ -509,7 +564,7 @@ __global__ __launch_bounds__(kRthreads, 1) void k3_resident1(G3 g, double* __res
     };
     if (t == 0) n_rx = n_ring = 0;
     __syncthreads();
-    for (int f = t; f < kTring; f += kRthreads) {
+    for (int f = t; f < kTring; f += NT) {
         int lx, ly, lz;
         ring_pos(f, lx, ly, lz);
         const int i = ox - 2 + lx, jj = oy - 2 + ly, k = oz - 2 + lz;
@@ -519,7 +574,7 @@ __global__ __launch_bounds__(kRthreads, 1) void k3_resident1(G3 g, double* __res
             ring_r[q] = rhs[gof(i, jj, k)];
         }
     }
-    for (int f = t; f < kTshell; f += kRthreads) {
+    for (int f = t; f < kTshell; f += NT) {
         int lx, ly, lz;
         shell_pos(f, lx, ly, lz);
         const int i = ox - 2 + lx, jj = oy - 2 + ly, k = oz - 2 + lz;
@@ -561,47 +616,124 @@ __global__ __launch_bounds__(kRthreads, 1) void k3_resident1(G3 g, double* __res
         return r;
     };
     double acc = 0.0;
+    // red cells one or more cells inside the box surface read only the box's
+    // black cells: they are computed into registers while the grid barrier
+    // completes (mode bit 11 off; sv, sacc) and written by commit() once the
+    // loop test says the iteration runs
+    auto deep = [&](int x, int z) {
+        return x >= 1 && x <= kRbx - 2 && y >= 1 && y <= kRby - 2 && z >= 1 && z <= kRbz - 2;
+    };
+    double sv[PZ];
+    double sacc = 0.0;
+    unsigned smask = 0;
+    // The thread's own cells (column pair, PZ planes) also live in registers
+    // when the box lies wholly inside the domain (every workgroup at 128^3):
+    // a cell's own value, its pair partner and its z-neighbours inside the
+    // thread's planes come from there, the rest (the far x-neighbour, y, the
+    // planes beyond) from LDS -- 3.5 LDS reads per update instead of 7 (the
+    // passes were LDS-bound).  LDS stays the complete copy (every update is
+    // written back): the neighbours read it.
+    double own[PZ][2];
     // the box's cells of colour col (1: red, i+j+k odd); black cells within two
-    // of the box surface go to the mailbox xm
-    auto pass = [&](int col, double* xm) {
+    // of the box surface go to the mailbox xm.  KIND 0: every cell; 1: the red
+    // cells that are not deep(); 2: the deep red cells, into sv / sacc only.
+    // REG: the register form (full boxes)
+    auto pass = [&](int col, double* xm, auto kind_c) {
+        constexpr int KIND = decltype(kind_c)::value;
         const int e0 = ((i0 + j + oz) & 1) == col ? 0 : 1;
 #pragma unroll
-        for (int z0 = 0; z0 < kRbz; z0 += kRg) {
-            double c[kRg], am[kRg], ap[kRg], bm[kRg], bp[kRg], cm[kRg], cp[kRg];
+        for (int z0 = 0; z0 < PZ; z0 += G) {
+            double c[G], am[G], ap[G], bm[G], bp[G], cm[G], cp[G];
 #pragma unroll
-            for (int u = 0; u < kRg; ++u) {
-                const int z = z0 + u, e = e0 ^ (z & 1);
+            for (int u = 0; u < G; ++u) {
+                const int z = zb + z0 + u, e = e0 ^ (u & 1);  // zb, z0 even
                 const int o = ((z + 2) * (kRby + 4) + (y + 2)) * kTsx + 2 * px + e + 2;
-                c[u] = L[o];
-                am[u] = L[o - 1];
-                ap[u] = L[o + 1];
-                bm[u] = L[o - kTsx];
-                bp[u] = L[o + kTsx];
-                cm[u] = L[o - kTsy];
-                cp[u] = L[o + kTsy];
+                if (REG) {
+                    const int w = z0 + u;
+                    const double far = L[e ? o + 1 : o - 1];
+                    const double mine = e ? own[w][1] : own[w][0];
+                    const double part = e ? own[w][0] : own[w][1];
+                    c[u] = mine;
+                    am[u] = e ? part : far;
+                    ap[u] = e ? far : part;
+                    bm[u] = L[o - kTsx];
+                    bp[u] = L[o + kTsx];
+                    cm[u] = w > 0 ? (e ? own[w - 1][1] : own[w - 1][0]) : L[o - kTsy];
+                    cp[u] = w < PZ - 1 ? (e ? own[w + 1][1] : own[w + 1][0]) : L[o + kTsy];
+                } else {
+                    c[u] = L[o];
+                    am[u] = L[o - 1];
+                    ap[u] = L[o + 1];
+                    bm[u] = L[o - kTsx];
+                    bp[u] = L[o + kTsx];
+                    cm[u] = L[o - kTsy];
+                    cp[u] = L[o + kTsy];
+                }
             }
 #pragma unroll
-            for (int u = 0; u < kRg; ++u) {
-                const int z = z0 + u, k = oz + z, e = e0 ^ (z & 1), i = i0 + e;
+            for (int u = 0; u < G; ++u) {
+                const int z = zb + z0 + u, k = oz + z, e = e0 ^ (u & 1), i = i0 + e;
                 if (i > I || j > J || k > K) continue;
                 const int x = 2 * px + e;
+                if (KIND == 1 && deep(x, z)) continue;
+                if (KIND == 2) {
+                    if (!deep(x, z)) continue;
+                    const double cc = c[u];
+                    const double tx = (ap[u] - 2.0 * cc) + am[u];
+                    const double ty = (bp[u] - 2.0 * cc) + bm[u];
+                    const double tz = (cp[u] - 2.0 * cc) + cm[u];
+                    const double r = (e ? rh[z0 + u][1] : rh[z0 + u][0]) -
+                                     ((tx * idx2 + ty * idy2) + tz * idz2);
+                    sv[z0 + u] = cc - (factor * r);
+                    sacc += (r * r);
+                    smask |= 1u << (z0 + u);
+                    continue;
+                }
                 const int o = ((z + 2) * (kRby + 4) + (y + 2)) * kTsx + x + 2;
-                const double r = upd(o, i, j, k, e ? rh[z][1] : rh[z][0], c[u], am[u], ap[u],
+                const double r = upd(o, i, j, k, e ? rh[z0 + u][1] : rh[z0 + u][0], c[u], am[u], ap[u],
                                      bm[u], bp[u], cm[u], cp[u]);
                 acc += (r * r);
-                if (col == 0 && (x < 2 || x >= kRbx - 2 || y < 2 || y >= kRby - 2 || z < 2 ||
+                const double nv = c[u] - (factor * r);  // the value upd() stored
+                if (REG) {
+                    if (e) own[z0 + u][1] = nv;
+                    else   own[z0 + u][0] = nv;
+                }
+                if (col == 0 && !(mode & 2) && (x < 2 || x >= kRbx - 2 || y < 2 || y >= kRby - 2 || z < 2 ||
                                  z >= kRbz - 2))
-                    xstore(xm + gof(i, j, k), L[o]);
+                    xstore(xm + gof(i, j, k), nv);
             }
         }
     };
+    // the deep red cells computed ahead (pass KIND 2) into the box, ghost faces
+    // included (a deep cell can be the last of a ragged domain)
+    auto commit = [&]() {
+        const int e0 = ((i0 + j + oz) & 1) == 1 ? 0 : 1;
+#pragma unroll
+        for (int u = 0; u < PZ; ++u) {
+            if (!(smask >> u & 1u)) continue;
+            const int z = zb + u, k = oz + z, e = e0 ^ (u & 1), i = i0 + e;
+            const int o = ((z + 2) * (kRby + 4) + (y + 2)) * kTsx + 2 * px + e + 2;
+            const double v = sv[u];
+            L[o] = v;
+            if (REG) {
+                if (e) own[u][1] = v;
+                else   own[u][0] = v;
+            }
+            if (i == I) L[o + 1] = v;
+            if (j == J) L[o + kTsx] = v;
+            if (k == K) L[o + kTsy] = v;
+        }
+        acc += sacc;
+        sacc = 0.0;
+        smask = 0;
+    };
     auto ring_red = [&]() {
-        constexpr int RQ = (kTring / 2 + 64 + kRthreads - 1) / kRthreads;
+        constexpr int RQ = (kTring / 2 + 64 + NT - 1) / NT;
         double c[RQ], am[RQ], ap[RQ], bm[RQ], bp[RQ], cm[RQ], cp[RQ];
         int oo[RQ];
 #pragma unroll
         for (int m = 0; m < RQ; ++m) {
-            const int q = t + kRthreads * m;
+            const int q = t + NT * m;
             oo[m] = q < nring ? ring_o[q] : -1;
             const int o = oo[m] < 0 ? kTsy + kTsx + 1 : (oo[m] & 0xffff);
             c[m] = L[o];
@@ -619,7 +751,7 @@ __global__ __launch_bounds__(kRthreads, 1) void k3_resident1(G3 g, double* __res
             const double tx = (ap[m] - 2.0 * c[m]) + am[m];
             const double ty = (bp[m] - 2.0 * c[m]) + bm[m];
             const double tz = (cp[m] - 2.0 * c[m]) + cm[m];
-            const double r = ring_r[t + kRthreads * m] - ((tx * idx2 + ty * idy2) + tz * idz2);
+            const double r = ring_r[t + NT * m] - ((tx * idx2 + ty * idy2) + tz * idz2);
             const double v = c[m] - (factor * r);
             L[o] = v;
             ghosts(o, oo[m] >> 16, v);
@@ -627,16 +759,17 @@ __global__ __launch_bounds__(kRthreads, 1) void k3_resident1(G3 g, double* __res
     };
     // the shell's black cells from mailbox xm, with their ghost faces
     auto receive = [&](const double* xm) {
-        double v[kTrxq];
-        int2 e[kTrxq];
+        constexpr int RXQ = (kTrx + NT - 1) / NT;
+        double v[RXQ];
+        int2 e[RXQ];
 #pragma unroll
-        for (int m = 0; m < kTrxq; ++m) {
-            const int q = t + kRthreads * m;
+        for (int m = 0; m < RXQ; ++m) {
+            const int q = t + NT * m;
             e[m] = q < nrx ? rx_list[q] : make_int2(-1, 0);
             v[m] = e[m].x >= 0 ? xload(xm + e[m].y) : 0.0;
         }
 #pragma unroll
-        for (int m = 0; m < kTrxq; ++m) {
+        for (int m = 0; m < RXQ; ++m) {
             if (e[m].x < 0) continue;
             const int o = e[m].x & 0xffff;
             L[o] = v[m];
@@ -651,21 +784,52 @@ __global__ __launch_bounds__(kRthreads, 1) void k3_resident1(G3 g, double* __res
     unsigned nbar = 0;
     bool ok = true;
     __syncthreads();
+    // mode bits 2 / 4 / 512 / 1024 (timing experiments only, results wrong):
+    // no shell exchange / no grid barrier / no ring update / no partials read
+    using K0 = std::integral_constant<int, 0>;
+    using K1 = std::integral_constant<int, 1>;
+    using K2 = std::integral_constant<int, 2>;
+    // bit 11: no work ahead of the barrier (the red pass whole, after it)
+    const bool ahead = PZ <= 8 && !(mode & 2048) && (mode & 24);
+    if (REG) {
+#pragma unroll
+        for (int u = 0; u < PZ; ++u) {
+            const int o = ((zb + u + 2) * (kRby + 4) + (y + 2)) * kTsx + 2 * px + 2;
+            own[u][0] = L[o];
+            own[u][1] = L[o + 1];
+        }
+    }
+    auto red_deep = [&]() { pass(1, nullptr, K2{}); };
+    if (ahead && !done) red_deep();
     while (!done) {
         double* const xm = mbox + (it & 1) * (long long)mstride;
-        ring_red();  // the neighbours' red cells next to the box
-        pass(1, xm);
+        if (!(mode & 512)) ring_red();  // the neighbours' red cells next to the box
+        if (ahead) {
+            commit();
+            pass(1, xm, K1{});
+        } else {
+            pass(1, xm, K0{});
+        }
         __syncthreads();
-        pass(0, xm);
-        const double s = rblock_sum(acc, sh);
+        pass(0, xm, K0{});
+        const double s = rblock_sum<NW>(acc, sh);
         acc = 0.0;
         double* part = partials + (it & 1) * gridDim.x;
         if (t == 0) xstore(part + b, s);
-        if (!(ok = rgrid_sync(bar, ++nbar, &sh_flag, mode))) break;
+        if (ahead) {
+            // arrive, compute the next iteration's deep red cells (from the
+            // final black cells of this one), then wait
+            if (!(mode & 4)) rgrid_arrive(bar, ++nbar, mode);
+            red_deep();
+            if (!(mode & 4) && !(ok = rgrid_wait(bar, nbar, &sh_flag, mode))) break;
+        } else if (!(mode & 4) && !(ok = rgrid_sync(bar, ++nbar, &sh_flag, mode))) {
+            break;
+        }
         double q = 0.0;
-        for (int w = t; w < (int)gridDim.x; w += kRthreads) q += xload(part + w);
-        receive(xm);
-        const double S = rblock_sum(q, sh);
+        if (!(mode & 1024))
+            for (int w = t; w < (int)gridDim.x; w += NT) q += xload(part + w);
+        if (!(mode & 2)) receive(xm);
+        const double S = rblock_sum<NW>(q, sh);
         res = (res + S) / cells;
         ++it;
         done = !((res >= epssq) && (it < itermax));
@@ -673,7 +837,7 @@ __global__ __launch_bounds__(kRthreads, 1) void k3_resident1(G3 g, double* __res
     }
     if (!ok) return;
 #pragma unroll
-    for (int z = 0; z < kRbz; ++z) {
+    for (int z = zb; z < zb + PZ; ++z) {
         const int k = oz + z;
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
@@ -697,6 +861,45 @@ __global__ __launch_bounds__(kRthreads, 1) void k3_resident1(G3 g, double* __res
     }
 }
 
+// the resident solve's form (MISOR3_RESIDENT_MODE, bits documented at
+// rgrid_sync and the kernels) and its kernel and threads per box (bit 7:
+// 1024, bit 8: 512, else 256).  Default 240: one barrier per iteration,
+// atomics, the two-level barrier, 1024 threads per box -- 128^3: 12.7 us per
+// iteration against 16.5 at 256 threads (profiles/r04_res3d_modes.txt)
+static int resident_mode() {
+    static const int mode = [] {
+        const char* e = getenv("MISOR3_RESIDENT_MODE");
+        return e ? atoi(e) : 240;
+    }();
+    return mode;
+}
+
+// full: every box lies wholly inside the domain; the register form (an
+// experiment, mode bit 12: slower at 1024 threads, 17.5 against 13.8 us at
+// 128^3 -- it spills at 128 VGPRs -- profiles/r04_res3d_modes.txt)
+static void resident_kernel(int md, bool full, const void** fn, int* nt) {
+    const bool reg = full && (md & 4096);
+    if (!(md & 64)) {
+        *fn = reinterpret_cast<const void*>(k3_resident);
+        *nt = kRthreads;
+    } else if (md & 128) {
+        *fn = reg ? reinterpret_cast<const void*>(k3_resident1<1024, true>)
+                  : reinterpret_cast<const void*>(k3_resident1<1024>);
+        *nt = 1024;
+    } else if (md & 256) {
+        *fn = reg ? reinterpret_cast<const void*>(k3_resident1<512, true>)
+                  : reinterpret_cast<const void*>(k3_resident1<512>);
+        *nt = 512;
+    } else {
+        *fn = reinterpret_cast<const void*>(k3_resident1<256>);
+        *nt = 256;
+    }
+}
+
+static bool resident_full(const G3& g) {
+    return g.I % kRbx == 0 && g.J % kRby == 0 && g.K % kRbz == 0;
+}
+
 // boxes of the resident solve for this grid, or 0 if it cannot run here
 int resident3_boxes(const G3& g) {
     if (g.koff != 0 || !g.lo_phys || !g.hi_phys) return 0;  // single domain only
@@ -704,16 +907,18 @@ int resident3_boxes(const G3& g) {
     const int nbx = (g.I + kRbx - 1) / kRbx, nby = (g.J + kRby - 1) / kRby,
               nbz = (g.K + kRbz - 1) / kRbz;
     const long long nb = (long long)nbx * nby * nbz;
-    // residency of BOTH resident kernels (the default mode launches
-    // k3_resident1, ~154 KB of LDS; k3_resident ~88 KB): the smaller answer, so
-    // the count reported here is one the launched kernel is admitted with
-    int dev = 0, cus = 0, per0 = 0, per1 = 0;
+    // residency of the kernel launch3_resident launches with the mailboxes
+    // (k3_resident1, ~154 KB of LDS) and of its fallback without them
+    // (k3_resident, ~88 KB): the smaller answer, so the count reported here is
+    // one the launched kernel is admitted with
+    const void* fn = nullptr;
+    int nt = 0, dev = 0, cus = 0, per0 = 0, per1 = 0;
+    resident_kernel(resident_mode(), resident_full(g), &fn, &nt);
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per0, reinterpret_cast<const void*>(k3_resident),
                                                      kRthreads, 0) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &per1, reinterpret_cast<const void*>(k3_resident1), kRthreads, 0) != hipSuccess)
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per1, fn, nt, 0) != hipSuccess)
         return 0;
     const int per = per0 < per1 ? per0 : per1;
     return nb <= (long long)cus * per && nb <= 256 ? (int)nb : 0;  // 256: partials slots
@@ -733,20 +938,17 @@ int launch3_resident(hipStream_t s, const G3& g, double* p, const double* rhs, d
     if (hipMemsetAsync(bar, 0, sizeof(Bar3), s) != hipSuccess) return -1;
     G3 ga = g;
     Bar3* b = static_cast<Bar3*>(bar);
-    static int mode = [] {
-        const char* e = getenv("MISOR3_RESIDENT_MODE");
-        return e ? atoi(e) : 112;  // one barrier per iteration, atomics, two-level barrier
-    }();
-    int md = mbox ? mode : (mode & ~8);
+    int md = mbox ? resident_mode() : (resident_mode() & ~(8 | 64));
+    const void* fn = nullptr;
+    int nt = 0;
+    resident_kernel(md, resident_full(g), &fn, &nt);
     void* args[] = {&ga, &p, const_cast<double**>(&rhs), &idx2, &idy2, &idz2, &factor, &cells,
                     &partials, &st, &b, &nbx, &nby, &md, &mbox};
     int mstride = (int)((g.K + 4) * g.sxy);  // the host's mailboxes: two buffers of p's size
     void* args1[] = {&ga, &p, const_cast<double**>(&rhs), &idx2, &idy2, &idz2, &factor, &cells,
                      &partials, &st, &b, &nbx, &nby, &md, &mbox, &mstride};
-    const bool one = (md & 64) && mbox;
-    const hipError_t e = hipLaunchCooperativeKernel(
-        one ? reinterpret_cast<const void*>(k3_resident1) : reinterpret_cast<const void*>(k3_resident),
-        dim3(nb), dim3(kRthreads), one ? args1 : args, 0, s);
+    const hipError_t e =
+        hipLaunchCooperativeKernel(fn, dim3(nb), dim3(nt), (md & 64) ? args1 : args, 0, s);
     if (e == hipSuccess) return 0;
     (void)hipGetLastError();  // clear the refusal
     return 1;

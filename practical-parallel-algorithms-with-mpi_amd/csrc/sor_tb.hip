@@ -21,7 +21,9 @@ int tb_xch(int variant) { return kTbVariants[variant].xch; }
 int tb_ring_slots(int T, int variant) {
     if (tb_xch(variant)) return std::max(2, 2 * T - 2);  // sor_tbx.h xslots
     const int D = kTbVariants[variant].ahead;
-    return 2 * T + D + (D & 1);
+    if (kTbVariants[variant].hr) return hr_slots(T, D, kTbVariants[variant].skew && T >= 2 ? 1 : 0);
+    const int sk = kTbVariants[variant].skew && T >= 4 ? 1 : 0;  // sor_tb.h skew_split
+    return 2 * T + D + sk + ((D + sk) & 1);
 }
 
 int tb_nbx(int ni, int T, int variant) {

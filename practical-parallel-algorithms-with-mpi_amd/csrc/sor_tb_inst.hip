@@ -3,6 +3,7 @@
 #include <algorithm>
 
 #include "sor_tb.h"
+#include "sor_tbh.h"
 #include "sor_tbx.h"
 
 #ifndef MISOR_TB_T
@@ -23,10 +24,10 @@ static int persistent_grid(K kernel, int threads) {
     return std::max(8, per_cu * cus);
 }
 
-template <int T, int W, int D, bool B>
+template <int T, int W, int D, bool B, int SK = 0, int DL = 0>
 static int resident2() {
     static int n = 0;
-    if (n == 0) n = persistent_grid(rb_tb_kernel<T, W, D, B>, kLanes * W);
+    if (n == 0) n = persistent_grid(rb_tb_kernel<T, W, D, B, false, SK, DL>, kLanes * W);
     return n;
 }
 
@@ -34,6 +35,13 @@ template <int T, int W, int D, bool P2, int E>
 static int resident_chain() {
     static int n = 0;
     if (n == 0) n = persistent_grid(rb_tbc_kernel<T, W, D, P2, E>, kLanes * W);
+    return n;
+}
+
+template <int T, int W, int D, bool P2, int SK = 0>
+static int residenth() {
+    static int n = 0;
+    if (n == 0) n = persistent_grid(rb_tbh_kernel<T, W, D, P2, SK>, kLanes * W);
     return n;
 }
 
@@ -134,6 +142,28 @@ void MISOR_CAT(launch_tb_t, MISOR_TB_T)(hipStream_t s, const SweepParams& prm,
         break;
     case 3: TB(1, 2); break;
     case 4: TB(4, 3); break;
+    case kSkewTbVariant:
+        if (prm.pow2) go(rb_tb_kernel<kT, 4, 2, false, true, 1>, kLanes * 4, resident2<kT, 4, 2, false, 1>());
+        else go(rb_tb_kernel<kT, 4, 2, false, false, 1>, kLanes * 4, resident2<kT, 4, 2, false, 1>());
+        break;
+    case kHrTbVariant:
+        if (prm.pow2) go(rb_tbh_kernel<kT, 4, 2, true>, kLanes * 4, residenth<kT, 4, 2, true>());
+        else go(rb_tbh_kernel<kT, 4, 2, false>, kLanes * 4, residenth<kT, 4, 2, false>());
+        break;
+    case kHrTbVariant + 1: {  // skewed (tb_ring_slots: T = 1 runs unskewed)
+        constexpr int SK_ = kT >= 2 ? 1 : 0;
+        if (prm.pow2) go(rb_tbh_kernel<kT, 4, 2, true, SK_>, kLanes * 4, residenth<kT, 4, 2, true, SK_>());
+        else go(rb_tbh_kernel<kT, 4, 2, false, SK_>, kLanes * 4, residenth<kT, 4, 2, false, SK_>());
+        break;
+    }
+    case kLdsTbVariant:
+        if (prm.pow2) go(rb_tb_kernel<kT, 4, 2, false, true, 0, 8>, kLanes * 4, resident2<kT, 4, 2, false, 0, 8>());
+        else go(rb_tb_kernel<kT, 4, 2, false, false, 0, 8>, kLanes * 4, resident2<kT, 4, 2, false, 0, 8>());
+        break;
+    case kLdsTbVariant + 1:
+        if (prm.pow2) go(rb_tb_kernel<kT, 4, 2, false, true, 0, 4>, kLanes * 4, resident2<kT, 4, 2, false, 0, 4>());
+        else go(rb_tb_kernel<kT, 4, 2, false, false, 0, 4>, kLanes * 4, resident2<kT, 4, 2, false, 0, 4>());
+        break;
 #define Q4(V)                                                                               \
     case V:                                                                                 \
         if constexpr (quad_ok<V>()) {                                                       \
@@ -158,6 +188,11 @@ int MISOR_CAT(tb_resident_t, MISOR_TB_T)(int variant) {
     case 2: return resident2<kT, 2, 2, false>();
     case 3: return resident2<kT, 1, 2, false>();
     case 4: return resident2<kT, 4, 3, false>();
+    case kSkewTbVariant: return resident2<kT, 4, 2, false, 1>();
+    case kLdsTbVariant: return resident2<kT, 4, 2, false, 0, 8>();
+    case kHrTbVariant: return residenth<kT, 4, 2, false>();
+    case kHrTbVariant + 1: return residenth<kT, 4, 2, false, kT >= 2 ? 1 : 0>();
+    case kLdsTbVariant + 1: return resident2<kT, 4, 2, false, 0, 4>();
     case 6:
     case 7: return residentx_of<kT>(variant);
 #define Q4(V)                                                                             \

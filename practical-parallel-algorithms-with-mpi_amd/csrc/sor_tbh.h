@@ -1,0 +1,462 @@
+// sor_tbh.h -- the temporally blocked sweep with a split rhs ring (TB
+// variant kHrTbVariant: rb_tbh_kernel).  Device code; included by
+// sor_tb_inst.hip after sor_tb.h, whose stage() arithmetic it runs unchanged.
+//
+// Why.  A pass of the 2-column march (sor_tb.h) costs, at 32768^2, about
+// 4.7 ms of streaming (T = 1: 4.68 ms per launch) plus ~0.19 ms per stage
+// (profiles/r04_tcurve.txt): the launch is close to HBM-bound, so the
+// driver's 20-iteration solve is cheapest in as few passes as possible.  The
+// register budget caps T at 8 (passes of 7 + 7 + 6): the rhs ring alone holds
+// 2T + D rows of the strip, 4 VGPRs each (88 at T = 10), beside the stages'
+// 10 VGPRs each, and T = 9 / 10 spill inside the steady chunk (8.1 / 9.2 ms
+// per launch against 5.6 at T = 8).
+//
+// What.  Stages 0 .. K-1 read their rhs rows from a register ring of S slots
+// as before; the older rows -- those stages K .. T-1 read -- move to an LDS
+// ring of the same S slots (row j in slot j mod S, so a chunk of S steps has
+// static slots in both rings): the row stage K-1 reads last in step n (row
+// n - 2K + 1) is written to LDS in that step, two 512-byte halves (column a
+// | column b, so a stage's read of one colour's column is one conflict-free
+// ds_read_b64).  K is chosen to balance the rings: S = max(2K + D,
+// 2(T - K) + 1), even -- 12 slots at T = 10 (48 VGPRs of ring instead of 88,
+// 12 KB of LDS per wave, 96 KB per CU at two workgroups of four waves).
+//
+// Every block runs the static ring from its first step: interior blocks warm
+// up in whole chunks (WU = 4T rounded up to S steps, the stream starting WU -
+// 4T rows early; kPre chunks), then kSteady chunks; blocks at a physical side
+// or of a height the ring does not divide run kEdge / kRowEdge chunks over
+// ceil((H + 4T) / S) chunks, the steps past the block's last row reading
+// zeros (range-checked buffer loads) and storing / counting nothing (the row
+// tests).  Rows the LDS stages read before any step wrote them belong to
+// rows below the stream, outside every stage's valid cone.
+#pragma once
+
+#include "sor_tb.h"
+
+namespace misor {
+
+namespace {
+
+// SK: the skewed form (hrs_step), T >= 2
+template <int T, int D, int SK = 0>
+struct Hr {
+    static constexpr int K = hr_k(T, D, SK);      // stages 0 .. K-1: rhs from registers
+    static constexpr int S = hr_slots(T, D, SK);  // slots of both rings (misor_internal.h)
+    static constexpr int SKH = SK ? T / 2 : 0;    // leading stages of the skewed form
+    // interior warm-up steps: 4T rounded up to whole chunks -- at least 4T + 1
+    // in the skewed form, whose leading stages never see the stream's first row
+    static constexpr int WU = (4 * T + SK + S - 1) / S * S;
+    static_assert(!SK || (T >= 2 && K <= SKH), "skewed split ring");
+};
+
+template <int T, int D>
+struct HrMarch {
+    d2 A[T], M1[T], M2[T];
+    d2 Pq[D];
+    TallyAcc acc[T];
+    d2 keep[2];
+    d2 B;  // skewed form: stage SKH-1's output of the previous step
+};
+
+struct HrIo {
+    __amdgpu_buffer_rsrc_t p, r, d;  // p rows from rs0, rhs rows from rs0 - 1, dst rows from j0
+    unsigned lane;                   // lane * 16
+    unsigned st_lane;                // kSteady: lane * 16 if the lane stores, else out of range
+    unsigned row_bytes;
+    lds_double* lx;                  // the wave's LDS ring (+ lane): slot s at lx + 128 s
+    double* dp;                      // kEdge / kRowEdge stores: dst at row 0 of the lane's columns
+    long long pitch;
+};
+
+__device__ __forceinline__ void hr_stv(double* p, d2 v) { stv(p, v); }
+
+// step n of the split-ring march (stream row r0 = rs0 + n; PH = n mod S)
+template <int T, int D, int MODE, int Q, int PH, bool P2>
+__device__ __forceinline__ void hr_step(HrMarch<T, D>& m, d2* R, const Lane& c, const HrIo& io,
+                                        int r0, unsigned off_n, unsigned st_base) {
+    constexpr int K = Hr<T, D>::K, S = Hr<T, D>::S;
+    const unsigned ld = off_n + (unsigned)D * io.row_bytes;
+    const d2 nP = bload(io.p, io.lane, ld);
+    R[(PH + D) % S] = bload(io.r, io.lane, ld);
+    // the LDS stages' rhs: column a (Q = 0) or b of rows n - 2t and n - 2t - 1
+    double lr[T], lb[T];
+#pragma unroll
+    for (int t = K; t < T; ++t) {
+        lr[t] = io.lx[((PH - 2 * t + 4 * S) % S) * 128 + Q * 64];
+        lb[t] = io.lx[((PH - 2 * t - 1 + 4 * S) % S) * 128 + Q * 64];
+    }
+    d2 v = m.Pq[0];
+    d2 prevM2 = d2{0.0, 0.0};
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        d2 Ra, Rb;
+        if (t < K) {
+            Ra = R[(PH - 2 * t + 4 * S) % S];
+            Rb = R[(PH - 2 * t - 1 + 4 * S) % S];
+        } else {
+            Ra = Q == 0 ? d2{lr[t], 0.0} : d2{0.0, lr[t]};
+            Rb = Q == 0 ? d2{lb[t], 0.0} : d2{0.0, lb[t]};
+        }
+        if (t == T - 1) prevM2 = m.M2[t];
+        v = stage<T, Q, MODE, false, P2>(c, t, t > 0, v, r0 - 2 * t, m.A[t], m.M1[t], m.M2[t], Ra,
+                                         Rb, m.acc[t]);
+    }
+    // row n - 2K + 1 leaves the register ring for the LDS one (read next step
+    // by stage K); its slot is not one this step's LDS stages read
+    {
+        constexpr int s = (PH - 2 * K + 1 + 4 * S) % S;
+        const d2 w = R[s];
+        io.lx[s * 128] = w.x;
+        io.lx[s * 128 + 64] = w.y;
+    }
+    if (MODE == kSteady) {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), io.d, io.st_lane,
+                                               off_n - st_base, 2);
+    } else if (MODE == kEdge || MODE == kRowEdge) {
+        const int jw = r0 - 2 * T;  // row finished by the last stage (tb_step)
+        if (jw >= c.j0 && jw < c.j1) {
+            double* drow = io.dp + (long long)jw * io.pitch;
+            if (MODE == kRowEdge) {
+                if (c.st_a) {
+                    hr_stv(drow, v);
+                    if (c.gb && jw == 1) hr_stv(drow - io.pitch, v);
+                    if (c.gt && jw == c.nj) hr_stv(drow + io.pitch, v);
+                }
+            } else {
+                auto put = [&](double* p, d2 o) {
+                    if (c.st_a && c.st_b) {
+                        hr_stv(p, o);
+                    } else if (c.st_a) {
+                        p[0] = o.x;
+                    } else if (c.st_b) {
+                        p[1] = o.y;
+                    }
+                };
+                put(drow, v);
+                if (c.gb && jw == 1) put(drow - io.pitch, d2{c.up_a ? v.x : prevM2.x, c.up_b ? v.y : prevM2.y});
+                if (c.gt && jw == c.nj) {
+                    const d2 gn = m.M1[T - 1];
+                    put(drow + io.pitch, d2{c.up_a ? v.x : gn.x, c.up_b ? v.y : gn.y});
+                }
+            }
+        }
+    }
+    // the stored row's registers stay live through the next two steps' loads
+    // (sor_tb.h steady_step)
+    asm volatile("" ::"v"(m.keep[0]));
+    m.keep[0] = m.keep[1];
+    m.keep[1] = v;
+#pragma unroll
+    for (int k = 0; k + 1 < D; ++k) m.Pq[k] = m.Pq[k + 1];
+    m.Pq[D - 1] = nP;
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// Step n of the skewed split-ring march (sor_tb.h skew_step's two chains on
+// the split ring): the trailing stages SKH .. T-1 run stream row r0 = rs0 + n
+// on m.B, the leading stages 0 .. SKH-1 row r0 + 1 on the streamed row; their
+// residual windows sit one row higher (stage<..., SKH>).  Register ring: rows
+// n - 2K + 2 .. n + 1 + D; the row the leading register stages read last (n -
+// 2K + 2) moves to the LDS ring, which holds rows down to n - 2T + 1.
+template <int T, int D, int MODE, int Q, int PH, bool P2>
+__device__ __forceinline__ void hrs_step(HrMarch<T, D>& m, d2* R, const Lane& c, const HrIo& io,
+                                         int r0, unsigned off_n, unsigned st_base) {
+    using G = Hr<T, D, 1>;
+    constexpr int K = G::K, S = G::S, SKH = G::SKH;
+    const unsigned ld = off_n + (unsigned)(D + 1) * io.row_bytes;
+    const d2 nP = bload(io.p, io.lane, ld);
+    R[(PH + 1 + D) % S] = bload(io.r, io.lane, ld);
+    // LDS stages' rhs: trailing t >= SKH rows n - 2t, n - 2t - 1 (colour Q),
+    // leading K <= t < SKH rows n + 1 - 2t, n - 2t (colour 1 - Q)
+    double lr[T], lb[T];
+#pragma unroll
+    for (int t = K; t < T; ++t) {
+        const int j = t < SKH ? PH + 1 - 2 * t : PH - 2 * t;
+        const int h = t < SKH ? 1 - Q : Q;
+        lr[t] = io.lx[((j + 4 * S) % S) * 128 + h * 64];
+        lb[t] = io.lx[((j - 1 + 4 * S) % S) * 128 + h * 64];
+    }
+    auto rr = [&](int t, bool red) -> d2 {  // stage t's rhs row (red: rows rin - 1)
+        const int q = t < SKH ? 1 - Q : Q;
+        if (t < K) {
+            const int j = (t < SKH ? PH + 1 - 2 * t : PH - 2 * t) - (red ? 0 : 1);
+            return R[(j + 4 * S) % S];
+        }
+        const double x = red ? lr[t] : lb[t];
+        return q == 0 ? d2{x, 0.0} : d2{0.0, x};
+    };
+    d2 v = m.Pq[0];
+    d2 u = m.B;
+    d2 prevM2 = m.M2[T - 1];
+    if constexpr (MODE == kSteady) {
+#pragma unroll
+        for (int k = 0; k < SKH; ++k) {
+            const int ta = SKH + k, tb = k;
+            stage_pair<Q, 1 - Q, P2>(c, u, m.A[ta], m.M1[ta], m.M2[ta], rr(ta, true), rr(ta, false),
+                                     m.acc[ta], v, m.A[tb], m.M1[tb], m.M2[tb], rr(tb, true),
+                                     rr(tb, false), m.acc[tb]);
+        }
+        if (T - SKH > SKH)
+            u = stage<T, Q, kSteady, false, P2, SKH>(c, T - 1, true, u, r0 - 2 * (T - 1),
+                                                     m.A[T - 1], m.M1[T - 1], m.M2[T - 1],
+                                                     rr(T - 1, true), rr(T - 1, false),
+                                                     m.acc[T - 1]);
+    } else {
+#pragma unroll
+        for (int t = SKH; t < T; ++t) {
+            if (t == T - 1) prevM2 = m.M2[t];
+            u = stage<T, Q, MODE, false, P2, SKH>(c, t, true, u, r0 - 2 * t, m.A[t], m.M1[t],
+                                                  m.M2[t], rr(t, true), rr(t, false), m.acc[t]);
+        }
+#pragma unroll
+        for (int t = 0; t < SKH; ++t)
+            v = stage<T, 1 - Q, MODE, false, P2, SKH>(c, t, t > 0, v, r0 + 1 - 2 * t, m.A[t],
+                                                      m.M1[t], m.M2[t], rr(t, true),
+                                                      rr(t, false), m.acc[t]);
+    }
+    m.B = v;
+    {
+        constexpr int s = (PH - 2 * K + 2 + 4 * S) % S;
+        const d2 w = R[s];
+        io.lx[s * 128] = w.x;
+        io.lx[s * 128 + 64] = w.y;
+    }
+    if (MODE == kSteady) {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, u), io.d, io.st_lane,
+                                               off_n - st_base, 2);
+    } else if (MODE == kEdge || MODE == kRowEdge) {
+        const int jw = r0 - 2 * T;
+        if (jw >= c.j0 && jw < c.j1) {
+            double* drow = io.dp + (long long)jw * io.pitch;
+            if (MODE == kRowEdge) {
+                if (c.st_a) {
+                    hr_stv(drow, u);
+                    if (c.gb && jw == 1) hr_stv(drow - io.pitch, u);
+                    if (c.gt && jw == c.nj) hr_stv(drow + io.pitch, u);
+                }
+            } else {
+                auto put = [&](double* p, d2 o) {
+                    if (c.st_a && c.st_b) {
+                        hr_stv(p, o);
+                    } else if (c.st_a) {
+                        p[0] = o.x;
+                    } else if (c.st_b) {
+                        p[1] = o.y;
+                    }
+                };
+                put(drow, u);
+                if (c.gb && jw == 1)
+                    put(drow - io.pitch, d2{c.up_a ? u.x : prevM2.x, c.up_b ? u.y : prevM2.y});
+                if (c.gt && jw == c.nj) {
+                    const d2 gn = m.M1[T - 1];
+                    put(drow + io.pitch, d2{c.up_a ? u.x : gn.x, c.up_b ? u.y : gn.y});
+                }
+            }
+        }
+    }
+    asm volatile("" ::"v"(m.keep[0]));
+    m.keep[0] = m.keep[1];
+    m.keep[1] = u;
+#pragma unroll
+    for (int k = 0; k + 1 < D; ++k) m.Pq[k] = m.Pq[k + 1];
+    m.Pq[D - 1] = nP;
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int T, int D, int SK, int MODE, int Q0, bool P2, int... NN>
+__device__ __forceinline__ void hr_chunk(HrMarch<T, D>& m, d2* R, const Lane& c, const HrIo& io,
+                                         int r0, unsigned off_n, unsigned st_base,
+                                         std::integer_sequence<int, NN...>) {
+    if constexpr (SK)
+        (hrs_step<T, D, MODE, Q0 ^ (NN & 1), NN, P2>(m, R, c, io, r0 + NN,
+                                                     off_n + (unsigned)NN * io.row_bytes, st_base),
+         ...);
+    else
+        (hr_step<T, D, MODE, Q0 ^ (NN & 1), NN, P2>(m, R, c, io, r0 + NN,
+                                                    off_n + (unsigned)NN * io.row_bytes, st_base),
+         ...);
+}
+
+// chunks [k0, k1) of a march of colour Q0 (colour of step 0)
+template <int T, int D, int SK, int MODE, int Q0, bool P2>
+__device__ __forceinline__ void hr_run(HrMarch<T, D>& m, d2* R, const Lane& c, const HrIo& io,
+                                       int rs0, int k0, int k1, unsigned st_base) {
+    constexpr int S = Hr<T, D, SK>::S;
+    for (int k = k0; k < k1; ++k)
+        hr_chunk<T, D, SK, MODE, Q0, P2>(m, R, c, io, rs0 + k * S,
+                                         (unsigned)(k * S) * io.row_bytes, st_base,
+                                         std::make_integer_sequence<int, S>{});
+}
+
+// one wave's strip (tb_strip2's geometry and lane setup) through the
+// split-ring march; lx: the wave's LDS ring
+template <int T, int D, bool P2, int SK = 0>
+__device__ __forceinline__ void hr_strip(const SweepParams& prm, const double* __restrict__ src,
+                                         double* __restrict__ dst, const double* __restrict__ rhs,
+                                         const int c_out, const int j0, const int j1, const int by,
+                                         const int lane, double (&acc)[T], lds_double* lx) {
+    constexpr int OW = kStripCells - 4 * T;
+    constexpr int S = Hr<T, D, SK>::S, WU = Hr<T, D, SK>::WU;
+    const int ni = prm.ni, nj = prm.nj;
+    const int c_ld = c_out - 2 * T;
+    const long long pitch = prm.pitch;
+    const int own_end = ni;
+
+    Lane c;
+    c.ia = c_ld + 2 * lane;
+    c.ib = c.ia + 1;
+    c.up_a = c.ia >= prm.upd_lo_i && c.ia <= prm.upd_hi_i;
+    c.up_b = c.ib >= prm.upd_lo_i && c.ib <= prm.upd_hi_i;
+    const bool own_lane = lane >= T && lane < kLanes - T;
+    c.own_a = own_lane && c.ia <= own_end;
+    c.own_b = own_lane && c.ib <= own_end;
+    c.fix0_b = prm.ghost_left && c.ib == 0;
+    c.fixr_a = prm.ghost_right && c.ia == ni + 1;
+    c.fixr_b = prm.ghost_right && c.ib == ni + 1;
+    c.st_a = c.own_a || c.fixr_a;
+    c.st_b = c.own_b || c.fix0_b || c.fixr_b;
+    c.lo_j = prm.upd_lo_j;
+    c.hi_j = prm.upd_hi_j;
+    c.j0 = j0;
+    c.j1 = j1;
+    c.wlo = by == 0 && prm.ghost_bottom;
+    c.whi = by == prm.nby - 1 && prm.ghost_top;
+    c.parity = prm.parity;
+    c.gb = prm.ghost_bottom;
+    c.gt = prm.ghost_top;
+    c.nj = nj;
+    c.idx2 = prm.idx2;
+    c.idy2 = prm.idy2;
+    c.coef = prm.coef;
+    c.bl = ((lane + 63) & 63) * 4;
+    c.br = ((lane + 1) & 63) * 4;
+
+    const int rs = j0 - 2 * T;  // first row of the cone
+    const int rend = j1 - 1 + 2 * T;
+    const bool cols_in = c_ld >= prm.upd_lo_i && c_ld + kStripCells - 1 <= prm.upd_hi_i &&
+                         (c_out + OW - 1 <= ni || (ni & 1) == 0);
+    const bool rows_in = rs >= prm.upd_lo_j && rend <= prm.upd_hi_j && (j1 - j0) % S == 0 &&
+                         j1 - j0 > 0;
+    const bool steady = cols_in && rows_in;
+    // interior: the stream starts WU - 4T rows early (whole warm-up chunks);
+    // skewed: the leading stages run one row ahead (they take rows rs0 + 1 ..
+    // rend + 1), so a side block starts one row early (its leading stages
+    // then see row rs first)
+    const int rs0 = steady ? rs - (WU - 4 * T) : rs - SK;
+    const int nsteps = rend - rs0 + 1;
+    const int nchunks = (nsteps + S - 1) / S;
+
+    auto rsrc = [&](const double* b, int row0, int rows) {
+        const unsigned long long a =
+            (unsigned long long)(b + (long long)(kYOff + row0) * pitch + kXOff + c_ld);
+        const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+        const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+        return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo),
+                                                 (short)0, (int)((long long)rows * pitch * 8),
+                                                 0x00020000);
+    };
+    HrIo io;
+    io.p = rsrc(src, rs0, nsteps + D + SK);
+    io.r = rsrc(rhs, rs0 - 1, nsteps + D + SK);
+    io.d = rsrc(dst, j0, j1 - j0);
+    io.lane = (unsigned)lane * 16u;
+    io.st_lane = c.own_a ? (unsigned)lane * 16u : 0x40000000u;
+    io.row_bytes = (unsigned)(pitch * 8);
+    io.lx = lx + lane;
+    io.dp = dst + (long long)kYOff * pitch + kXOff + c.ia;
+    io.pitch = pitch;
+
+    HrMarch<T, D> m;
+    d2 R[S];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        m.acc[t] = 0.0;
+        m.A[t] = m.M1[t] = m.M2[t] = d2{0.0, 0.0};
+    }
+    m.keep[0] = m.keep[1] = d2{0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < S; ++k) R[k] = d2{0.0, 0.0};
+    m.B = d2{0.0, 0.0};
+    // p rows SK .. SK + D - 1 (the leading stages' first), rhs rows 0 .. SK + D - 1
+#pragma unroll
+    for (int k = 0; k < D; ++k) m.Pq[k] = bload(io.p, io.lane, (unsigned)(k + SK) * io.row_bytes);
+#pragma unroll
+    for (int k = 0; k < D + SK; ++k) R[k] = bload(io.r, io.lane, (unsigned)k * io.row_bytes);
+    const bool q1 = ((c.parity + rs0) & 1) != 0;  // colour of step 0 (S even: of every chunk)
+    if (steady) {
+        // stores: step n finishes row rs0 + n - 2T = j0 + n - WU
+        const unsigned sb = (unsigned)WU * io.row_bytes;
+        constexpr int KW = WU / S;
+        if (q1) {
+            hr_run<T, D, SK, kPre, 1, P2>(m, R, c, io, rs0, 0, KW, sb);
+            hr_run<T, D, SK, kSteady, 1, P2>(m, R, c, io, rs0, KW, nchunks, sb);
+        } else {
+            hr_run<T, D, SK, kPre, 0, P2>(m, R, c, io, rs0, 0, KW, sb);
+            hr_run<T, D, SK, kSteady, 0, P2>(m, R, c, io, rs0, KW, nchunks, sb);
+        }
+    } else if (cols_in) {
+        if (q1) hr_run<T, D, SK, kRowEdge, 1, P2>(m, R, c, io, rs0, 0, nchunks, 0);
+        else    hr_run<T, D, SK, kRowEdge, 0, P2>(m, R, c, io, rs0, 0, nchunks, 0);
+    } else {
+        if (q1) hr_run<T, D, SK, kEdge, 1, P2>(m, R, c, io, rs0, 0, nchunks, 0);
+        else    hr_run<T, D, SK, kEdge, 0, P2>(m, R, c, io, rs0, 0, nchunks, 0);
+    }
+    if (cols_in && !c.own_a) {
+#pragma unroll
+        for (int t = 0; t < T; ++t) m.acc[t] = 0.0;
+    }
+#pragma unroll
+    for (int t = 0; t < T; ++t) acc[t] += m.acc[t];
+}
+
+// one block (bx, by) of a split-ring pass: logical block L (tb_block)
+template <int T, int WAVES, int D, bool P2, int SK>
+__device__ __forceinline__ void hr_block(const SweepParams& prm, const double* __restrict__ src,
+                                         double* __restrict__ dst, const double* __restrict__ rhs,
+                                         double* __restrict__ partials, const int L,
+                                         double (*wsum)[WAVES], lds_double* lx) {
+    constexpr int OW = kStripCells - 4 * T;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int bx = L % prm.nbx, by = L / prm.nbx;
+    int j0, j1;
+    block_rows(prm, by, j0, j1);
+    if (prm.part != 0) {  // overlapped decomposed pass (tb_block)
+        const int lo = 1 + bx * WAVES * OW - 2 * T;
+        const int hi = 1 + (bx * WAVES + WAVES - 1) * OW - 2 * T + kStripCells - 1;
+        const bool interior = lo >= prm.int_lo_i && hi <= prm.int_hi_i &&
+                              j0 - 2 * T >= prm.int_lo_j && j1 - 1 + 2 * T <= prm.int_hi_j;
+        if (interior != (prm.part == 1)) return;
+    }
+    const int c_out = 1 + (bx * WAVES + wave) * OW;
+    if (L == 0) copy_corners(prm, src, dst);
+    double acc[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) acc[t] = 0.0;
+    if (c_out <= prm.ni)
+        hr_strip<T, D, P2, SK>(prm, src, dst, rhs, c_out, j0, j1, by, lane, acc, lx);
+    block_partials<T, WAVES>(prm, acc, partials, L, wsum);
+}
+
+}  // namespace
+
+// the split-ring pass: persistent per-XCD queues and block partials as
+// rb_tb_kernel; an LDS ring of S rows per wave.  SK: the skewed form (T >= 2)
+template <int T, int WAVES, int D, bool P2, int SK = 0>
+__global__ __launch_bounds__(kLanes* WAVES, 2) void rb_tbh_kernel(
+    SweepParams prm, const double* __restrict__ src, double* __restrict__ dst,
+    const double* __restrict__ rhs, double* __restrict__ partials,
+    const DevState* __restrict__ st, int force, int* __restrict__ queue) {
+    __shared__ double wsum[T][WAVES];
+    __shared__ int ticket;
+    constexpr int S = Hr<T, D, SK>::S;
+    __shared__ __attribute__((aligned(16))) double ring[WAVES * S * kStripCells];
+    if (!force && st->done) return;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    lds_double* lx = (lds_double*)(ring + wave * S * kStripCells);
+    for_each_block(prm, queue, &ticket, [&](int L) __attribute__((always_inline)) {
+        hr_block<T, WAVES, D, P2, SK>(prm, src, dst, rhs, partials, L, wsum, lx);
+    });
+}
+
+}  // namespace misor

@@ -172,7 +172,7 @@ def test_solve_fixed_iterations_bitwise(golden, dims, itermax, tune):
 
 @pytest.mark.parametrize("tune", SOLVE_TUNES)
 @pytest.mark.parametrize("dims,eps", [((24, 20, 16), 1e-3), ((40, 12, 10), 1e-4),
-                                      ((33, 33, 33), 1e-4)])
+                                      ((33, 33, 33), 1e-4), ((64, 32, 32), 1e-4)])
 def test_solve_converges_like_oracle(golden, dims, eps, tune):
     """convergence-driven stop: same iteration count and bit-identical p"""
     prm = params(golden, "a6_dcavity.par", imax=dims[0], jmax=dims[1], kmax=dims[2],

@@ -1,0 +1,219 @@
+"""Variants of the temporally blocked sweep against the restatement of solveRB
+(assignment-4/src/solver.c:179-238): p bit for bit, identical iteration
+counts, res to 1e-12.
+
+  9   skewed march (sor_tb.h skew_step): the leading half of the stages runs
+      one step ahead of the trailing half, so a step holds two independent
+      dependency chains; the leading stages' residual windows sit one row up
+      and every block streams one more row
+  10  the steady march's rows through an LDS queue 8 rows deep (sor_tb.h
+      steady_step DL: LDS DMA ahead of the registers)
+  11  the same, 4 rows deep
+  12  split rhs ring (sor_tbh.h): the rows the later stages read move from
+      registers to an LDS ring, so T = 9 .. 12 fit the registers; every
+      block runs static-phase chunks (interior: whole warm-up chunks from a few
+      rows early; sides and ragged blocks: row-tested chunks past the block's
+      end)
+  13  the split ring with the skew of 9 (sor_tbh.h hrs_step; T = 1 as 12)
+
+The geometry runs interior blocks (static-ring chunks), the general march
+(physical sides, ragged last block rows), convergence inside a pass, the
+power-of-two form and decomposed ranks (interior and halo parts of a
+pipelined pass).
+"""
+import threading
+
+import numpy as np
+import pytest
+
+import orc
+import pymisor as M
+
+pytestmark = pytest.mark.gpu
+
+SKEW, LDS8, LDS4, HR, HRS = 9, 10, 11, 12, 13
+VARIANTS = [SKEW, LDS8, LDS4, HR, HRS]
+
+
+def hr_slots(T, D=2, sk=0, most=18):
+    """misor_internal.h hr_slots: the fewest register stages K whose ring fits"""
+    for k in range(T + 1):
+        s = max(2 * k + D + sk, 2 * (T - k) + 1 + sk)
+        s += s & 1
+        if s <= most:
+            return s
+    return T
+
+
+def ring(T, variant):
+    """sor_tb.h ring_slots<T, 2, skew> / sor_tbh.h Hr<T, 2, sk>::S"""
+    if variant in (HR, HRS):
+        return hr_slots(T, sk=1 if variant == HRS and T >= 2 else 0)
+    sk = 1 if T >= 4 and variant == SKEW else 0
+    return 2 * T + 2 + sk + ((2 + sk) & 1)
+
+
+def solve(p, rhs, dx, dy, k, T, variant, rows=0, omega=1.7, eps=1e-300, itermax=None):
+    nj, ni = p.shape[0] - 2, p.shape[1] - 2
+    with M.Grid(ni, nj, dx, dy, omega, eps, itermax or k) as g:
+        g.set_tuning(M.TUNE_SMALL_SOLVE, 0)
+        g.set_tuning(M.TUNE_TB_VARIANT, variant)
+        g.set_tuning(M.TUNE_TSTEPS, T)
+        if rows:
+            g.set_tuning(M.TUNE_TB_ROWS, rows)
+        g.upload(M.P, p)
+        g.upload(M.RHS, rhs)
+        it, res = g.solve_rb() if itermax else g.solve_rb(itermax=k)
+        assert g.get_tuning(M.TUNE_TB_VARIANT) == variant
+        st = g.stats()
+        return it, res, g.download(M.P), st
+
+
+def fields(ni, nj, seed):
+    rng = np.random.default_rng(seed)
+    p = rng.standard_normal((nj + 2, ni + 2))
+    rhs = rng.standard_normal((nj + 2, ni + 2)) * 10
+    return p, rhs
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("T", range(1, 13))
+@pytest.mark.parametrize("ni,nj", [(1201, 700), (2000, 1033), (1826, 600), (300, 190)])
+def test_variant_random_vs_oracle(ni, nj, T, variant):
+    p, rhs = fields(ni, nj, ni + 7 * nj + T)
+    dx, dy = 1.1 / ni, 0.9 / nj
+    for k in (T, 2 * T + 1):
+        want = p.copy()
+        it_ref, res_ref = orc.solve_rb(want, rhs, dx, dy, 1.7, 1e-300, k)
+        # block rows of 3 ring lengths: interior blocks and several block rows
+        it, res, got, st = solve(p, rhs, dx, dy, k, T, variant, rows=3 * ring(T, variant))
+        assert st["iters_per_pass"] == T
+        assert it == it_ref == k
+        assert np.array_equal(got, want), (k, np.argwhere(got != want)[:5])
+        assert abs(res - res_ref) <= 1e-12 * res_ref
+
+
+@pytest.fixture(scope="module")
+def mid_pass_case():
+    """a field whose solveRB residual sequence has strict drops: eps is put
+    between the residual of iteration k* and the smallest one before it, so
+    solveRB stops at k*"""
+    ni, nj = 1000, 150
+    rng = np.random.default_rng(5)
+    # scaled so every residual is < 1 (solveRB's loop starts from res = 1.0)
+    p0 = rng.standard_normal((nj + 2, ni + 2)) * 2.0 ** -30
+    rhs = np.zeros_like(p0)
+    res = {}
+    for k in range(1, 80):
+        q = p0.copy()
+        res[k] = orc.solve_rb(q, rhs, 1.0 / ni, 1.0 / nj, 1.9, 1e-300, k)[1]
+    return ni, nj, p0, rhs, res
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("T", range(2, 13))
+def test_variant_converges_mid_pass(T, variant, mid_pass_case):
+    """convergence inside a pass: the pass is recomputed with fewer
+    iterations, so the count and p equal solveRB's"""
+    ni, nj, p0, rhs, res = mid_pass_case
+    for ks in range(25, 80):
+        lo = min(res[k] for k in range(1, ks))
+        if res[ks] < lo * (1 - 1e-6) and ks % T:
+            break
+    else:
+        pytest.skip("no strictly decreasing residual step in range")
+    eps = ((res[ks] + lo) / 2) ** 0.5
+    want = p0.copy()
+    it_ref, res_ref = orc.solve_rb(want, rhs, 1.0 / ni, 1.0 / nj, 1.9, eps, 100000)
+    assert it_ref == ks
+    it, r, got, st = solve(p0, rhs, 1.0 / ni, 1.0 / nj, 0, T, variant, rows=2 * ring(T, variant),
+                           omega=1.9, eps=eps, itermax=100000)
+    assert st["iters_per_pass"] == T
+    assert it == it_ref
+    assert np.array_equal(got, want)
+    assert abs(r - res_ref) <= 1e-12 * res_ref
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("T", [2, 5, 8, 11])
+@pytest.mark.parametrize("ni,nj", [(1024, 1024), (2050, 300)])
+def test_variant_pow2_spacing(ni, nj, T, variant, monkeypatch):
+    """dx == dy == 2^-10: the power-of-two form of r (sor_tb.h resid<true>)
+    on fields of a wide dynamic range, and the general form"""
+    rng = np.random.default_rng(ni + 7 * nj + T)
+    p = rng.standard_normal((nj + 2, ni + 2)) * np.exp(rng.uniform(-20, 20, (nj + 2, ni + 2)))
+    rhs = rng.standard_normal((nj + 2, ni + 2)) * 1e6
+    h = 2.0 ** -10
+    k = 2 * T + 1
+    want = p.copy()
+    orc.solve_rb(want, rhs, h, h, 1.7, 1e-300, k)
+    for no in ("0", "1"):
+        monkeypatch.setenv("MISOR_NO_POW2", no)
+        it, _, got, _ = solve(p, rhs, h, h, k, T, variant, rows=4 * ring(T, variant))
+        assert it == k
+        assert np.array_equal(got, want), (no, np.argwhere(got != want)[:5])
+
+
+@pytest.mark.parametrize("variant,T", [(v, 8) for v in VARIANTS] +
+                         [(HR, 10), (HR, 12), (HRS, 10), (HRS, 12)])
+def test_variant_default_geometry_large(variant, T):
+    """8192^2, the automatic block height, the bench's problem 2 fields: one
+    pass and a 20-iteration solve (T = 8: passes of 7 + 7 + 6; T = 10: 10 + 10)"""
+    n = 8192
+    p, rhs = orc.poisson_init(n, n)
+    for k in (T, 20):
+        want = p.copy()
+        it_ref, res_ref = orc.solve_rb_mt(want, rhs, 1.0 / n, 1.0 / n, 1.9, 1e-300, k, 16)
+        it, res, got, st = solve(p, rhs, 1.0 / n, 1.0 / n, k, T, variant, omega=1.9)
+        assert it == k
+        assert np.array_equal(got, want)
+        assert abs(res - res_ref) <= 1e-12 * res_ref
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("T", [3, 8, 10])
+def test_variant_decomposed(world, T, variant):
+    """in-process ranks (LOCAL transport): neighbour sides are interior
+    columns / rows fed by the 2T-deep halo, pipelined interior / halo parts"""
+    ni, nj, k = 2100, 900, 2 * T + 1
+    p, rhs = fields(ni, nj, world * 100 + T)
+    dx, dy = 1.1 / ni, 0.8 / nj
+    want = p.copy()
+    orc.solve_rb(want, rhs, dx, dy, 1.85, 1e-300, k)
+    cid = ("LOCAL:tbv%d_%d_%d" % (variant, world, T)).encode()
+    outs, errs = [None] * world, []
+
+    def body(r):
+        try:
+            with M.Grid(ni, nj, dx, dy, 1.85, 1e-300, k, device=0, nranks=world, rank=r,
+                        comm_id=cid) as g:
+                g.set_tuning(M.TUNE_TB_VARIANT, variant)
+                g.set_tuning(M.TUNE_TSTEPS, T)
+                loc = g.loc
+                g.upload(M.P, np.ascontiguousarray(
+                    p[loc.joff:loc.joff + loc.nj + 2, loc.ioff:loc.ioff + loc.ni + 2]))
+                g.upload(M.RHS, np.ascontiguousarray(
+                    rhs[loc.joff:loc.joff + loc.nj + 2, loc.ioff:loc.ioff + loc.ni + 2]))
+                it, _ = g.solve_rb()
+                outs[r] = (loc, g.download(M.P), it)
+        except BaseException as e:
+            errs.append((r, repr(e)))
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+        assert not t.is_alive(), "rank thread hung"
+    assert not errs, errs
+    got = np.full(p.shape, np.nan)
+    for loc, blk, it in outs:
+        assert it == k
+        nb = list(loc.neighbours)
+        i0, j0 = (0 if nb[0] < 0 else 1), (0 if nb[2] < 0 else 1)
+        i1 = loc.ni + 1 if nb[1] < 0 else loc.ni
+        j1 = loc.nj + 1 if nb[3] < 0 else loc.nj
+        got[loc.joff + j0:loc.joff + j1 + 1, loc.ioff + i0:loc.ioff + i1 + 1] = \
+            blk[j0:j1 + 1, i0:i1 + 1]
+    assert np.array_equal(got, want), np.argwhere(got != want)[:5]

@@ -144,7 +144,7 @@ def cpu_baseline_multicore(p, rhs, sweeps=10):
                       % (n, p.shape[0] - 2, sweeps, sec, threads)}
 
 
-def pmc_summary(size, nranks, T, chain):
+def pmc_summary(size, nranks, T, chain, kernel="rb_tb_kernel"):
     """The committed PMC summary (tools/pmc_summary.py) of the same launch shape
     -- size, ranks, iterations per pass, chained kernel or not -- or {} (the
     latest file in name order wins)."""
@@ -156,7 +156,8 @@ def pmc_summary(size, nranks, T, chain):
             continue
         if (d.get("size") == size and d.get("nranks", 1) == nranks
                 and d.get("iters_per_pass", 1) == T and "bytes_per_launch" in d
-                and bool(d.get("chain", False)) == bool(chain)):
+                and bool(d.get("chain", False)) == bool(chain)
+                and ("::%s<" % kernel) in d.get("kernel", "::rb_tb_kernel<")):
             best = dict(d, file=os.path.basename(path))
     return best
 
@@ -650,12 +651,17 @@ def main():
     split = pass_split(args.steps, T)
     if len(split) != st["timed_passes"]:
         split = None
+    # the passes' kernel: the library's pass plan picks the split-ring kernel
+    # (TB variants 12 / 13, sor_tbh.h) for short capped solves (misor_api.hip)
+    tbv = st.get("tb_variant", 0)
+    kernel = ("rb_tbh_kernel" if tbv in (12, 13) else
+              "rb_tbc_kernel" if chain else "rb_tb_kernel") if T > 1 else "rb_sweep_kernel"
     # traffic / VALU of the timed launches: the committed PMC summaries of each
     # pass length the split contains, weighted by its launches (null if one is
     # missing)
     traffic, valu, pmc_files = None, None, []
     if split:
-        pm = {t: pmc_summary(n, world, t, chain) for t in set(split)}
+        pm = {t: pmc_summary(n, world, t, chain, kernel) for t in set(split)}
         if all(pm[t] for t in pm):
             traffic = sum(pm[t]["bytes_per_launch"] for t in split) / len(split)
             pmc_files = sorted(pm[t]["file"] for t in pm)
@@ -688,15 +694,14 @@ def main():
                                "fixed %d iterations per timed region, 1 iteration = 1 step, "
                                "passes (kernel launches) of %s iterations" % (
                                    imax, jmax, args.steps, split_txt),
-                   "iters_per_pass": T, "pass_split": split,
+                   "iters_per_pass": T, "pass_split": split, "tb_variant": tbv,
                    "imax": imax, "jmax": jmax, "omega": 1.9, "problem": 2,
                    "decomposition": dims, "baseline_config": 4},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / PEAK_GBS, 4),
                      "traffic": traffic,
                      "traffic_ratio": round(traffic / hbm_min, 4) if traffic else None,
-                     "kernel": ("rb_tbc_kernel" if chain else "rb_tb_kernel") if T > 1
-                     else "rb_sweep_kernel",
+                     "kernel": kernel,
                      "iters_per_launch": round(iters_launch, 3), "kernel_ms": round(kern_ms, 4),
                      "bytes_per_launch": hbm_min,
                      "floors_ms": {"hbm": round(hbm_min / (PEAK_GBS * 1e9) * 1e3, 4),

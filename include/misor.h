@@ -109,7 +109,7 @@ typedef struct {
     long long timed_sweeps; /* iterations computed by the timed passes */
     long long timed_passes; /* passes covered by sweep_ms */
     int iters_per_pass;     /* T of the last multi-block solve (1: single sweep) */
-    int pad_;
+    int tb_variant;         /* its TB variant (MISOR_TUNE_TB_VARIANT; -1: single sweep) */
     /* decomposed solves, timing on: HIP events around every halo exchange
      * (pack + transport + unpack) and every residual all-reduce (+ loop test)
      * on the stream that runs it (the communication stream when overlapped) */

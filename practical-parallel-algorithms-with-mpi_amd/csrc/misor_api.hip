@@ -143,6 +143,7 @@ struct misor_grid {
     // temporally blocked sweep (sor_tb.hip): T iterations per pass over HBM
     int tsteps = kDefaultTsteps;  // requested T (1: single-iteration kernel)
     bool tsteps_set = false;      // T requested by MISOR_TUNE_TSTEPS (else the default rule)
+    bool short_plan = false;      // capped solves may run as kShortT-iteration split-ring passes
     SweepParams tp{};             // its launch geometry (for T = tsteps)
     int tb_nparts = 0;
     int tb_rows_req = 0;          // MISOR_TUNE_TB_ROWS (0: automatic)
@@ -896,6 +897,27 @@ static int configure_tb(misor_grid* g, int T, int variant, int rows) {
     }
     tb_geometry(g, std::max(2, Te), tp);
     g->tb_nparts = tb_parts(tp);
+    // The short plan (solve_rb_from): a single-rank solve capped at few
+    // iterations runs them in fewer, longer passes of the split-ring kernel
+    // when that saves a pass; its geometries share the partials
+    static const bool short_env = [] {
+        const char* e = getenv("MISOR_SHORT_PLAN");
+        return !(e && e[0] == '0');
+    }();
+    g->short_plan = short_env && variant == kDefaultTbVariant && !g->tsteps_set && !g->dist &&
+                    !chain_on(g, variant) && (long long)g->loc.ni * g->loc.nj >= kTsteps8Cells;
+    if (g->short_plan) {
+        for (int Tp = 1; Tp <= kShortT; ++Tp) {
+            SweepParams q = tp;
+            q.variant = kShortTbVariant;
+            tb_geometry(g, Tp, q);
+            if ((q.rows_per_block + 4LL * kMaxT + 8) * tp.pitch * 8 >= (1LL << 30)) {
+                g->short_plan = false;
+                break;
+            }
+            need = std::max(need, (long long)Tp * tb_parts(q));
+        }
+    }
     drop_chain_plans(g);  // geometry changed: rebuilt on first use
     if (chain_on(g, variant)) {
         for (int k = 0; k < 2; ++k) {  // the edge kernels' streams
@@ -1649,12 +1671,29 @@ static int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* 
     }
     // multi-block path: passes of T iterations (T = 1: single-iteration sweep
     // kernel; T >= 2: temporally blocked kernel, sor_tb.hip)
-    const int T = effective_tsteps(g);
+    //
+    // The short plan: a pass costs about the same for any T <= 8 (it streams
+    // its fields; profiles/r04_tcurve.txt), so a solve capped at few iterations
+    // is cheapest in as few passes as possible.  The split-ring kernel runs
+    // kShortT = 10 iterations a pass at ~1.4 x the time of a T = 8 pass
+    // (profiles/r04_ab_splitring.txt): where its passes times 1.4 undercut the
+    // default's pass count -- 9-10 and 17-20 iterations (the driver's
+    // 20-iteration solve: 2 passes instead of 7 + 7 + 6) -- the solve takes it.
+    const int todo0 = itermax - it0;
+    const bool shortp = g->short_plan && effective_tsteps(g) == kDefaultTsteps &&
+                        7LL * ((todo0 + kShortT - 1) / kShortT) <
+                            5LL * ((todo0 + kDefaultTsteps - 1) / kDefaultTsteps);
+    const int T = shortp ? kShortT : effective_tsteps(g);
+    SweepParams tpl = g->tp;  // the plan's geometry
+    if (shortp) {
+        tpl.variant = kShortTbVariant;
+        tb_geometry(g, T, tpl);
+    }
     // time the communication steps of the loop (collected after each batch)
     g->comm_timing = g->timing && g->dist;
     g->cev_used[0] = g->cev_used[1] = 0;
     const int depth = 2 * T;  // halo of src each pass needs
-    const int nparts = T == 1 ? g->nparts : g->tb_nparts;
+    const int nparts = T == 1 ? g->nparts : tb_parts(tpl);
     double* const rhs = g->fld[kRhs];
     auto pass = [&](hipStream_t s, int part, const double* src, double* dst, int Tp, int force,
                     double* partials) -> int {
@@ -1663,7 +1702,7 @@ static int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* 
             sp.part = part;
             launch_sweep(s, sp, src, dst, rhs, partials, g->st);
         } else {
-            SweepParams tp = g->tp;
+            SweepParams tp = tpl;
             tp.part = part;
             // the interior blocks of an overlapped pass leave workgroup slots to the
             // halo exchange, the residual all-reduce + loop test and the edge blocks
@@ -1786,7 +1825,7 @@ static int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* 
     };
     auto nparts_of = [&](int Tk) -> int {
         if (T == 1 || Tk == T) return nparts;
-        SweepParams tp = g->tp;
+        SweepParams tp = tpl;
         tb_geometry(g, Tk, tp);
         return tb_parts(tp);
     };
@@ -1981,6 +2020,7 @@ static int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* 
     g->last_iters = it;
     g->stats.sweeps += it - it0;
     g->stats.iters_per_pass = T;
+    g->stats.tb_variant = T == 1 ? -1 : tpl.variant;
     if (g->st_host->near)  // stopped before an iteration near the threshold
         return exact_tail(g, itermax, it, g->st_host->res, iters, res);
     if (iters) *iters = it;

@@ -84,6 +84,9 @@ constexpr TbVariant kTbVariants[] = {{4, 2, 2, 0, kMaxT, 0}, {8, 2, 2, 0, kMaxT,
                                      {4, 2, 2, 0, kMaxT, 0, 0, 0, 1}, {4, 2, 2, 0, kMaxT, 0, 1, 0, 1}};
 constexpr int kNumTbVariants = 14;
 constexpr int kHrTbVariant = 12;   // 13: skewed (T >= 2; T = 1 as 12)
+// the short plan of capped solves (misor_api.hip solve_rb_from)
+constexpr int kShortTbVariant = kHrTbVariant + 1;
+constexpr int kShortT = 10;
 constexpr int kSkewTbVariant = 9;
 constexpr int kLdsTbVariant = 10;  // 8 rows in flight; 11: 4
 constexpr int kQuadTbVariant = 5;

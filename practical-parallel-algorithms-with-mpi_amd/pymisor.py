@@ -59,7 +59,7 @@ class Local(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("sweeps", C.c_longlong), ("launches", C.c_longlong), ("sweep_ms", C.c_double),
                 ("timed_sweeps", C.c_longlong), ("timed_passes", C.c_longlong),
-                ("iters_per_pass", C.c_int), ("pad_", C.c_int),
+                ("iters_per_pass", C.c_int), ("tb_variant", C.c_int),
                 ("halo_ms", C.c_double), ("halos", C.c_longlong),
                 ("allreduce_ms", C.c_double), ("allreduces", C.c_longlong)]
 
@@ -329,7 +329,8 @@ class Grid:
         _check(lib().misor_get_stats(self.h, C.byref(s)))
         return {"sweeps": s.sweeps, "launches": s.launches, "sweep_ms": s.sweep_ms,
                 "timed_sweeps": s.timed_sweeps, "timed_passes": s.timed_passes,
-                "iters_per_pass": s.iters_per_pass, "halo_ms": s.halo_ms, "halos": s.halos,
+                "iters_per_pass": s.iters_per_pass, "tb_variant": s.tb_variant,
+                "halo_ms": s.halo_ms, "halos": s.halos,
                 "allreduce_ms": s.allreduce_ms, "allreduces": s.allreduces}
 
     def reset_stats(self):

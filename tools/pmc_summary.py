@@ -52,7 +52,7 @@ def main():
         for path in glob.glob(os.path.join(a.dir, "**", "fetch*counter_collection.csv"),
                               recursive=True):
             for r in csv.DictReader(open(path)):
-                m = re.search(r"rb_tb[cx]?_kernel<(\d+),", r["Kernel_Name"])
+                m = re.search(r"rb_tb[cxh]?_kernel<(\d+),", r["Kernel_Name"])
                 if m:
                     ts.add(int(m.group(1)))
         for t in sorted(ts):
@@ -62,7 +62,7 @@ def main():
 
 
 def summarise(a, iters, path_out):
-    kernel = a.kernel or r"rb_tb[cx]?_kernel<%d," % iters
+    kernel = a.kernel or r"rb_tb[cxh]?_kernel<%d," % iters
     f = rows(a.dir, "fetch", kernel)
     w = rows(a.dir, "write", kernel)
     s = rows(a.dir, "sq", kernel)

@@ -189,6 +189,38 @@ __device__ void rgrid_arrive(Bar3* bar, unsigned n, int mode) {
     }
 }
 
+// rgrid_arrive with the workgroup's residual partial folded in: every wave has
+// put its wave sum in sh[]; after the arrival barrier thread 0 adds them in
+// wave order (rblock_sum's order), stores the partial (relaxed agent-scope,
+// acknowledged before the arrival counts) and arrives -- one workgroup
+// barrier instead of rblock_sum's two plus the arrival's
+template <int NW>
+__device__ void rgrid_arrive_sum(Bar3* bar, unsigned n, int mode, const double* sh,
+                                 double* part, bool count) {
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double s = sh[0];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) s += sh[w];
+        __hip_atomic_store(part, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_s_waitcnt(0);
+        if (!count) return;
+        if (mode & 32) {
+            const unsigned x = blockIdx.x & 7, nb = gridDim.x;
+            const unsigned cx = (nb - x + 7) / 8;
+            const unsigned old = __hip_atomic_fetch_add(&bar->xcd[16 * x], 1u, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+            if (old + 1 == n * cx)
+                __hip_atomic_fetch_add(&bar->count, 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_fetch_add(&bar->count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 __device__ bool rgrid_wait(Bar3* bar, unsigned n, int* sh_flag, int mode) {
     if (threadIdx.x == 0) {
         const unsigned nb = gridDim.x;
@@ -514,6 +546,7 @@ __global__ __launch_bounds__(NT, 1) void k3_resident1(G3 g, double* __restrict__
     static_assert(NT % 256 == 0 && PZ % 2 == 0 && PZ % G == 0 && G % 2 == 0, "thread layout");
     __shared__ double L[kTcells];
     __shared__ double sh[NW];
+    __shared__ double sh_S;
     __shared__ int sh_flag;
     // built once: the shell's black cells to receive (LDS index | ghost-face bits
     // << 16, global offset) and the inner layer's red cells (LDS index | ghost
@@ -616,30 +649,14 @@ __global__ __launch_bounds__(NT, 1) void k3_resident1(G3 g, double* __restrict__
         return r;
     };
     double acc = 0.0;
-    // red cells one or more cells inside the box surface read only the box's
-    // black cells: they are computed into registers while the grid barrier
-    // completes (mode bit 11 off; sv, sacc) and written by commit() once the
-    // loop test says the iteration runs
-    auto deep = [&](int x, int z) {
-        return x >= 1 && x <= kRbx - 2 && y >= 1 && y <= kRby - 2 && z >= 1 && z <= kRbz - 2;
-    };
-    double sv[PZ];
-    double sacc = 0.0;
-    unsigned smask = 0;
-    // The thread's own cells (column pair, PZ planes) also live in registers
-    // when the box lies wholly inside the domain (every workgroup at 128^3):
-    // a cell's own value, its pair partner and its z-neighbours inside the
-    // thread's planes come from there, the rest (the far x-neighbour, y, the
-    // planes beyond) from LDS -- 3.5 LDS reads per update instead of 7 (the
-    // passes were LDS-bound).  LDS stays the complete copy (every update is
-    // written back): the neighbours read it.
+    // (round 4 also tried computing the red cells deep inside the box during
+    // the grid barrier's wait: ~1% with the separate residual sums, slower
+    // once they were folded into the barrier -- profiles/r04_res3d_modes.txt)
     double own[PZ][2];
     // the box's cells of colour col (1: red, i+j+k odd); black cells within two
-    // of the box surface go to the mailbox xm.  KIND 0: every cell; 1: the red
-    // cells that are not deep(); 2: the deep red cells, into sv / sacc only.
-    // REG: the register form (full boxes)
-    auto pass = [&](int col, double* xm, auto kind_c) {
-        constexpr int KIND = decltype(kind_c)::value;
+    // of the box surface go to the mailbox xm.  REG: the register form (full
+    // boxes)
+    auto pass = [&](int col, double* xm) {
         const int e0 = ((i0 + j + oz) & 1) == col ? 0 : 1;
 #pragma unroll
         for (int z0 = 0; z0 < PZ; z0 += G) {
@@ -675,20 +692,6 @@ __global__ __launch_bounds__(NT, 1) void k3_resident1(G3 g, double* __restrict__
                 const int z = zb + z0 + u, k = oz + z, e = e0 ^ (u & 1), i = i0 + e;
                 if (i > I || j > J || k > K) continue;
                 const int x = 2 * px + e;
-                if (KIND == 1 && deep(x, z)) continue;
-                if (KIND == 2) {
-                    if (!deep(x, z)) continue;
-                    const double cc = c[u];
-                    const double tx = (ap[u] - 2.0 * cc) + am[u];
-                    const double ty = (bp[u] - 2.0 * cc) + bm[u];
-                    const double tz = (cp[u] - 2.0 * cc) + cm[u];
-                    const double r = (e ? rh[z0 + u][1] : rh[z0 + u][0]) -
-                                     ((tx * idx2 + ty * idy2) + tz * idz2);
-                    sv[z0 + u] = cc - (factor * r);
-                    sacc += (r * r);
-                    smask |= 1u << (z0 + u);
-                    continue;
-                }
                 const int o = ((z + 2) * (kRby + 4) + (y + 2)) * kTsx + x + 2;
                 const double r = upd(o, i, j, k, e ? rh[z0 + u][1] : rh[z0 + u][0], c[u], am[u], ap[u],
                                      bm[u], bp[u], cm[u], cp[u]);
@@ -703,29 +706,6 @@ __global__ __launch_bounds__(NT, 1) void k3_resident1(G3 g, double* __restrict__
                     xstore(xm + gof(i, j, k), nv);
             }
         }
-    };
-    // the deep red cells computed ahead (pass KIND 2) into the box, ghost faces
-    // included (a deep cell can be the last of a ragged domain)
-    auto commit = [&]() {
-        const int e0 = ((i0 + j + oz) & 1) == 1 ? 0 : 1;
-#pragma unroll
-        for (int u = 0; u < PZ; ++u) {
-            if (!(smask >> u & 1u)) continue;
-            const int z = zb + u, k = oz + z, e = e0 ^ (u & 1), i = i0 + e;
-            const int o = ((z + 2) * (kRby + 4) + (y + 2)) * kTsx + 2 * px + e + 2;
-            const double v = sv[u];
-            L[o] = v;
-            if (REG) {
-                if (e) own[u][1] = v;
-                else   own[u][0] = v;
-            }
-            if (i == I) L[o + 1] = v;
-            if (j == J) L[o + kTsx] = v;
-            if (k == K) L[o + kTsy] = v;
-        }
-        acc += sacc;
-        sacc = 0.0;
-        smask = 0;
     };
     auto ring_red = [&]() {
         constexpr int RQ = (kTring / 2 + 64 + NT - 1) / NT;
@@ -786,11 +766,6 @@ __global__ __launch_bounds__(NT, 1) void k3_resident1(G3 g, double* __restrict__
     __syncthreads();
     // mode bits 2 / 4 / 512 / 1024 (timing experiments only, results wrong):
     // no shell exchange / no grid barrier / no ring update / no partials read
-    using K0 = std::integral_constant<int, 0>;
-    using K1 = std::integral_constant<int, 1>;
-    using K2 = std::integral_constant<int, 2>;
-    // bit 11: no work ahead of the barrier (the red pass whole, after it)
-    const bool ahead = PZ <= 8 && !(mode & 2048) && (mode & 24);
     if (REG) {
 #pragma unroll
         for (int u = 0; u < PZ; ++u) {
@@ -799,41 +774,41 @@ __global__ __launch_bounds__(NT, 1) void k3_resident1(G3 g, double* __restrict__
             own[u][1] = L[o + 1];
         }
     }
-    auto red_deep = [&]() { pass(1, nullptr, K2{}); };
-    if (ahead && !done) red_deep();
     while (!done) {
         double* const xm = mbox + (it & 1) * (long long)mstride;
         if (!(mode & 512)) ring_red();  // the neighbours' red cells next to the box
-        if (ahead) {
-            commit();
-            pass(1, xm, K1{});
-        } else {
-            pass(1, xm, K0{});
-        }
+        pass(1, xm);
         __syncthreads();
-        pass(0, xm, K0{});
-        const double s = rblock_sum<NW>(acc, sh);
+        pass(0, xm);
+        // the workgroup's residual: wave sums to sh[], added and published
+        // with the arrival (rgrid_arrive_sum)
+        {
+            const double ws = rwave_sum(acc);
+            if ((t & 63) == 0) sh[t >> 6] = ws;
+        }
         acc = 0.0;
         double* part = partials + (it & 1) * gridDim.x;
-        if (t == 0) xstore(part + b, s);
-        if (ahead) {
-            // arrive, compute the next iteration's deep red cells (from the
-            // final black cells of this one), then wait
-            if (!(mode & 4)) rgrid_arrive(bar, ++nbar, mode);
-            red_deep();
-            if (!(mode & 4) && !(ok = rgrid_wait(bar, nbar, &sh_flag, mode))) break;
-        } else if (!(mode & 4) && !(ok = rgrid_sync(bar, ++nbar, &sh_flag, mode))) {
-            break;
+        ++nbar;
+        rgrid_arrive_sum<NW>(bar, nbar, mode, sh, part + b, !(mode & 4));
+        if (!(mode & 4) && !(ok = rgrid_wait(bar, nbar, &sh_flag, mode))) break;
+        // the sum of all partials, by wave 0 in rblock_sum's order (the wave
+        // tree of partials 64 w .. 64 w + 63, then w = 0, 1, ...): every
+        // workgroup gets the same bits
+        if (t < 64) {
+            double S = 0.0;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const int k = t + 64 * w;
+                const double v = !(mode & 1024) && k < (int)gridDim.x ? xload(part + k) : 0.0;
+                S = w == 0 ? rwave_sum(v) : S + rwave_sum(v);
+            }
+            if (t == 0) sh_S = S;
         }
-        double q = 0.0;
-        if (!(mode & 1024))
-            for (int w = t; w < (int)gridDim.x; w += NT) q += xload(part + w);
         if (!(mode & 2)) receive(xm);
-        const double S = rblock_sum<NW>(q, sh);
-        res = (res + S) / cells;
+        __syncthreads();
+        res = (res + sh_S) / cells;
         ++it;
         done = !((res >= epssq) && (it < itermax));
-        __syncthreads();
     }
     if (!ok) return;
 #pragma unroll
@@ -863,9 +838,10 @@ __global__ __launch_bounds__(NT, 1) void k3_resident1(G3 g, double* __restrict__
 
 // the resident solve's form (MISOR3_RESIDENT_MODE, bits documented at
 // rgrid_sync and the kernels) and its kernel and threads per box (bit 7:
-// 1024, bit 8: 512, else 256).  Default 240: one barrier per iteration,
-// atomics, the two-level barrier, 1024 threads per box -- 128^3: 12.7 us per
-// iteration against 16.5 at 256 threads (profiles/r04_res3d_modes.txt)
+// 1024, bit 8: 512, else 256; bit 12: no register form).  Default 240: one
+// barrier per iteration, atomics, the two-level barrier, 1024 threads per box
+// -- 128^3: 12.7 us per iteration against 16.5 at 256 threads, same box
+// (profiles/r04_res3d_modes.txt)
 static int resident_mode() {
     static const int mode = [] {
         const char* e = getenv("MISOR3_RESIDENT_MODE");
@@ -874,11 +850,11 @@ static int resident_mode() {
     return mode;
 }
 
-// full: every box lies wholly inside the domain; the register form (an
-// experiment, mode bit 12: slower at 1024 threads, 17.5 against 13.8 us at
-// 128^3 -- it spills at 128 VGPRs -- profiles/r04_res3d_modes.txt)
+// full: every box lies wholly inside the domain -- then the register form
+// (REG; mode bit 12 turns it off): 128^3 at 12.2-12.6 us per iteration against
+// 12.7-13.2 for the LDS-only form, same box (profiles/r04_res3d_forms.txt)
 static void resident_kernel(int md, bool full, const void** fn, int* nt) {
-    const bool reg = full && (md & 4096);
+    const bool reg = full && !(md & 4096);
     if (!(md & 64)) {
         *fn = reinterpret_cast<const void*>(k3_resident);
         *nt = kRthreads;

@@ -22,10 +22,13 @@ def main():
     ap.add_argument("--size", type=int, nargs="+", default=[128, 384])
     ap.add_argument("--iters", type=int, default=60)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--lib", default="", help="load this libmisor.so instead (A/B runs)")
     ap.add_argument("--configs", nargs="+",
                     default=["0,8,0", "1,4,0", "1,8,0", "1,12,0", "1,4,16", "1,8,16",
                              "1,8,64"])
     a = ap.parse_args()
+    if a.lib:
+        M.LIBPATH = os.path.abspath(a.lib)
     for n in a.size:
         prm = dict(imax=n, jmax=n, kmax=n, xlength=1.0, ylength=1.0, zlength=1.0, re=1000.0,
                    gamma=0.9, tau=0.5, omg=1.8, eps=1e-300, itermax=a.iters, gx=0.0, gy=0.0,

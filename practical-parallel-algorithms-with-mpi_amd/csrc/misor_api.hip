@@ -871,6 +871,9 @@ static int chain_plan(misor_grid* g, int Tp, int part, const misor_grid::ChainPl
 static int configure_tb(misor_grid* g, int T, int variant, int rows) {
     if (T < 1 || T > kMaxT) return fail(MISOR_EINVAL, "iterations per pass must be 1..%d", kMaxT);
     if (variant < 0 || variant >= kNumTbVariants) return fail(MISOR_EINVAL, "bad tb variant");
+    if (variant == kHrTbVariant)  // measured, then not built
+        return fail(MISOR_EINVAL, "TB variant %d (unskewed split ring) is retired: use %d",
+                    kHrTbVariant, kHrTbVariant + 1);
     if (T > tb_max_t(variant))
         return fail(MISOR_EINVAL, "TB variant %d runs at most %d iterations per pass", variant,
                     tb_max_t(variant));

@@ -83,7 +83,7 @@ constexpr TbVariant kTbVariants[] = {{4, 2, 2, 0, kMaxT, 0}, {8, 2, 2, 0, kMaxT,
                                      {4, 2, 2, 0, kMaxT, 0, 0, 8}, {4, 2, 2, 0, kMaxT, 0, 0, 4},
                                      {4, 2, 2, 0, kMaxT, 0, 0, 0, 1}, {4, 2, 2, 0, kMaxT, 0, 1, 0, 1}};
 constexpr int kNumTbVariants = 14;
-constexpr int kHrTbVariant = 12;   // 13: skewed (T >= 2; T = 1 as 12)
+constexpr int kHrTbVariant = 12;   // retired after measurement; 13: skewed (T = 1 unskewed)
 // the short plan of capped solves (misor_api.hip solve_rb_from)
 constexpr int kShortTbVariant = kHrTbVariant + 1;
 constexpr int kShortT = 10;

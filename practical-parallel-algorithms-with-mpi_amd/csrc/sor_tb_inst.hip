@@ -146,10 +146,6 @@ void MISOR_CAT(launch_tb_t, MISOR_TB_T)(hipStream_t s, const SweepParams& prm,
         if (prm.pow2) go(rb_tb_kernel<kT, 4, 2, false, true, 1>, kLanes * 4, resident2<kT, 4, 2, false, 1>());
         else go(rb_tb_kernel<kT, 4, 2, false, false, 1>, kLanes * 4, resident2<kT, 4, 2, false, 1>());
         break;
-    case kHrTbVariant:
-        if (prm.pow2) go(rb_tbh_kernel<kT, 4, 2, true>, kLanes * 4, residenth<kT, 4, 2, true>());
-        else go(rb_tbh_kernel<kT, 4, 2, false>, kLanes * 4, residenth<kT, 4, 2, false>());
-        break;
     case kHrTbVariant + 1: {  // skewed (tb_ring_slots: T = 1 runs unskewed)
         constexpr int SK_ = kT >= 2 ? 1 : 0;
         if (prm.pow2) go(rb_tbh_kernel<kT, 4, 2, true, SK_>, kLanes * 4, residenth<kT, 4, 2, true, SK_>());
@@ -190,7 +186,6 @@ int MISOR_CAT(tb_resident_t, MISOR_TB_T)(int variant) {
     case 4: return resident2<kT, 4, 3, false>();
     case kSkewTbVariant: return resident2<kT, 4, 2, false, 1>();
     case kLdsTbVariant: return resident2<kT, 4, 2, false, 0, 8>();
-    case kHrTbVariant: return residenth<kT, 4, 2, false>();
     case kHrTbVariant + 1: return residenth<kT, 4, 2, false, kT >= 2 ? 1 : 0>();
     case kLdsTbVariant + 1: return resident2<kT, 4, 2, false, 0, 4>();
     case 6:

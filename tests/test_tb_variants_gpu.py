@@ -14,7 +14,9 @@ counts, res to 1e-12.
       block runs static-phase chunks (interior: whole warm-up chunks from a few
       rows early; sides and ragged blocks: row-tested chunks past the block's
       end)
-  13  the split ring with the skew of 9 (sor_tbh.h hrs_step; T = 1 as 12)
+  13  the split ring with the skew of 9 (sor_tbh.h hrs_step; T = 1 unskewed).
+      12 (the unskewed split ring) was measured and is no longer built:
+      configuring it fails (test_variant_12_retired)
 
 The geometry runs interior blocks (static-ring chunks), the general march
 (physical sides, ragged last block rows), convergence inside a pass, the
@@ -32,7 +34,7 @@ import pymisor as M
 pytestmark = pytest.mark.gpu
 
 SKEW, LDS8, LDS4, HR, HRS = 9, 10, 11, 12, 13
-VARIANTS = [SKEW, LDS8, LDS4, HR, HRS]
+VARIANTS = [SKEW, LDS8, LDS4, HRS]  # 12: measured, then retired (not built)
 
 
 def hr_slots(T, D=2, sk=0, most=18):
@@ -154,8 +156,7 @@ def test_variant_pow2_spacing(ni, nj, T, variant, monkeypatch):
         assert np.array_equal(got, want), (no, np.argwhere(got != want)[:5])
 
 
-@pytest.mark.parametrize("variant,T", [(v, 8) for v in VARIANTS] +
-                         [(HR, 10), (HR, 12), (HRS, 10), (HRS, 12)])
+@pytest.mark.parametrize("variant,T", [(v, 8) for v in VARIANTS] + [(HRS, 10), (HRS, 12)])
 def test_variant_default_geometry_large(variant, T):
     """8192^2, the automatic block height, the bench's problem 2 fields: one
     pass and a 20-iteration solve (T = 8: passes of 7 + 7 + 6; T = 10: 10 + 10)"""
@@ -217,3 +218,9 @@ def test_variant_decomposed(world, T, variant):
         got[loc.joff + j0:loc.joff + j1 + 1, loc.ioff + i0:loc.ioff + i1 + 1] = \
             blk[j0:j1 + 1, i0:i1 + 1]
     assert np.array_equal(got, want), np.argwhere(got != want)[:5]
+
+
+def test_variant_12_retired():
+    with M.Grid(300, 190, 1.0 / 300, 1.0 / 190, 1.7, 1e-300, 10) as g:
+        with pytest.raises(M.MisorError):
+            g.set_tuning(M.TUNE_TB_VARIANT, HR)

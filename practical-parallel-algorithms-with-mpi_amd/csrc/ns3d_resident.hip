@@ -76,17 +76,6 @@ __device__ __forceinline__ double rwave_sum(double v) {
     return v;
 }
 
-// 64-bit moves within 16-lane DPP rows: lane l receives lane l-1's (l+1's)
-// value; the row's first (last) lane receives 0
-__device__ __forceinline__ double row_from_left(double v) {
-    return __hiloint2double(__builtin_amdgcn_mov_dpp(__double2hiint(v), 0x111, 0xf, 0xf, true),
-                            __builtin_amdgcn_mov_dpp(__double2loint(v), 0x111, 0xf, 0xf, true));
-}
-__device__ __forceinline__ double row_from_right(double v) {
-    return __hiloint2double(__builtin_amdgcn_mov_dpp(__double2hiint(v), 0x101, 0xf, 0xf, true),
-                            __builtin_amdgcn_mov_dpp(__double2loint(v), 0x101, 0xf, 0xf, true));
-}
-
 // fixed-order sum over the workgroup (wave trees, then waves 0..NW-1 in
 // order); every thread gets the result
 template <int NW = 4>
@@ -678,11 +667,10 @@ __global__ __launch_bounds__(NT, 1) void k3_resident1(G3 g, double* __restrict__
                 const int o = ((z + 2) * (kRby + 4) + (y + 2)) * kTsx + 2 * px + e + 2;
                 if (REG) {
                     const int w = z0 + u;
-                    // the far x-neighbour is the next thread's register in the
-                    // same 16-lane DPP row (lane px -+ 1), except at the box's
-                    // x-faces, where it is a shell cell in LDS
-                    double far = e ? row_from_right(own[w][0]) : row_from_left(own[w][1]);
-                    if (e ? px == 15 : px == 0) far = L[e ? o + 1 : o - 1];
+                    // (the far x-neighbour from the next thread's register by a
+                    // DPP row shift measured slower, 12.8-13.1 against 12.3-12.6
+                    // us: profiles/r04_res3d_dpp.txt)
+                    const double far = L[e ? o + 1 : o - 1];
                     const double mine = e ? own[w][1] : own[w][0];
                     const double part = e ? own[w][0] : own[w][1];
                     c[u] = mine;

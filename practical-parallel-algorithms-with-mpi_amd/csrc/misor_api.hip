@@ -907,8 +907,13 @@ static int configure_tb(misor_grid* g, int T, int variant, int rows) {
         const char* e = getenv("MISOR_SHORT_PLAN");
         return !(e && e[0] == '0');
     }();
-    g->short_plan = short_env && variant == kDefaultTbVariant && !g->tsteps_set && !g->dist &&
-                    !chain_on(g, variant) && (long long)g->loc.ni * g->loc.nj >= kTsteps8Cells;
+    // (decomposed: on blocks of >= kShortDistCells, the two-GPU split of the
+    // bench grid, where a 10-iteration pass still costs ~1.4 T = 7 passes --
+    // 8.2 against 8.5 ms for 20 iterations, profiles/r04_blocks_splitring.txt;
+    // at 4 and 8 ranks it does not pay)
+    const long long cells = (long long)g->loc.ni * g->loc.nj;
+    g->short_plan = short_env && variant == kDefaultTbVariant && !g->tsteps_set &&
+                    !chain_on(g, variant) && cells >= (g->dist ? kShortDistCells : kTsteps8Cells);
     if (g->short_plan) {
         for (int Tp = 1; Tp <= kShortT; ++Tp) {
             SweepParams q = tp;

@@ -87,6 +87,7 @@ constexpr int kHrTbVariant = 12;   // retired after measurement; 13: skewed (T =
 // the short plan of capped solves (misor_api.hip solve_rb_from)
 constexpr int kShortTbVariant = kHrTbVariant + 1;
 constexpr int kShortT = 10;
+constexpr long long kShortDistCells = 1LL << 29;  // decomposed: local blocks at least this big
 constexpr int kSkewTbVariant = 9;
 constexpr int kLdsTbVariant = 10;  // 8 rows in flight; 11: 4
 constexpr int kQuadTbVariant = 5;

@@ -91,10 +91,13 @@ def test_fullfield_32768_bench_sequence():
     assert abs(res - res_ref) <= 1e-12 * res_ref, (res, res_ref)
 
 
-def test_fullfield_32768_eight_ranks():
-    n, world = 32768, 8
+@pytest.mark.parametrize("world", [2, 8])
+def test_fullfield_32768_ranks(world):
+    """8 ranks: chained T = 8 passes on 2^27-cell blocks; 2 ranks: 2^29-cell
+    blocks, the short pass plan (two 10-iteration split-ring passes)"""
+    n = 32768
     dx = 1.0 / n
-    cid = b"LOCAL:full8"
+    cid = ("LOCAL:full%d" % world).encode()
     outs, errs = [None] * world, []
 
     def body(r):
@@ -107,7 +110,9 @@ def test_fullfield_32768_eight_ranks():
                 p0, rhs = g.download(M.P), g.download(M.RHS)
                 it, res = g.solve_rb(itermax=STEPS)
                 chain = g.get_tuning(M.TUNE_TB_CHAIN)
-                outs[r] = [g.loc, p0, rhs, g.download(M.P), it, res, chain]
+                st = g.stats()
+                outs[r] = [g.loc, p0, rhs, g.download(M.P), it, res, chain,
+                           (st["iters_per_pass"], st["tb_variant"])]
         except BaseException as e:
             errs.append((r, repr(e)))
 
@@ -119,8 +124,11 @@ def test_fullfield_32768_eight_ranks():
         assert not t.is_alive(), "rank thread hung"
     assert not errs, errs
     assert all(o[4] == STEPS for o in outs)
-    assert all(o[6] == 1 for o in outs)  # chained passes on a 2^27-cell block
-    assert tuple(outs[0][0].dims) == (4, 2) and (outs[0][0].ni, outs[0][0].nj) == (8192, 16384)
+    if world == 8:
+        assert all(o[6] == 1 for o in outs)  # chained passes on a 2^27-cell block
+        assert tuple(outs[0][0].dims) == (4, 2) and (outs[0][0].ni, outs[0][0].nj) == (8192, 16384)
+    else:
+        assert all(o[7] == (10, 13) for o in outs), [o[7] for o in outs]  # the short plan
     p = np.empty((n + 2, n + 2))
     rhs = np.empty((n + 2, n + 2))
     got = np.empty((n + 2, n + 2))

@@ -22,8 +22,9 @@
 // 12 KB of LDS per wave, 96 KB per CU at two workgroups of four waves).
 //
 // Every block runs the static ring from its first step: interior blocks warm
-// up in whole chunks (WU = 4T rounded up to S steps, the stream starting WU -
-// 4T rows early; kPre chunks), then kSteady chunks; blocks at a physical side
+// up for exactly 4T steps (4T + 1 skewed) -- whole kPre chunks, then a partial
+// one -- and run kSteady chunks from that ring phase on (the warm-up rounded
+// up to whole chunks cost ~3% of a T = 10 pass); blocks at a physical side
 // or of a height the ring does not divide run kEdge / kRowEdge chunks over
 // ceil((H + 4T) / S) chunks, the steps past the block's last row reading
 // zeros (range-checked buffer loads) and storing / counting nothing (the row
@@ -43,9 +44,11 @@ struct Hr {
     static constexpr int K = hr_k(T, D, SK);      // stages 0 .. K-1: rhs from registers
     static constexpr int S = hr_slots(T, D, SK);  // slots of both rings (misor_internal.h)
     static constexpr int SKH = SK ? T / 2 : 0;    // leading stages of the skewed form
-    // interior warm-up steps: 4T rounded up to whole chunks -- at least 4T + 1
-    // in the skewed form, whose leading stages never see the stream's first row
-    static constexpr int WU = (4 * T + SK + S - 1) / S * S;
+    // interior warm-up steps: 4T -- 4T + 1 in the skewed form, whose leading
+    // stages never see the stream's first row: WU / S whole chunks, then WR
+    // steps; the steady chunks start at ring phase WR
+    static constexpr int WU = 4 * T + SK;
+    static constexpr int WR = WU % S;
     static_assert(!SK || (T >= 2 && K <= SKH), "skewed split ring");
 };
 
@@ -263,29 +266,34 @@ __device__ __forceinline__ void hrs_step(HrMarch<T, D>& m, d2* R, const Lane& c,
     __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int T, int D, int SK, int MODE, int Q0, bool P2, int... NN>
+// steps NN of a chunk whose first step has ring phase P0 and colour Q0
+template <int T, int D, int SK, int MODE, int Q0, bool P2, int P0 = 0, int... NN>
 __device__ __forceinline__ void hr_chunk(HrMarch<T, D>& m, d2* R, const Lane& c, const HrIo& io,
                                          int r0, unsigned off_n, unsigned st_base,
                                          std::integer_sequence<int, NN...>) {
+    constexpr int S = Hr<T, D, SK>::S;
     if constexpr (SK)
-        (hrs_step<T, D, MODE, Q0 ^ (NN & 1), NN, P2>(m, R, c, io, r0 + NN,
-                                                     off_n + (unsigned)NN * io.row_bytes, st_base),
+        (hrs_step<T, D, MODE, Q0 ^ (NN & 1), (P0 + NN) % S, P2>(
+             m, R, c, io, r0 + NN, off_n + (unsigned)NN * io.row_bytes, st_base),
          ...);
     else
-        (hr_step<T, D, MODE, Q0 ^ (NN & 1), NN, P2>(m, R, c, io, r0 + NN,
-                                                    off_n + (unsigned)NN * io.row_bytes, st_base),
+        (hr_step<T, D, MODE, Q0 ^ (NN & 1), (P0 + NN) % S, P2>(
+             m, R, c, io, r0 + NN, off_n + (unsigned)NN * io.row_bytes, st_base),
          ...);
 }
 
-// chunks [k0, k1) of a march of colour Q0 (colour of step 0)
-template <int T, int D, int SK, int MODE, int Q0, bool P2>
+// chunks [k0, k1) of a march of colour Q0 (colour of step 0), the first
+// starting at step n0 (ring phase n0 mod S = P0)
+template <int T, int D, int SK, int MODE, int Q0, bool P2, int P0 = 0>
 __device__ __forceinline__ void hr_run(HrMarch<T, D>& m, d2* R, const Lane& c, const HrIo& io,
-                                       int rs0, int k0, int k1, unsigned st_base) {
+                                       int rs0, int k0, int k1, unsigned st_base, int n0 = 0) {
     constexpr int S = Hr<T, D, SK>::S;
-    for (int k = k0; k < k1; ++k)
-        hr_chunk<T, D, SK, MODE, Q0, P2>(m, R, c, io, rs0 + k * S,
-                                         (unsigned)(k * S) * io.row_bytes, st_base,
-                                         std::make_integer_sequence<int, S>{});
+    for (int k = k0; k < k1; ++k) {
+        const int n = n0 + (k - k0) * S;
+        hr_chunk<T, D, SK, MODE, Q0 ^ (P0 & 1), P2, P0>(m, R, c, io, rs0 + n,
+                                                        (unsigned)n * io.row_bytes, st_base,
+                                                        std::make_integer_sequence<int, S>{});
+    }
 }
 
 // one wave's strip (tb_strip2's geometry and lane setup) through the
@@ -338,11 +346,10 @@ __device__ __forceinline__ void hr_strip(const SweepParams& prm, const double* _
     const bool rows_in = rs >= prm.upd_lo_j && rend <= prm.upd_hi_j && (j1 - j0) % S == 0 &&
                          j1 - j0 > 0;
     const bool steady = cols_in && rows_in;
-    // interior: the stream starts WU - 4T rows early (whole warm-up chunks);
     // skewed: the leading stages run one row ahead (they take rows rs0 + 1 ..
-    // rend + 1), so a side block starts one row early (its leading stages
-    // then see row rs first)
-    const int rs0 = steady ? rs - (WU - 4 * T) : rs - SK;
+    // rend + 1), so every block's stream starts one row early (its leading
+    // stages then see row rs first)
+    const int rs0 = rs - SK;
     const int nsteps = rend - rs0 + 1;
     const int nchunks = (nsteps + S - 1) / S;
 
@@ -384,16 +391,22 @@ __device__ __forceinline__ void hr_strip(const SweepParams& prm, const double* _
     for (int k = 0; k < D + SK; ++k) R[k] = bload(io.r, io.lane, (unsigned)k * io.row_bytes);
     const bool q1 = ((c.parity + rs0) & 1) != 0;  // colour of step 0 (S even: of every chunk)
     if (steady) {
-        // stores: step n finishes row rs0 + n - 2T = j0 + n - WU
+        // stores: step n finishes row rs0 + n - 2T = j0 + n - WU; the warm-up:
+        // KW whole chunks and WR steps, then H / S steady chunks from phase WR
         const unsigned sb = (unsigned)WU * io.row_bytes;
-        constexpr int KW = WU / S;
-        if (q1) {
-            hr_run<T, D, SK, kPre, 1, P2>(m, R, c, io, rs0, 0, KW, sb);
-            hr_run<T, D, SK, kSteady, 1, P2>(m, R, c, io, rs0, KW, nchunks, sb);
-        } else {
-            hr_run<T, D, SK, kPre, 0, P2>(m, R, c, io, rs0, 0, KW, sb);
-            hr_run<T, D, SK, kSteady, 0, P2>(m, R, c, io, rs0, KW, nchunks, sb);
-        }
+        constexpr int KW = WU / S, WR = Hr<T, D, SK>::WR;
+        const int nsteady = (j1 - j0) / S;
+        auto warm_steady = [&](auto q_c) {
+            constexpr int Q = decltype(q_c)::value;
+            hr_run<T, D, SK, kPre, Q, P2>(m, R, c, io, rs0, 0, KW, sb);
+            if constexpr (WR > 0)
+                hr_chunk<T, D, SK, kPre, Q, P2, 0>(m, R, c, io, rs0 + KW * S,
+                                                   (unsigned)(KW * S) * io.row_bytes, sb,
+                                                   std::make_integer_sequence<int, WR>{});
+            hr_run<T, D, SK, kSteady, Q, P2, WR>(m, R, c, io, rs0, 0, nsteady, sb, WU);
+        };
+        if (q1) warm_steady(std::integral_constant<int, 1>{});
+        else    warm_steady(std::integral_constant<int, 0>{});
     } else if (cols_in) {
         if (q1) hr_run<T, D, SK, kRowEdge, 1, P2>(m, R, c, io, rs0, 0, nchunks, 0);
         else    hr_run<T, D, SK, kRowEdge, 0, P2>(m, R, c, io, rs0, 0, nchunks, 0);

@@ -871,9 +871,9 @@ static int chain_plan(misor_grid* g, int Tp, int part, const misor_grid::ChainPl
 static int configure_tb(misor_grid* g, int T, int variant, int rows) {
     if (T < 1 || T > kMaxT) return fail(MISOR_EINVAL, "iterations per pass must be 1..%d", kMaxT);
     if (variant < 0 || variant >= kNumTbVariants) return fail(MISOR_EINVAL, "bad tb variant");
-    if (variant == kHrTbVariant)  // measured, then not built
-        return fail(MISOR_EINVAL, "TB variant %d (unskewed split ring) is retired: use %d",
-                    kHrTbVariant, kHrTbVariant + 1);
+    if (tb_max_t(variant) == 0)  // measured slower, then not built
+        return fail(MISOR_EINVAL, "TB variant %d is retired (measured slower; not built)",
+                    variant);
     if (T > tb_max_t(variant))
         return fail(MISOR_EINVAL, "TB variant %d runs at most %d iterations per pass", variant,
                     tb_max_t(variant));
@@ -1468,12 +1468,28 @@ static int ensure_events(misor_grid* g, size_t n) {
 }
 
 static int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* iters,
-                         double* res);
+                         double* res, bool* hand_off);
+static int exact_tail(misor_grid* g, int itermax, int it0, double res0, int* iters, double* res,
+                      bool* hand_off);
 
+// The batched passes and the exact tail (below) hand the solve to each other
+// (*hand_off) with the iterations done and the last residual; this loop runs
+// them in turn, so the hand-overs of a long solve need no stack.
 int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
     if (!g) return fail(MISOR_EINVAL, "null grid");
     HIPCHK(hipSetDevice(g->device));
-    return solve_rb_from(g, itermax, 0, 1.0, iters, res);  // res = 1.0: solver.c:196
+    int it = 0;
+    double r = 1.0;  // solver.c:196
+    for (bool tail = false;; tail = !tail) {
+        bool hand_off = false;
+        const int rc = tail ? exact_tail(g, itermax, it, r, &it, &r, &hand_off)
+                            : solve_rb_from(g, itermax, it, r, &it, &r, &hand_off);
+        if (rc) return rc;
+        if (!hand_off) break;
+    }
+    if (iters) *iters = it;
+    if (res) *res = r;
+    return MISOR_OK;
 }
 
 // ---------------------------------------------------------------------------
@@ -1538,8 +1554,8 @@ static int exact_residual(misor_grid* g, double cells, double* out) {
 
 // iterations it0 + 1 .. of solveRB from the current field, one sweep each with
 // the exact residual and the loop test on the host (solver.c:197)
-static int exact_tail(misor_grid* g, int itermax, int it0, double res0, int* iters,
-                      double* res) {
+static int exact_tail(misor_grid* g, int itermax, int it0, double res0, int* iters, double* res,
+                      bool* hand_off) {
     const double epssq = g->desc.eps * g->desc.eps;
     const double cells = (double)g->desc.imax * (double)g->desc.jmax;
     if (!g->rsq) {
@@ -1591,10 +1607,12 @@ static int exact_tail(misor_grid* g, int itermax, int it0, double res0, int* ite
         g->stats.launches += 1;
         // back to the batched passes after 2T iterations outside the band
         far = fabs(r - epssq) > g->near_rel * epssq ? far + 1 : 0;
-        if (far >= 2 * T && (r >= epssq) && (it < itermax))
-            return solve_rb_from(g, itermax, it, r, iters, res);
+        if (far >= 2 * T && (r >= epssq) && (it < itermax)) {
+            *hand_off = true;  // back to solve_rb_from (misor_solve_rb_n)
+            break;
+        }
     }
-    if (g->dist) {  // leave the halo of the final field consistent (adaptUV reads it)
+    if (g->dist && !*hand_off) {  // leave the halo of the final field consistent (adaptUV reads it)
         int rc = exchange(g, pbuf(g, g->cur), 2);
         if (rc) return rc;
     }
@@ -1604,13 +1622,13 @@ static int exact_tail(misor_grid* g, int itermax, int it0, double res0, int* ite
     }
     g->stats.sweeps += it - it0;
     g->last_iters = it;
-    if (iters) *iters = it;
-    if (res) *res = r;
+    *iters = it;
+    *res = r;
     return MISOR_OK;
 }
 
 static int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* iters,
-                         double* res) {
+                         double* res, bool* hand_off) {
     const double epssq = g->desc.eps * g->desc.eps;
     DevState s0{};
     s0.it = it0;
@@ -1622,8 +1640,8 @@ static int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* 
     s0.nband = g->near_rel > 0.0 && epssq > 0.0 ? g->near_rel * epssq : -1.0;
     s0.done = !((res0 >= epssq) && (it0 < itermax));  // loop test of solver.c:197
     if (s0.done) {
-        if (iters) *iters = it0;
-        if (res) *res = res0;
+        *iters = it0;
+        *res = res0;
         return MISOR_OK;
     }
     *g->st_host = s0;
@@ -1669,12 +1687,15 @@ static int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* 
                                g->sp.idx2, g->sp.idy2, g->sp.coef, cells, g->st);
             HIPCHK(hipGetLastError());
             g->stats.sweeps += it - it0;
-            return exact_tail(g, itermax, it, rn, iters, res);
+            *hand_off = true;  // the exact tail from iteration it (misor_solve_rb_n)
+            *iters = it;
+            *res = rn;
+            return MISOR_OK;
         }
         g->stats.sweeps += it - it0;
         g->last_iters = it;
-        if (iters) *iters = it;
-        if (res) *res = g->st_host->res;
+        *iters = it;
+        *res = g->st_host->res;
         return MISOR_OK;
     }
     // multi-block path: passes of T iterations (T = 1: single-iteration sweep
@@ -2029,10 +2050,11 @@ static int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* 
     g->stats.sweeps += it - it0;
     g->stats.iters_per_pass = T;
     g->stats.tb_variant = T == 1 ? -1 : tpl.variant;
-    if (g->st_host->near)  // stopped before an iteration near the threshold
-        return exact_tail(g, itermax, it, g->st_host->res, iters, res);
-    if (iters) *iters = it;
-    if (res) *res = g->st_host->res;
+    // stopped before an iteration near the threshold: the exact tail goes on
+    // from it (misor_solve_rb_n)
+    if (g->st_host->near) *hand_off = true;
+    *iters = it;
+    *res = g->st_host->res;
     return MISOR_OK;
 }
 
@@ -2299,9 +2321,16 @@ int misor_set_tuning(misor_grid* g, int key, int value) {
         return configure_sweep(g, g->sp.variant, g->sp.rows_per_block, value != 0);
     case MISOR_TUNE_SMALL_SOLVE: g->small_solve = value != 0; return MISOR_OK;
     case MISOR_TUNE_OVERLAP: g->overlap = value != 0; return MISOR_OK;
-    case MISOR_TUNE_TSTEPS:
-        g->tsteps_set = true;
-        return configure_tb(g, value, g->tp.variant, g->tb_rows_req);
+    case MISOR_TUNE_TSTEPS: {
+        // a request equal to the default rule's T is no request (the short
+        // plan and the chained-block re-pick stay on); a rejected one changes
+        // nothing
+        const bool prev = g->tsteps_set;
+        g->tsteps_set = value != default_tsteps(g, g->tp.variant);
+        const int rc = configure_tb(g, value, g->tp.variant, g->tb_rows_req);
+        if (rc) g->tsteps_set = prev;
+        return rc;
+    }
     case MISOR_TUNE_TB_VARIANT: return configure_tb(g, g->tsteps, value, g->tb_rows_req);
     case MISOR_TUNE_TB_ROWS: return configure_tb(g, g->tsteps, g->tp.variant, value);
     case MISOR_TUNE_TB_PERSISTENT:

@@ -66,32 +66,30 @@ int sweep_waves(int variant);
 // SIMD) or 4 (256-column strips, rhs ring in LDS, 1 wave per SIMD; T <= kMaxQuadT)
 // quad variants: sched = how far the compiler may interleave steps (sor_tb.h
 // qstep), max_t = the largest T whose LDS ring fits (2T + D (+1) rows of 2 KB per wave)
-// xch: the strips of a workgroup exchange their edge columns through LDS
-// (sor_tbx.h rb_tbx_kernel): the workgroup loads 128 W columns and owns
-// 128 W - 4T of them; its rhs ring is in LDS (max_t: two workgroups per CU)
-// skew: the steady march in two independent stage chains per step (sor_tb.h
-// skew_step); lds: rows in flight per array through an LDS queue (sor_tb.h
-// steady_step DL); hr: the split rhs ring, registers + LDS (sor_tbh.h)
+// skew: the split-ring march in two independent stage chains per step (sor_tbh.h
+// hrs_step); hr: the split rhs ring, registers + LDS (sor_tbh.h)
+// max_t = 0: retired -- measured slower and no longer built (DESIGN.md section 4:
+// 6-8 strips exchanging edge columns through LDS, 9 the skewed register-ring
+// march, 10/11 an LDS row queue, 12 the unskewed split ring); configuring one
+// fails.  The 2-column register-ring kernels run T <= kMaxT2 (above that their
+// rhs ring spills); only the split ring (13) runs T up to kMaxT.
+constexpr int kMaxT2 = 8;
 struct TbVariant {
-    int waves, ahead, cols, sched, max_t, xch, skew, lds, hr;
+    int waves, ahead, cols, sched, max_t, skew, hr;
 };
-constexpr TbVariant kTbVariants[] = {{4, 2, 2, 0, kMaxT, 0}, {8, 2, 2, 0, kMaxT, 0},
-                                     {2, 2, 2, 0, kMaxT, 0}, {1, 2, 2, 0, kMaxT, 0},
-                                     {4, 3, 2, 0, kMaxT, 0}, {4, 2, 4, 0, 8, 0},
-                                     {4, 2, 2, 0, 10, 1},    {8, 2, 2, 0, 10, 1},
-                                     {2, 2, 2, 0, 10, 1},    {4, 2, 2, 0, kMaxT, 0, 1},
-                                     {4, 2, 2, 0, kMaxT, 0, 0, 8}, {4, 2, 2, 0, kMaxT, 0, 0, 4},
-                                     {4, 2, 2, 0, kMaxT, 0, 0, 0, 1}, {4, 2, 2, 0, kMaxT, 0, 1, 0, 1}};
+constexpr TbVariant kTbVariants[] = {
+    {4, 2, 2, 0, kMaxT2}, {8, 2, 2, 0, kMaxT2}, {2, 2, 2, 0, kMaxT2}, {1, 2, 2, 0, kMaxT2},
+    {4, 3, 2, 0, kMaxT2}, {4, 2, 4, 0, 8},
+    {4, 2, 2, 0, 0},      {4, 2, 2, 0, 0},      {4, 2, 2, 0, 0},      {4, 2, 2, 0, 0},
+    {4, 2, 2, 0, 0},      {4, 2, 2, 0, 0},      {4, 2, 2, 0, 0},
+    {4, 2, 2, 0, kMaxT, 1, 1}};
 constexpr int kNumTbVariants = 14;
-constexpr int kHrTbVariant = 12;   // retired after measurement; 13: skewed (T = 1 unskewed)
+constexpr int kHrTbVariant = 13;   // the skewed split ring (T = 1 unskewed)
 // the short plan of capped solves (misor_api.hip solve_rb_from)
-constexpr int kShortTbVariant = kHrTbVariant + 1;
+constexpr int kShortTbVariant = kHrTbVariant;
 constexpr int kShortT = 10;
 constexpr long long kShortDistCells = 1LL << 29;  // decomposed: local blocks at least this big
-constexpr int kSkewTbVariant = 9;
-constexpr int kLdsTbVariant = 10;  // 8 rows in flight; 11: 4
 constexpr int kQuadTbVariant = 5;
-constexpr int kXchTbVariant = 6;
 // iterations per pass: 8 on large local blocks, 7 below kTsteps8Cells cells
 // (32768^2 0.744 vs 0.785 ms/iteration, profiles/r02_tune_t789.txt; one rank's
 // 8192 x 16384 block at 8 GPUs 0.118-0.122 at T = 7 vs 0.125 at T = 8,
@@ -133,7 +131,6 @@ int tb_resident(int T, int variant);
 int tb_cols(int variant);
 int tb_max_t(int variant);
 int tb_out_width(int T, int variant);           // owned columns of one wave's strip
-int tb_xch(int variant);                        // the exchange kernel (sor_tbx.h)
 int tb_nbx(int ni, int T, int variant);         // block columns of a pass of T iterations
 
 // Solver state that lives on the device between launches.  Written only by
@@ -146,7 +143,8 @@ struct DevState {
                    // eps^2 (misor_api.hip exact_tail recomputes from there)
     double res;    // residual of the last iteration
     double epssq;
-    double nband;  // |res - eps^2| <= nband: near the threshold (0: never)
+    double nband = -1.0;  // |res - eps^2| <= nband: near the threshold (< 0: off, the
+                          // default of every DevState the host builds)
     double sum[kMaxT];  // sum r^2 of each iteration of the last pass (this rank,
                         // then all-reduced)
 };

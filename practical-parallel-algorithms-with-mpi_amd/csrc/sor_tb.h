@@ -151,13 +151,6 @@ __host__ __device__ constexpr int ring_slots() {
     return 2 * T + D + SK + ((D + SK) & 1);
 }
 
-// the skewed steady march (skew_step) splits the stages at SKH = T/2; T < 4:
-// no skew
-template <int T>
-__host__ __device__ constexpr int skew_split() {
-    return T >= 4 ? T / 2 : 0;
-}
-
 // per-lane constants shared by all stages
 struct Lane {
     int ia, ib;            // the lane's two columns (ia odd)
@@ -251,7 +244,7 @@ __device__ __forceinline__ d2 stage(const Lane& c, int t, bool fixrows, d2 In, i
     const double idx2 = c.idx2, idy2 = c.idy2, coef = c.coef;
     // residual windows of this stage (header): red rows [j0 + sh, j1 + sh),
     // black rows one lower, extended to the physical sides; in a skewed pass
-    // (SKH > 0, skew_step) the leading stages t < SKH one row higher
+    // (SKH > 0, sor_tbh.h hrs_step) the leading stages t < SKH one row higher
     const int sh = 2 * T - 1 - 2 * t + (t < SKH ? 1 : 0);
     auto tally = [&](double r, int row, int wsh, bool own_col) {
         if (MODE == kSteady) {
@@ -328,7 +321,6 @@ struct March {
     d2 Pq[D], Rq[D];  // rows in flight: p(r0 .. r0+D-1), rhs(r0-1 .. r0+D-2)
     TallyAcc acc[T];
     d2 keep[2];
-    d2 B;  // skewed march: stage SKH-1's output row of the previous step
 };
 
 struct Io {
@@ -340,7 +332,7 @@ struct Io {
 
 // one paired-march step: stream in old row r0, push it through the T stages,
 // store the row the last stage finished (r0 - 2T) if this block owns it
-template <int T, int D, int Q, int MODE, bool BP = false, bool P2 = false, int SKH = 0>
+template <int T, int D, int Q, int MODE, bool BP = false, bool P2 = false>
 __device__ __forceinline__ void tb_step(March<T, D>& m, const Lane& c, const Io& io, int r0) {
     const long long pitch = io.pitch;
     const d2 nP = ldv(io.sp + (long long)(r0 + D) * pitch);
@@ -353,8 +345,8 @@ __device__ __forceinline__ void tb_step(March<T, D>& m, const Lane& c, const Io&
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         const d2 prevM2 = m.M2[t];
-        v = stage<T, Q, MODE, BP, P2, SKH>(c, t, t > 0, v, r0 - 2 * t, m.A[t], m.M1[t], m.M2[t],
-                                       m.R[2 * t], m.R[2 * t + 1], m.acc[t]);
+        v = stage<T, Q, MODE, BP, P2>(c, t, t > 0, v, r0 - 2 * t, m.A[t], m.M1[t], m.M2[t],
+                                      m.R[2 * t], m.R[2 * t + 1], m.acc[t]);
         if (t == T - 1 && MODE != kPre) {
             const int jw = r0 - 2 * T;  // row finished by the last stage
             if (MODE == kRowEdge) {
@@ -401,14 +393,14 @@ __device__ __forceinline__ void tb_step(March<T, D>& m, const Lane& c, const Io&
 }
 
 // paired march over steps r0 = rs .. rend (the colour Q0 of row rs a constant)
-template <int T, int D, int Q0, int MODE, bool BP = false, bool P2 = false, int SKH = 0>
+template <int T, int D, int Q0, int MODE, bool BP = false, bool P2 = false>
 __device__ __forceinline__ void march_pairs(March<T, D>& m, const Lane& c, const Io& io, int r0,
                                             int rend) {
     for (; r0 + 1 <= rend; r0 += 2) {
-        tb_step<T, D, Q0, MODE, BP, P2, SKH>(m, c, io, r0);
-        tb_step<T, D, 1 - Q0, MODE, BP, P2, SKH>(m, c, io, r0 + 1);
+        tb_step<T, D, Q0, MODE, BP, P2>(m, c, io, r0);
+        tb_step<T, D, 1 - Q0, MODE, BP, P2>(m, c, io, r0 + 1);
     }
-    if (r0 <= rend) tb_step<T, D, Q0, MODE, BP, P2, SKH>(m, c, io, r0);
+    if (r0 <= rend) tb_step<T, D, Q0, MODE, BP, P2>(m, c, io, r0);
 }
 
 // Steady march: buffer descriptors over the wave's strip (wave-uniform base,
@@ -421,16 +413,7 @@ struct Sio {
     unsigned st_lane;                // lane * 16 if the lane stores, else out of range
     unsigned st_a, st_b;             // kSteadyEdge: per column (lane * 16 (+ 8) or out of range)
     unsigned row_bytes;              // pitch * 8
-    double* lq;                      // DL > 0: the wave's LDS row queue (steady_step)
 };
-
-// one 16-byte-per-lane LDS DMA of a 128-column row segment (lane l's 16 bytes
-// land at lds + 16 l)
-__device__ __forceinline__ void row_dma(__amdgpu_buffer_rsrc_t r, double* lds, unsigned voff,
-                                        unsigned soff) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16,
-                                             voff, soff, 0, 0);
-}
 
 __device__ __forceinline__ d2 bload(__amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned soff) {
     return __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
@@ -439,35 +422,16 @@ __device__ __forceinline__ d2 bload(__amdgpu_buffer_rsrc_t rs, unsigned voff, un
 // one step of the steady march: stream row r0 = rs + n, tally and store.  PH
 // = n mod S (a constant): rhs row rs - 1 + j lives in ring slot j mod S, and
 // stage t reads rows j = n - 2t (red) and n - 2t - 1 (black)
-//
-// DL > 0: the rows come through an LDS queue of DL slots per array (io.lq: p
-// slots 0 .. DL-1, rhs slots DL .. 2DL-1; row n in slot n mod DL), filled by
-// LDS DMA DL rows ahead -- DL rows of each array in flight per wave instead
-// of the D the registers hold.  Every steady step issues exactly 3 VMEM
-// operations (the store, then the two DMAs), so the DMAs of row n + D, issued
-// DL - D steps ago, have landed once at most 3 (DL - D - 1) younger ones are
-// outstanding; the registers take row n + D from LDS in place of the loads.
-template <int T, int D, int Q, int PH, bool BP, bool P2, bool EM = false, int DL = 0>
+template <int T, int D, int Q, int PH, bool BP, bool P2, bool EM = false>
 __device__ __forceinline__ void steady_step(March<T, D>& m, d2* R, const Lane& c, const Sio& io,
-                                            int r0, unsigned off_n, int n = 0) {
+                                            int r0, unsigned off_n) {
     constexpr int S = ring_slots<T, D>();
     // p row r0 + D (p descriptor starts at row rs), rhs row r0 - 1 + D (rhs
     // descriptor starts at row rs - 1): both n + D rows in; the rhs row lands
     // in the slot of the row stage T-1 finished with in the previous step
     const unsigned ld = off_n + (unsigned)D * io.row_bytes;
-    d2 nP;
-    if constexpr (DL > 0) {
-        static_assert(DL > D + 1 && (DL & (DL - 1)) == 0, "LDS queue depth");
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * (DL - D - 1)) : "memory");
-        const int sl = (n + D) & (DL - 1);
-        const lds_double* q = (const lds_double*)io.lq + (io.lane >> 3);
-        nP = *reinterpret_cast<const __attribute__((address_space(3))) d2*>(q + sl * kStripCells);
-        R[(PH + D) % S] =
-            *reinterpret_cast<const __attribute__((address_space(3))) d2*>(q + (DL + sl) * kStripCells);
-    } else {
-        nP = bload(io.p, io.lane, ld);
-        R[(PH + D) % S] = bload(io.r, io.lane, ld);
-    }
+    const d2 nP = bload(io.p, io.lane, ld);
+    R[(PH + D) % S] = bload(io.r, io.lane, ld);
     d2 v = m.Pq[0];
 #pragma unroll
     for (int t = 0; t < T; ++t) {
@@ -499,12 +463,6 @@ __device__ __forceinline__ void steady_step(March<T, D>& m, d2* R, const Lane& c
     asm volatile("" ::"v"(m.keep[0]));
     m.keep[0] = m.keep[1];
     m.keep[1] = v;
-    if constexpr (DL > 0) {  // row n + DL into slot n mod DL (row n's, read D steps ago)
-        const int sl = n & (DL - 1);
-        const unsigned o = off_n + (unsigned)DL * io.row_bytes;
-        row_dma(io.p, io.lq + sl * kStripCells, io.lane, o);
-        row_dma(io.r, io.lq + (DL + sl) * kStripCells, io.lane, o);
-    }
 #pragma unroll
     for (int k = 0; k + 1 < D; ++k) m.Pq[k] = m.Pq[k + 1];
     m.Pq[D - 1] = nP;
@@ -514,13 +472,13 @@ __device__ __forceinline__ void steady_step(March<T, D>& m, d2* R, const Lane& c
 }
 
 // S steps of the steady march, the first (step n) at slot phase P0 (colour Q0)
-template <int T, int D, int Q0, int P0, bool BP, bool P2, bool EM = false, int DL = 0, int... NN>
+template <int T, int D, int Q0, int P0, bool BP, bool P2, bool EM = false, int... NN>
 __device__ __forceinline__ void steady_chunk(March<T, D>& m, d2* R, const Lane& c, const Sio& io,
                                              int r0, unsigned off_n,
-                                             std::integer_sequence<int, NN...>, int n = 0) {
+                                             std::integer_sequence<int, NN...>) {
     constexpr int S = ring_slots<T, D>();
-    (steady_step<T, D, Q0 ^ (NN & 1), (P0 + NN) % S, BP, P2, EM, DL>(
-         m, R, c, io, r0 + NN, off_n + (unsigned)NN * io.row_bytes, n + NN),
+    (steady_step<T, D, Q0 ^ (NN & 1), (P0 + NN) % S, BP, P2, EM>(
+         m, R, c, io, r0 + NN, off_n + (unsigned)NN * io.row_bytes),
      ...);
 }
 
@@ -586,91 +544,13 @@ __device__ __forceinline__ void stage_pair(const Lane& c, d2& InA, d2& A_a, d2& 
     M2_b = F_b; M1_b = Mr_b; A_b = InB; InB = F_b;
 }
 
-// One step n of the skewed steady march (SKH > 0).  Within a plain step the
-// T stages form ONE dependency chain (stage t's input is stage t-1's output
-// of the same step: 2T updates of ~6 dependent FP64 operations each, which two
-// waves per SIMD do not hide).  Here the trailing stages SKH .. T-1 run step n
-// on the row stage SKH-1 finished one step earlier (m.B), while the leading
-// stages 0 .. SKH-1 run step n + 1 on the streamed row: two independent
-// chains per step.  The leading stages are one row ahead, so they stream one
-// more row per block (tb_strip2) and their residual windows sit one row higher
-// (stage()); the ring keeps one more row (ring_slots<T, D, 1>).  FIRST: the
-// leading stages' mode (kPre in the half step that opens the skew); SECOND:
-// run the trailing stages and store (not in that half step).  Q / PH: colour
-// and ring phase of step n.
-template <int T, int D, int SKH, int Q, int PH, bool P2, int FIRST, bool SECOND>
-__device__ __forceinline__ void skew_step(March<T, D>& m, d2* R, const Lane& c, const Sio& io,
-                                          int r0, unsigned off_n) {
-    constexpr int S = ring_slots<T, D, 1>();
-    // p row r0 + 1 + D, rhs row (r0 - 1) + 1 + D: the leading stages' row D steps ahead
-    const unsigned ld = off_n + (unsigned)(D + 1) * io.row_bytes;
-    const d2 nP = bload(io.p, io.lane, ld);
-    R[(PH + 1 + D) % S] = bload(io.r, io.lane, ld);
-    d2 v = m.Pq[0];
-    if (SECOND) {
-        static_assert(!SECOND || FIRST == kSteady, "the pair form runs steady stages");
-        // stage SKH + k of the trailing chain beside stage k of the leading one
-        d2 u = m.B;
-#pragma unroll
-        for (int k = 0; k < SKH; ++k) {
-            const int ta = SKH + k, tb = k;
-            stage_pair<Q, 1 - Q, P2>(c, u, m.A[ta], m.M1[ta], m.M2[ta], R[(PH - 2 * ta + 4 * S) % S],
-                                     R[(PH - 2 * ta - 1 + 4 * S) % S], m.acc[ta], v, m.A[tb],
-                                     m.M1[tb], m.M2[tb], R[(PH + 1 - 2 * tb + 4 * S) % S],
-                                     R[(PH - 2 * tb + 4 * S) % S], m.acc[tb]);
-        }
-        if (T - SKH > SKH)  // odd T: the trailing chain's last stage alone
-            u = stage<T, Q, kSteady, false, P2, SKH>(
-                c, T - 1, true, u, r0 - 2 * (T - 1), m.A[T - 1], m.M1[T - 1], m.M2[T - 1],
-                R[(PH - 2 * (T - 1) + 4 * S) % S], R[(PH - 2 * (T - 1) - 1 + 4 * S) % S],
-                m.acc[T - 1]);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, u), io.d, io.st_lane,
-                                               off_n - 4u * T * io.row_bytes, 2);
-        asm volatile("" ::"v"(m.keep[0]));  // the store's data registers (steady_step)
-        m.keep[0] = m.keep[1];
-        m.keep[1] = u;
-    } else {
-#pragma unroll
-        for (int t = 0; t < SKH; ++t)
-            v = stage<T, 1 - Q, FIRST, false, P2, SKH>(c, t, t > 0, v, r0 + 1 - 2 * t, m.A[t],
-                                                       m.M1[t], m.M2[t],
-                                                       R[(PH + 1 - 2 * t + 4 * S) % S],
-                                                       R[(PH - 2 * t + 4 * S) % S], m.acc[t]);
-    }
-    m.B = v;
-#pragma unroll
-    for (int k = 0; k + 1 < D; ++k) m.Pq[k] = m.Pq[k + 1];
-    m.Pq[D - 1] = nP;
-    __builtin_amdgcn_sched_barrier(0);
-}
-
-template <int T, int D, int SKH, int Q0, int P0, bool P2, int... NN>
-__device__ __forceinline__ void skew_chunk(March<T, D>& m, d2* R, const Lane& c, const Sio& io,
-                                           int r0, unsigned off_n,
-                                           std::integer_sequence<int, NN...>) {
-    constexpr int S = ring_slots<T, D, 1>();
-    (skew_step<T, D, SKH, Q0 ^ (NN & 1), (P0 + NN) % S, P2, kSteady, true>(
-         m, R, c, io, r0 + NN, off_n + (unsigned)NN * io.row_bytes),
-     ...);
-}
-
 // interior block of H = k * S rows: 4T paired warm-up steps, then k chunks of
-// S statically unrolled steps (SKH > 0: skewed, after a half step)
-template <int T, int D, int Q0, bool BP, bool P2, int SKH = 0, int DL = 0>
+// S statically unrolled steps
+template <int T, int D, int Q0, bool BP, bool P2>
 __device__ __forceinline__ void march_interior(March<T, D>& m, const Lane& c, const Io& io,
                                                const Sio& sio, int rs, int nchunks) {
-    constexpr int S = ring_slots<T, D, SKH ? 1 : 0>();
-    if constexpr (DL > 0) {
-        // the LDS queue's first rows 4T + D .. 4T + DL - 1 (steady_step reads
-        // row n + D at step n >= 4T), in flight through the warm-up
-        for (int k = 4 * T + D; k < 4 * T + DL; ++k) {
-            const int sl = k & (DL - 1);
-            const unsigned o = (unsigned)k * sio.row_bytes;
-            row_dma(sio.p, sio.lq + sl * kStripCells, sio.lane, o);
-            row_dma(sio.r, sio.lq + (DL + sl) * kStripCells, sio.lane, o);
-        }
-    }
-    march_pairs<T, D, Q0, kPre, BP, P2, SKH>(m, c, io, rs, rs + 4 * T - 1);  // 4T is even
+    constexpr int S = ring_slots<T, D>();
+    march_pairs<T, D, Q0, kPre, BP, P2>(m, c, io, rs, rs + 4 * T - 1);  // 4T is even
     // ring in static slots: rhs row rs - 1 + j in slot j mod S; at step n = 4T
     // the paired ring holds j = 4T - 1 - k (k < 2T), the rows in flight j = 4T + k
     d2 R[S];
@@ -684,23 +564,9 @@ __device__ __forceinline__ void march_interior(March<T, D>& m, const Lane& c, co
     constexpr int P0 = (4 * T) % S;
     int r0 = rs + 4 * T;
     unsigned off = 4u * T * sio.row_bytes;
-    if constexpr (SKH > 0) {
-        // half step: the leading stages run step 4T (no residual), the
-        // trailing ones already ran step 4T - 1 in the warm-up
-        skew_step<T, D, SKH, 1 - Q0, (4 * T - 1) % S, P2, kPre, false>(m, R, c, sio, r0 - 1,
-                                                                       off - sio.row_bytes);
-        for (int k = 0; k < nchunks; ++k) {
-            skew_chunk<T, D, SKH, Q0, P0, P2>(m, R, c, sio, r0, off,
-                                              std::make_integer_sequence<int, S>{});
-            r0 += S;
-            off += (unsigned)S * sio.row_bytes;
-        }
-        return;
-    }
     for (int k = 0; k < nchunks; ++k) {
-        steady_chunk<T, D, Q0, P0, BP, P2, false, DL>(m, R, c, sio, r0, off,
-                                                      std::make_integer_sequence<int, S>{},
-                                                      4 * T + k * S);
+        steady_chunk<T, D, Q0, P0, BP, P2>(m, R, c, sio, r0, off,
+                                           std::make_integer_sequence<int, S>{});
         r0 += S;
         off += (unsigned)S * sio.row_bytes;
     }
@@ -716,19 +582,14 @@ __device__ __forceinline__ void march_interior(March<T, D>& m, const Lane& c, co
 // added to acc[].
 // STEADY = false: no static-ring path (the caller knows the block's rows are
 // not steady-able; the chained kernel's edge blocks)
-// SKH > 0: the skewed march (skew_step): every path streams one more row and
-// the leading stages' residual windows sit one row higher
-// DL > 0: the steady march's rows through the LDS queue lq (steady_step)
-template <int T, int D, bool BP, bool P2 = false, bool STEADY = true, int SKH = 0, int DL = 0>
+template <int T, int D, bool BP, bool P2 = false, bool STEADY = true>
 __device__ __forceinline__ void tb_strip2(const SweepParams& prm, const double* __restrict__ src,
                                           double* __restrict__ dst,
                                           const double* __restrict__ rhs, const int c_out,
                                           const int own_hi, const int j0, const int j1,
-                                          const int by, const int lane, double (&acc)[T],
-                                          double* lq = nullptr) {
+                                          const int by, const int lane, double (&acc)[T]) {
     constexpr int OW = kStripCells - 4 * T;
-    constexpr int SK = SKH > 0 ? 1 : 0;
-    constexpr int S = ring_slots<T, D, SK>();
+    constexpr int S = ring_slots<T, D>();
     const int ni = prm.ni, nj = prm.nj;
     const int c_ld = c_out - 2 * T;
     const long long pitch = prm.pitch;
@@ -773,7 +634,6 @@ __device__ __forceinline__ void tb_strip2(const SweepParams& prm, const double* 
     Io io{src + base, rhs + base, dst + base, pitch};
     const int rs = j0 - 2 * T;  // first streamed row
     const int rend = j1 - 1 + 2 * T;
-    m.B = d2{0.0, 0.0};
 #pragma unroll
     for (int k = 0; k < D; ++k) {
         m.Pq[k] = ldv(io.sp + (long long)(rs + k) * pitch);
@@ -797,8 +657,8 @@ __device__ __forceinline__ void tb_strip2(const SweepParams& prm, const double* 
     const bool rows_in = rs >= prm.upd_lo_j && rend <= prm.upd_hi_j &&
                          (j1 - j0) % S == 0 && j1 - j0 > 0;
     if (!cols_in) {
-        if (q1) march_pairs<T, D, 1, kEdge, false, P2, SKH>(m, c, io, rs, rend + SK);
-        else    march_pairs<T, D, 0, kEdge, false, P2, SKH>(m, c, io, rs, rend + SK);
+        if (q1) march_pairs<T, D, 1, kEdge, false, P2>(m, c, io, rs, rend);
+        else    march_pairs<T, D, 0, kEdge, false, P2>(m, c, io, rs, rend);
     } else {
         if (STEADY && rows_in) {
             // wave-uniform descriptors over the strip's 128 columns
@@ -812,19 +672,18 @@ __device__ __forceinline__ void tb_strip2(const SweepParams& prm, const double* 
                     (int)((long long)rows * pitch * 8), 0x00020000);
             };
             Sio sio;
-            sio.p = rsrc(src, rs, rend - rs + 1 + D + SK);
-            sio.r = rsrc(rhs, rs - 1, rend - rs + 1 + D + SK);
+            sio.p = rsrc(src, rs, rend - rs + 1 + D);
+            sio.r = rsrc(rhs, rs - 1, rend - rs + 1 + D);
             sio.d = rsrc(dst, j0, j1 - j0);
             sio.lane = (unsigned)lane * 16u;
             sio.st_lane = c.own_a ? (unsigned)lane * 16u : 0x40000000u;
             sio.row_bytes = (unsigned)(pitch * 8);
-            sio.lq = lq;
             const int nchunks = (j1 - j0) / S;
-            if (q1) march_interior<T, D, 1, BP, P2, SKH, DL>(m, c, io, sio, rs, nchunks);
-            else    march_interior<T, D, 0, BP, P2, SKH, DL>(m, c, io, sio, rs, nchunks);
+            if (q1) march_interior<T, D, 1, BP, P2>(m, c, io, sio, rs, nchunks);
+            else    march_interior<T, D, 0, BP, P2>(m, c, io, sio, rs, nchunks);
         } else {
-            if (q1) march_pairs<T, D, 1, kRowEdge, false, P2, SKH>(m, c, io, rs, rend + SK);
-            else    march_pairs<T, D, 0, kRowEdge, false, P2, SKH>(m, c, io, rs, rend + SK);
+            if (q1) march_pairs<T, D, 1, kRowEdge, false, P2>(m, c, io, rs, rend);
+            else    march_pairs<T, D, 0, kRowEdge, false, P2>(m, c, io, rs, rend);
         }
         if (!c.own_a) {
 #pragma unroll
@@ -882,11 +741,11 @@ __device__ __forceinline__ void block_partials(const SweepParams& prm, const dou
 }
 
 // one block (bx, by) of a pass: logical block L
-template <int T, int WAVES, int D, bool BP, bool P2, int SKH = 0, int DL = 0>
+template <int T, int WAVES, int D, bool BP, bool P2>
 __device__ __forceinline__ void tb_block(const SweepParams& prm, const double* __restrict__ src,
                                          double* __restrict__ dst, const double* __restrict__ rhs,
                                          double* __restrict__ partials, const int L,
-                                         double (*wsum)[WAVES], double* lqwg = nullptr) {
+                                         double (*wsum)[WAVES]) {
     constexpr int OW = kStripCells - 4 * T;
     const int bx = L % prm.nbx, by = L / prm.nbx;
     int j0, j1;
@@ -906,9 +765,7 @@ __device__ __forceinline__ void tb_block(const SweepParams& prm, const double* _
 #pragma unroll
     for (int t = 0; t < T; ++t) acc[t] = 0.0;
     if (c_out <= prm.ni)  // wave-uniform
-        tb_strip2<T, D, BP, P2, true, SKH, DL>(prm, src, dst, rhs, c_out, 0x7fffffff, j0, j1, by,
-                                               lane, acc,
-                                               DL ? lqwg + wave * 2 * DL * kStripCells : nullptr);
+        tb_strip2<T, D, BP, P2>(prm, src, dst, rhs, c_out, 0x7fffffff, j0, j1, by, lane, acc);
     block_partials<T, WAVES>(prm, acc, partials, L, wsum);
 }
 
@@ -1748,21 +1605,16 @@ __global__ __launch_bounds__(kLanes* WAVES, 2) void rb_tbc_kernel(
     }
 }
 
-// SK: the skewed steady march (skew_step) with the stages split at
-// skew_split<T>(); DL: the steady march's rows through an LDS queue of DL rows
-// per array and wave (steady_step)
-template <int T, int WAVES, int D, bool BP, bool P2 = false, int SK = 0, int DL = 0>
+template <int T, int WAVES, int D, bool BP, bool P2 = false>
 __global__ __launch_bounds__(kLanes* WAVES, 2) void rb_tb_kernel(
     SweepParams prm, const double* __restrict__ src, double* __restrict__ dst,
     const double* __restrict__ rhs, double* __restrict__ partials,
     const DevState* __restrict__ st, int force, int* __restrict__ queue) {
     __shared__ double wsum[T][WAVES];
     __shared__ int ticket;
-    __shared__ __attribute__((aligned(16))) double lq[DL > 0 ? WAVES * 2 * DL * kStripCells : 2];
     if (!force && st->done) return;
     for_each_block(prm, queue, &ticket, [&](int L) {
-        tb_block<T, WAVES, D, BP, P2, SK ? skew_split<T>() : 0, DL>(prm, src, dst, rhs, partials, L,
-                                                                    wsum, lq);
+        tb_block<T, WAVES, D, BP, P2>(prm, src, dst, rhs, partials, L, wsum);
     });
 }
 

@@ -16,21 +16,13 @@ int tb_out_width(int T, int variant) { return kLanes * tb_cols(variant) - 4 * T;
 
 int tb_waves(int variant) { return kTbVariants[variant].waves; }
 
-int tb_xch(int variant) { return kTbVariants[variant].xch; }
-
 int tb_ring_slots(int T, int variant) {
-    if (tb_xch(variant)) return std::max(2, 2 * T - 2);  // sor_tbx.h xslots
     const int D = kTbVariants[variant].ahead;
     if (kTbVariants[variant].hr) return hr_slots(T, D, kTbVariants[variant].skew && T >= 2 ? 1 : 0);
-    const int sk = kTbVariants[variant].skew && T >= 4 ? 1 : 0;  // sor_tb.h skew_split
-    return 2 * T + D + sk + ((D + sk) & 1);
+    return 2 * T + D + (D & 1);  // sor_tb.h ring_slots
 }
 
 int tb_nbx(int ni, int T, int variant) {
-    if (tb_xch(variant)) {  // one block column = one workgroup strip
-        const int owg = kStripCells * tb_waves(variant) - 4 * T;
-        return (ni + owg - 1) / owg;
-    }
     const int ow = tb_out_width(T, variant);
     const int strips = (ni + ow - 1) / ow;
     const int waves = tb_waves(variant);

@@ -4,7 +4,6 @@
 
 #include "sor_tb.h"
 #include "sor_tbh.h"
-#include "sor_tbx.h"
 
 #ifndef MISOR_TB_T
 #error "compile with -DMISOR_TB_T=<iterations per pass>"
@@ -24,10 +23,10 @@ static int persistent_grid(K kernel, int threads) {
     return std::max(8, per_cu * cus);
 }
 
-template <int T, int W, int D, bool B, int SK = 0, int DL = 0>
+template <int T, int W, int D, bool B>
 static int resident2() {
     static int n = 0;
-    if (n == 0) n = persistent_grid(rb_tb_kernel<T, W, D, B, false, SK, DL>, kLanes * W);
+    if (n == 0) n = persistent_grid(rb_tb_kernel<T, W, D, B, false>, kLanes * W);
     return n;
 }
 
@@ -43,41 +42,6 @@ static int residenth() {
     static int n = 0;
     if (n == 0) n = persistent_grid(rb_tbh_kernel<T, W, D, P2, SK>, kLanes * W);
     return n;
-}
-
-template <int T, int W, int D, bool P2>
-static int residentx() {
-    static int n = 0;
-    if (n == 0) n = persistent_grid(rb_tbx_kernel<T, W, D, P2>, kLanes * W);
-    return n;
-}
-
-// the exchange variant exists for T = 1 .. 10 (its LDS ring: sor_tbx.h); the
-// templates keep the other units from instantiating it
-template <int TT>
-static int residentx_of(int variant) {
-    if constexpr (TT >= 1 && TT <= 10)
-        return variant == 7   ? residentx<TT, 8, 2, false>()
-               : variant == 8 ? residentx<TT, 2, 2, false>()
-                              : residentx<TT, 4, 2, false>();
-    else
-        return 0;
-}
-
-template <int TT, class Go>
-static void launchx(const SweepParams& prm, Go&& go) {
-    if constexpr (TT >= 1 && TT <= 10) {
-        if (prm.variant == 7) {
-            if (prm.pow2) go(rb_tbx_kernel<TT, 8, 2, true>, kLanes * 8, residentx<TT, 8, 2, true>());
-            else go(rb_tbx_kernel<TT, 8, 2, false>, kLanes * 8, residentx<TT, 8, 2, false>());
-        } else if (prm.variant == 8) {
-            if (prm.pow2) go(rb_tbx_kernel<TT, 2, 2, true>, kLanes * 2, residentx<TT, 2, 2, true>());
-            else go(rb_tbx_kernel<TT, 2, 2, false>, kLanes * 2, residentx<TT, 2, 2, false>());
-        } else {
-            if (prm.pow2) go(rb_tbx_kernel<TT, 4, 2, true>, kLanes * 4, residentx<TT, 4, 2, true>());
-            else go(rb_tbx_kernel<TT, 4, 2, false>, kLanes * 4, residentx<TT, 4, 2, false>());
-        }
-    }
 }
 
 template <int T, int W, int D, int SC>
@@ -99,26 +63,6 @@ void MISOR_CAT(launch_tb_t, MISOR_TB_T)(hipStream_t s, const SweepParams& prm,
                                         const double* src, double* dst, const double* rhs,
                                         double* partials, const DevState* st, int force,
                                         int* queue) {
-    if (prm.chain && queue && prm.variant == 0) {
-        // chained pass (sor_tb.h rb_tbc_kernel): the work area gets the launch's
-        // initial segment list; as many workgroups as are resident (less the
-        // reserve), at most one per block
-        launch_chain_init(s, queue, prm.seg_tmpl, prm.nseg0, prm.seg_cap);
-        auto gc = [&](auto kernel, int resident) {
-            const int grid = std::min(prm.chain_blocks, std::max(8, resident - prm.reserve));
-            hipLaunchKernelGGL(kernel, dim3(grid), dim3(kLanes * 4), 0, s, prm, src, dst, rhs,
-                               partials, st, force, queue);
-        };
-        // main kernel, or the edge kernel (columns at a physical left / right side)
-        if (prm.chain_edge) {
-            if (prm.pow2) gc(rb_tbc_kernel<kT, 4, 2, true, 1>, resident_chain<kT, 4, 2, true, 1>());
-            else          gc(rb_tbc_kernel<kT, 4, 2, false, 1>, resident_chain<kT, 4, 2, false, 1>());
-        } else {
-            if (prm.pow2) gc(rb_tbc_kernel<kT, 4, 2, true, 0>, resident_chain<kT, 4, 2, true, 0>());
-            else          gc(rb_tbc_kernel<kT, 4, 2, false, 0>, resident_chain<kT, 4, 2, false, 0>());
-        }
-        return;
-    }
     auto go = [&](auto kernel, int threads, int resident) {
         int grid = prm.nblocks;
         if (queue) {
@@ -128,77 +72,74 @@ void MISOR_CAT(launch_tb_t, MISOR_TB_T)(hipStream_t s, const SweepParams& prm,
         hipLaunchKernelGGL(kernel, dim3(grid), dim3(threads), 0, s, prm, src, dst, rhs, partials,
                            st, force, queue);
     };
-#define TB(W, DD) go(rb_tb_kernel<kT, W, DD, false>, kLanes * W, resident2<kT, W, DD, false>())
-    // must match kTbVariants (misor_internal.h)
-    if (tb_xch(prm.variant)) {  // configure_tb keeps T within 2 .. max_t (10)
-        launchx<kT>(prm, go);
-        return;
-    }
-    switch (prm.variant) {
-    case 1: TB(8, 2); break;
-    case 2:  // 2 strips per workgroup (finer slots for small rank blocks)
-        if (prm.pow2) go(rb_tb_kernel<kT, 2, 2, false, true>, kLanes * 2, resident2<kT, 2, 2, false>());
-        else TB(2, 2);
-        break;
-    case 3: TB(1, 2); break;
-    case 4: TB(4, 3); break;
-    case kSkewTbVariant:
-        if (prm.pow2) go(rb_tb_kernel<kT, 4, 2, false, true, 1>, kLanes * 4, resident2<kT, 4, 2, false, 1>());
-        else go(rb_tb_kernel<kT, 4, 2, false, false, 1>, kLanes * 4, resident2<kT, 4, 2, false, 1>());
-        break;
-    case kHrTbVariant + 1: {  // skewed (tb_ring_slots: T = 1 runs unskewed)
+    if (prm.variant == kHrTbVariant) {  // skewed (tb_ring_slots: T = 1 runs unskewed)
         constexpr int SK_ = kT >= 2 ? 1 : 0;
         if (prm.pow2) go(rb_tbh_kernel<kT, 4, 2, true, SK_>, kLanes * 4, residenth<kT, 4, 2, true, SK_>());
         else go(rb_tbh_kernel<kT, 4, 2, false, SK_>, kLanes * 4, residenth<kT, 4, 2, false, SK_>());
-        break;
+        return;
     }
-    case kLdsTbVariant:
-        if (prm.pow2) go(rb_tb_kernel<kT, 4, 2, false, true, 0, 8>, kLanes * 4, resident2<kT, 4, 2, false, 0, 8>());
-        else go(rb_tb_kernel<kT, 4, 2, false, false, 0, 8>, kLanes * 4, resident2<kT, 4, 2, false, 0, 8>());
-        break;
-    case kLdsTbVariant + 1:
-        if (prm.pow2) go(rb_tb_kernel<kT, 4, 2, false, true, 0, 4>, kLanes * 4, resident2<kT, 4, 2, false, 0, 4>());
-        else go(rb_tb_kernel<kT, 4, 2, false, false, 0, 4>, kLanes * 4, resident2<kT, 4, 2, false, 0, 4>());
-        break;
-#define Q4(V)                                                                               \
-    case V:                                                                                 \
-        if constexpr (quad_ok<V>()) {                                                       \
-            constexpr int D_ = kTbVariants[V].ahead, SC_ = kTbVariants[V].sched;            \
-            go(rb_tb4_kernel<kT, 4, D_, SC_>, kLanes * 4, resident4<kT, 4, D_, SC_>());     \
-            break;                                                                          \
-        }                                                                                   \
-        [[fallthrough]];
-    Q4(5)
-    default:
-        if (prm.pow2) go(rb_tb_kernel<kT, 4, 2, false, true>, kLanes * 4, resident2<kT, 4, 2, false>());
-        else TB(4, 2);
-        break;
-    }
-#undef Q4
+    // the 2- and 4-column register-ring kernels: T <= kMaxT2 (configure_tb)
+    if constexpr (kT <= kMaxT2) {
+        if (prm.chain && queue && prm.variant == 0) {
+            // chained pass (sor_tb.h rb_tbc_kernel): the work area gets the launch's
+            // initial segment list; as many workgroups as are resident (less the
+            // reserve), at most one per block
+            launch_chain_init(s, queue, prm.seg_tmpl, prm.nseg0, prm.seg_cap);
+            auto gc = [&](auto kernel, int resident) {
+                const int grid = std::min(prm.chain_blocks, std::max(8, resident - prm.reserve));
+                hipLaunchKernelGGL(kernel, dim3(grid), dim3(kLanes * 4), 0, s, prm, src, dst, rhs,
+                                   partials, st, force, queue);
+            };
+            // main kernel, or the edge kernel (columns at a physical left / right side)
+            if (prm.chain_edge) {
+                if (prm.pow2) gc(rb_tbc_kernel<kT, 4, 2, true, 1>, resident_chain<kT, 4, 2, true, 1>());
+                else          gc(rb_tbc_kernel<kT, 4, 2, false, 1>, resident_chain<kT, 4, 2, false, 1>());
+            } else {
+                if (prm.pow2) gc(rb_tbc_kernel<kT, 4, 2, true, 0>, resident_chain<kT, 4, 2, true, 0>());
+                else          gc(rb_tbc_kernel<kT, 4, 2, false, 0>, resident_chain<kT, 4, 2, false, 0>());
+            }
+            return;
+        }
+#define TB(W, DD) go(rb_tb_kernel<kT, W, DD, false>, kLanes * W, resident2<kT, W, DD, false>())
+        // must match kTbVariants (misor_internal.h)
+        switch (prm.variant) {
+        case 1: TB(8, 2); break;
+        case 2:  // 2 strips per workgroup (finer slots for small rank blocks)
+            if (prm.pow2) go(rb_tb_kernel<kT, 2, 2, false, true>, kLanes * 2, resident2<kT, 2, 2, false>());
+            else TB(2, 2);
+            break;
+        case 3: TB(1, 2); break;
+        case 4: TB(4, 3); break;
+        case kQuadTbVariant: {
+            constexpr int D_ = kTbVariants[kQuadTbVariant].ahead;
+            constexpr int SC_ = kTbVariants[kQuadTbVariant].sched;
+            go(rb_tb4_kernel<kT, 4, D_, SC_>, kLanes * 4, resident4<kT, 4, D_, SC_>());
+            break;
+        }
+        default:
+            if (prm.pow2) go(rb_tb_kernel<kT, 4, 2, false, true>, kLanes * 4, resident2<kT, 4, 2, false>());
+            else TB(4, 2);
+            break;
+        }
 #undef TB
+    }
 }
 
 int MISOR_CAT(tb_resident_t, MISOR_TB_T)(int variant) {
-    switch (variant) {
-    case 1: return resident2<kT, 8, 2, false>();
-    case 2: return resident2<kT, 2, 2, false>();
-    case 3: return resident2<kT, 1, 2, false>();
-    case 4: return resident2<kT, 4, 3, false>();
-    case kSkewTbVariant: return resident2<kT, 4, 2, false, 1>();
-    case kLdsTbVariant: return resident2<kT, 4, 2, false, 0, 8>();
-    case kHrTbVariant + 1: return residenth<kT, 4, 2, false, kT >= 2 ? 1 : 0>();
-    case kLdsTbVariant + 1: return resident2<kT, 4, 2, false, 0, 4>();
-    case 6:
-    case 7: return residentx_of<kT>(variant);
-#define Q4(V)                                                                             \
-    case V:                                                                               \
-        if constexpr (quad_ok<V>())                                                       \
-            return resident4<kT, 4, kTbVariants[V].ahead, kTbVariants[V].sched>();        \
-        [[fallthrough]];
-    Q4(5)
-#undef Q4
-    default: return resident2<kT, 4, 2, false>();
+    if (variant == kHrTbVariant) return residenth<kT, 4, 2, false, kT >= 2 ? 1 : 0>();
+    if constexpr (kT <= kMaxT2) {
+        switch (variant) {
+        case 1: return resident2<kT, 8, 2, false>();
+        case 2: return resident2<kT, 2, 2, false>();
+        case 3: return resident2<kT, 1, 2, false>();
+        case 4: return resident2<kT, 4, 3, false>();
+        case kQuadTbVariant:
+            return resident4<kT, 4, kTbVariants[kQuadTbVariant].ahead,
+                             kTbVariants[kQuadTbVariant].sched>();
+        default: return resident2<kT, 4, 2, false>();
+        }
     }
+    return 0;
 }
 
 }  // namespace misor

@@ -155,8 +155,8 @@ __device__ __forceinline__ void hr_step(HrMarch<T, D>& m, d2* R, const Lane& c, 
     __builtin_amdgcn_sched_barrier(0);
 }
 
-// Step n of the skewed split-ring march (sor_tb.h skew_step's two chains on
-// the split ring): the trailing stages SKH .. T-1 run stream row r0 = rs0 + n
+// Step n of the skewed split-ring march (two independent stage chains per
+// step on the split ring): the trailing stages SKH .. T-1 run stream row r0 = rs0 + n
 // on m.B, the leading stages 0 .. SKH-1 row r0 + 1 on the streamed row; their
 // residual windows sit one row higher (stage<..., SKH>).  Register ring: rows
 // n - 2K + 2 .. n + 1 + D; the row the leading register stages read last (n -

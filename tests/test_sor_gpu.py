@@ -23,12 +23,14 @@ def set_mode(g, small):
     """small = 1: whole-solve LDS kernel where the grid fits; 0: the
     multi-block path with the default iterations per pass; "tN": the
     multi-block path with N iterations per pass (1: single-iteration sweep
-    kernel, 2..: temporally blocked kernel); "qN": the same with 4 columns per
+    kernel, 2..8: temporally blocked kernel, 9..: its split-ring variant 13,
+    the only one that runs more than 8); "qN": the same with 4 columns per
     lane (TB variant 5).  All must match the reference."""
     if isinstance(small, str):
+        T = int(small[1:])
         g.set_tuning(M.TUNE_SMALL_SOLVE, 0)
-        g.set_tuning(M.TUNE_TB_VARIANT, QUAD if small[0] == "q" else 0)
-        g.set_tuning(M.TUNE_TSTEPS, int(small[1:]))
+        g.set_tuning(M.TUNE_TB_VARIANT, QUAD if small[0] == "q" else (HRS if T > 8 else 0))
+        g.set_tuning(M.TUNE_TSTEPS, T)
     else:
         g.set_tuning(M.TUNE_SMALL_SOLVE, small)
     return g
@@ -41,6 +43,7 @@ def make_grid(ni, nj, xl=1.0, yl=1.0, omega=OMEGA, eps=EPS, itermax=1000000,
 
 
 QUAD = 5  # TB variant: 4 columns per lane (sor_tb.h, quad_interior)
+HRS = 13  # TB variant: the skewed split ring (sor_tbh.h)
 TS = ["t%d" % t for t in range(1, 11)] + ["q2", "q5", "q7", "q8"]
 PATHS = pytest.mark.parametrize("small", [1] + TS, ids=["lds"] + TS)
 
@@ -202,15 +205,13 @@ def test_tb_converges_mid_pass(T, variant):
     want = p.copy()
     eps = 3e-3
     it_ref, res_ref = orc.solve_rb(want, rhs, 1.0 / ni, 1.0 / nj, OMEGA, eps, 100000)
-    if variant == QUAD and T > 8:
+    if T > 8:  # the register-ring kernels (and the quad one) run T <= 8
         with make_grid(ni, nj, small="t8") as g:
+            g.set_tuning(M.TUNE_TB_VARIANT, variant)
             with pytest.raises(M.MisorError):
-                g.set_tuning(M.TUNE_TB_VARIANT, QUAD)
                 g.set_tuning(M.TUNE_TSTEPS, T)
         return
     with make_grid(ni, nj, eps=eps, small="t%d" % T) as g:
-        if variant == QUAD:  # the quad variant first caps T at 8
-            g.set_tuning(M.TUNE_TSTEPS, 2)
         g.set_tuning(M.TUNE_TB_VARIANT, variant)  # strips per workgroup, rows in flight
         g.set_tuning(M.TUNE_TSTEPS, T)
         g.poisson_init(1.0, 1.0, 2)

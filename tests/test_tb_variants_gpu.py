@@ -2,21 +2,15 @@
 (assignment-4/src/solver.c:179-238): p bit for bit, identical iteration
 counts, res to 1e-12.
 
-  9   skewed march (sor_tb.h skew_step): the leading half of the stages runs
-      one step ahead of the trailing half, so a step holds two independent
-      dependency chains; the leading stages' residual windows sit one row up
-      and every block streams one more row
-  10  the steady march's rows through an LDS queue 8 rows deep (sor_tb.h
-      steady_step DL: LDS DMA ahead of the registers)
-  11  the same, 4 rows deep
-  12  split rhs ring (sor_tbh.h): the rows the later stages read move from
-      registers to an LDS ring, so T = 9 .. 12 fit the registers; every
+  13  the split rhs ring (sor_tbh.h): the rhs rows the later stages read move
+      from registers to an LDS ring, so T = 9 .. 12 fit the registers; every
       block runs static-phase chunks (interior: whole warm-up chunks from a few
       rows early; sides and ragged blocks: row-tested chunks past the block's
-      end)
-  13  the split ring with the skew of 9 (sor_tbh.h hrs_step; T = 1 unskewed).
-      12 (the unskewed split ring) was measured and is no longer built:
-      configuring it fails (test_variant_12_retired)
+      end); the march in two independent stage chains per step (hrs_step;
+      T = 1 unskewed).  It runs the short pass plan of the driver's solve.
+
+Variants 6-12 were measured slower and are no longer built: configuring one
+fails (test_retired_variants), as does T > 8 on the register-ring kernels.
 
 The geometry runs interior blocks (static-ring chunks), the general march
 (physical sides, ragged last block rows), convergence inside a pass, the
@@ -33,8 +27,9 @@ import pymisor as M
 
 pytestmark = pytest.mark.gpu
 
-SKEW, LDS8, LDS4, HR, HRS = 9, 10, 11, 12, 13
-VARIANTS = [SKEW, LDS8, LDS4, HRS]  # 12: measured, then retired (not built)
+HRS = 13
+VARIANTS = [HRS]
+RETIRED = range(6, 13)
 
 
 def hr_slots(T, D=2, sk=0, most=18):
@@ -48,11 +43,9 @@ def hr_slots(T, D=2, sk=0, most=18):
 
 
 def ring(T, variant):
-    """sor_tb.h ring_slots<T, 2, skew> / sor_tbh.h Hr<T, 2, sk>::S"""
-    if variant in (HR, HRS):
-        return hr_slots(T, sk=1 if variant == HRS and T >= 2 else 0)
-    sk = 1 if T >= 4 and variant == SKEW else 0
-    return 2 * T + 2 + sk + ((2 + sk) & 1)
+    """sor_tbh.h Hr<T, 2, sk>::S"""
+    assert variant == HRS
+    return hr_slots(T, sk=1 if T >= 2 else 0)
 
 
 def solve(p, rhs, dx, dy, k, T, variant, rows=0, omega=1.7, eps=1e-300, itermax=None):
@@ -156,7 +149,7 @@ def test_variant_pow2_spacing(ni, nj, T, variant, monkeypatch):
         assert np.array_equal(got, want), (no, np.argwhere(got != want)[:5])
 
 
-@pytest.mark.parametrize("variant,T", [(v, 8) for v in VARIANTS] + [(HRS, 10), (HRS, 12)])
+@pytest.mark.parametrize("variant,T", [(HRS, 8), (HRS, 10), (HRS, 12)])
 def test_variant_default_geometry_large(variant, T):
     """8192^2, the automatic block height, the bench's problem 2 fields: one
     pass and a 20-iteration solve (T = 8: passes of 7 + 7 + 6; T = 10: 10 + 10)"""
@@ -220,7 +213,21 @@ def test_variant_decomposed(world, T, variant):
     assert np.array_equal(got, want), np.argwhere(got != want)[:5]
 
 
-def test_variant_12_retired():
+@pytest.mark.parametrize("variant", RETIRED)
+def test_retired_variants(variant):
     with M.Grid(300, 190, 1.0 / 300, 1.0 / 190, 1.7, 1e-300, 10) as g:
         with pytest.raises(M.MisorError):
-            g.set_tuning(M.TUNE_TB_VARIANT, HR)
+            g.set_tuning(M.TUNE_TB_VARIANT, variant)
+        assert g.get_tuning(M.TUNE_TB_VARIANT) == 0
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+def test_register_ring_caps_t(variant):
+    """the register-ring kernels (and the quad one) run at most 8 iterations
+    a pass; asking for more is refused and leaves the grid as it was"""
+    with M.Grid(300, 190, 1.0 / 300, 1.0 / 190, 1.7, 1e-300, 10) as g:
+        g.set_tuning(M.TUNE_TB_VARIANT, variant)
+        T0 = g.get_tuning(M.TUNE_TSTEPS)
+        with pytest.raises(M.MisorError):
+            g.set_tuning(M.TUNE_TSTEPS, 9)
+        assert g.get_tuning(M.TUNE_TSTEPS) == T0

@@ -41,10 +41,11 @@ region launches (T and the remainder steps % T) runs once before timing.
 cpu_baseline: the reference's own solveRB (assignment-4/src/solver.c:179-238,
 compiled in place by oracle/Makefile into oracle/_ref/libref.so) on one host
 core, on the bench's own 32768^2 grid (the device's fields after the timed
-solve), 3 sweeps, the solve timed alone; falls back to the C
-restatement (oracle/liboracle.so, kind "port") when _ref is absent.
-cpu_baseline_multicore: the restatement over every core of the affinity mask
-(pthreads over row bands), same grid, 10 sweeps.
+solve), 3 sweeps per run, best of 3 runs and their median,
+the solve timed alone; falls back to the C restatement
+(oracle/liboracle.so, kind "port") when _ref is absent.
+cpu_baseline_multicore: the restatement over the cores the job is granted
+(pthreads over row bands), same grid, 10 sweeps per run, best of 3 and median.
 """
 from __future__ import annotations
 
@@ -62,37 +63,54 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 PEAK_GBS = 8000.0
 BYTES_PER_LUP = 24.0
+# waves each SIMD runs of the temporally blocked kernels (launch bounds)
+WAVES_PER_SIMD = {"rb_tb_kernel": 2, "rb_tbc_kernel": 2, "rb_tbh_kernel": 2, "rb_tbhc_kernel": 2}
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(p, rhs, sweeps=3):
+def runs_summary(vals):
+    """best of the runs and their median"""
+    v = sorted(vals)
+    med = v[len(v) // 2] if len(v) % 2 else 0.5 * (v[len(v) // 2 - 1] + v[len(v) // 2])
+    return v[-1], med
+
+
+def cpu_baseline(p, rhs, sweeps=3, runs=3):
     """The reference's own solveRB (assignment-4/src/solver.c:179-238, compiled
     in place by oracle/Makefile into oracle/_ref/libref.so) on one host core,
     on the bench's own grid: the fields the GPU holds after the timed solve,
-    `sweeps` iterations, the solve timed alone (init excluded, as
-    assignment-4/src/main.c:33-35 times solve()).  Falls back to the C
-    restatement (oracle/liboracle.so, kind "port") when _ref is absent."""
+    `sweeps` iterations per run, each run from its own copy of that field, the
+    solve timed alone (init excluded, as assignment-4/src/main.c:33-35 times
+    solve()); best of `runs` and their median.  Falls back to
+    the C restatement (oracle/liboracle.so, kind "port") when _ref is absent."""
     import orc
 
     n = p.shape[1] - 2
-    if orc.have_ref():
-        kind = "reference"
-        it, sec = orc.ref_solve_rb_arrays(p, rhs, 1.0 / n, 1.0 / n, 1.9, 1e-300, sweeps)
-    else:
-        kind = "port"
-        t1 = time.perf_counter()
-        it, _ = orc.solve_rb(p, rhs, 1.0 / n, 1.0 / n, 1.9, 1e-300, sweeps)
-        sec = time.perf_counter() - t1
-    assert it == sweeps
+    kind = "reference" if orc.have_ref() else "port"
     lup = float(n) * (p.shape[0] - 2) * sweeps
-    return {"value": round(lup / sec / 1e6, 2), "unit": "MLUP/s", "cores": 1, "kind": kind,
-            "cpu": cpu_model(),
+    rates, secs = [], []
+    for _ in range(runs):
+        q = p.copy()
+        if kind == "reference":
+            it, sec = orc.ref_solve_rb_arrays(q, rhs, 1.0 / n, 1.0 / n, 1.9, 1e-300, sweeps)
+        else:
+            t1 = time.perf_counter()
+            it, _ = orc.solve_rb(q, rhs, 1.0 / n, 1.0 / n, 1.9, 1e-300, sweeps)
+            sec = time.perf_counter() - t1
+        del q
+        assert it == sweeps
+        rates.append(lup / sec / 1e6)
+        secs.append(sec)
+    best, med = runs_summary(rates)
+    return {"value": round(best, 2), "median": round(med, 2), "runs": [round(r, 2) for r in rates],
+            "unit": "MLUP/s", "cores": 1, "kind": kind, "cpu": cpu_model(),
             "sample": "solveRB on the bench's %dx%d grid (its fields after the timed solve), "
-                      "%d sweeps, one run (%.2f s solve, init excluded), 1 host core"
-                      % (n, p.shape[0] - 2, sweeps, sec)}
+                      "%d sweeps per run, best of %d runs (%s s solve each, init excluded; "
+                      "median in 'median'), 1 host core"
+                      % (n, p.shape[0] - 2, sweeps, runs, "/".join("%.2f" % t for t in secs))}
 
 
 def cpu_model():
@@ -114,11 +132,12 @@ def cgroup_cpus():
         return None
 
 
-def cpu_baseline_multicore(p, rhs, sweeps=10):
+def cpu_baseline_multicore(p, rhs, sweeps=10, runs=3):
     """solveRB on every host core the affinity mask allows (no MPI
     on the box, so pthreads over row bands, oracle/oracle_mt.c -- the
     restatement, p bit-identical to the single-core solve), on the bench's own
-    grid; one run of `sweeps` iterations"""
+    grid; `sweeps` iterations per run, each from its own copy of the field,
+    best of `runs` and their median"""
     import orc
 
     n = p.shape[1] - 2
@@ -130,18 +149,29 @@ def cpu_baseline_multicore(p, rhs, sweeps=10):
     # which it states in OMP_NUM_THREADS; 256 threads there ran at 1.8x one)
     omp = os.environ.get("OMP_NUM_THREADS", "")
     threads = max(1, min(aff, 256, quota or 256, int(omp) if omp.isdigit() and int(omp) > 0 else 256))
-    t1 = time.perf_counter()
-    it, _ = orc.solve_rb_mt(p, rhs, 1.0 / n, 1.0 / n, 1.9, 1e-300, sweeps, threads)
-    sec = time.perf_counter() - t1
-    assert it == sweeps
     lup = float(n) * (p.shape[0] - 2) * sweeps
-    return {"value": round(lup / sec / 1e6, 1), "unit": "MLUP/s", "cores": threads,
+    rates, secs = [], []
+    for _ in range(runs):
+        q = p.copy()
+        t1 = time.perf_counter()
+        it, _ = orc.solve_rb_mt(q, rhs, 1.0 / n, 1.0 / n, 1.9, 1e-300, sweeps, threads)
+        sec = time.perf_counter() - t1
+        del q
+        assert it == sweeps
+        rates.append(lup / sec / 1e6)
+        secs.append(sec)
+    best, med = runs_summary(rates)
+    return {"value": round(best, 1), "median": round(med, 1), "runs": [round(r, 1) for r in rates],
+            "unit": "MLUP/s", "cores": threads,
             "kind": "port", "cpu": cpu_model(), "nproc": os.cpu_count(), "affinity": aff,
             "cgroup_cpus": quota,
             "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
-            "sample": "solveRB on the bench's %dx%d grid, %d sweeps, one run (%.2f s), %d "
-                      "threads over row bands (oracle/oracle_mt.c)"
-                      % (n, p.shape[0] - 2, sweeps, sec, threads)}
+            "sample": "solveRB on the bench's %dx%d grid, %d sweeps per run, best of %d runs "
+                      "(%s s each; median in 'median'), %d threads over row bands "
+                      "(oracle/oracle_mt.c); the GPU box lists its whole machine in the "
+                      "affinity mask but grants this job a share of it (OMP_NUM_THREADS=%s)"
+                      % (n, p.shape[0] - 2, sweeps, runs, "/".join("%.2f" % t for t in secs),
+                         threads, os.environ.get("OMP_NUM_THREADS"))}
 
 
 def pmc_summary(size, nranks, T, chain, kernel="rb_tb_kernel"):
@@ -646,15 +676,14 @@ def main():
     fp64_ops = 9 if pow2 else 11
     fp64_floor_ms = fp64_ops * local_cells * iters_launch / (16 * 1024 * 2.4e9) * 1e3
     dims = "%dx%d" % tuple(g.loc.dims)
-    chain = (T > 1 and g.get_tuning(M.TUNE_TB_CHAIN) == 1 and g.get_tuning(M.TUNE_TB_PERSISTENT)
-             == 1 and g.get_tuning(M.TUNE_TB_VARIANT) == 0)
+    chain = T > 1 and st.get("chained", 0) == 1
     split = pass_split(args.steps, T)
     if len(split) != st["timed_passes"]:
         split = None
     # the passes' kernel: the library's pass plan picks the split-ring kernel
     # (TB variants 12 / 13, sor_tbh.h) for short capped solves (misor_api.hip)
     tbv = st.get("tb_variant", 0)
-    kernel = ("rb_tbh_kernel" if tbv in (12, 13) else
+    kernel = (("rb_tbhc_kernel" if chain else "rb_tbh_kernel") if tbv in (12, 13) else
               "rb_tbc_kernel" if chain else "rb_tb_kernel") if T > 1 else "rb_sweep_kernel"
     # traffic / VALU of the timed launches: the committed PMC summaries of each
     # pass length the split contains, weighted by its launches (null if one is
@@ -735,10 +764,20 @@ def main():
                                "per pass"}
     if pmc_files:
         out["roofline"]["traffic_source"] = pmc_files
+    # the VALU roof beside the HBM one: the algorithmic FP64 operations of the
+    # launch at the FP64 vector peak (16 lanes/clk/SIMD x 1024 SIMDs x 2.4 GHz)
+    # against the launch time
+    out["roofline"]["valu_frac"] = round(fp64_floor_ms / kern_ms, 4) if kern_ms > 0 else None
     if valu:
         # what actually bounds the temporally blocked kernel: VALU issue
-        # (SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES per wave, 2 waves per SIMD)
+        # (SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES per wave, x waves per SIMD); a
+        # launch whose SIMDs issue VALU work >= 85% of their cycles is VALU-bound
+        wps = WAVES_PER_SIMD.get(kernel, 2)
+        valu["waves_per_simd"] = wps
+        valu["valu_busy_per_simd"] = round(valu["valu_busy_per_wave"] * wps, 3)
         out["roofline"]["valu"] = valu
+        if valu["valu_busy_per_simd"] >= 0.85:
+            out["roofline"]["bound"] = "valu"
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # the bench's own grid: the fields the device holds after the timed solve
         hp, hrhs = g.download(M.P), g.download(M.RHS)

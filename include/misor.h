@@ -117,6 +117,8 @@ typedef struct {
     long long halos;        /* exchanges covered by halo_ms */
     double allreduce_ms;    /* total device time of the residual all-reduces */
     long long allreduces;   /* all-reduces covered by allreduce_ms */
+    int chained;            /* 1: the last multi-block solve's passes were chained runs
+                             * (sor_tb.h rb_tbc_kernel / sor_tbh.h rb_tbhc_kernel) */
 } misor_stats;
 
 const char* misor_last_error(void);

@@ -144,6 +144,7 @@ struct misor_grid {
     int tsteps = kDefaultTsteps;  // requested T (1: single-iteration kernel)
     bool tsteps_set = false;      // T requested by MISOR_TUNE_TSTEPS (else the default rule)
     bool short_plan = false;      // capped solves may run as kShortT-iteration split-ring passes
+    bool short_all = false;       // ... every solve of more than kDefaultTsteps iterations
     SweepParams tp{};             // its launch geometry (for T = tsteps)
     int tb_nparts = 0;
     int tb_rows_req = 0;          // MISOR_TUNE_TB_ROWS (0: automatic)
@@ -166,7 +167,7 @@ struct misor_grid {
     struct ChainPlan {
         ChainList main, edge;
         bool built = false;
-    } chain_plan[kMaxT + 1][3];
+    } chain_plan[2][kMaxT + 1][3];  // [the default variant's / the split ring's][T][part]
     int* tb_work[4] = {nullptr, nullptr, nullptr, nullptr};  // main / edge x parts 0-1 / 2
     long long tb_work_bytes[4] = {0, 0, 0, 0};
     hipStream_t xstream[2] = {nullptr, nullptr};  // edge kernels (parts 0-1 / 2)
@@ -287,11 +288,12 @@ void misor_destroy(misor_grid* g) {
         if (f) (void)hipFree(f);
     (void)hipFree(g->partials);
     (void)hipFree(g->tb_queue);
-    for (auto& row : g->chain_plan)
-        for (auto& pl : row) {
-            (void)hipFree(pl.main.tmpl);
-            (void)hipFree(pl.edge.tmpl);
-        }
+    for (auto& v : g->chain_plan)
+        for (auto& row : v)
+            for (auto& pl : row) {
+                (void)hipFree(pl.main.tmpl);
+                (void)hipFree(pl.edge.tmpl);
+            }
     for (int* w : g->tb_work) (void)hipFree(w);
     for (int k = 0; k < 2; ++k) {
         if (g->xstream[k]) {
@@ -652,9 +654,14 @@ static int pick_tb_rows(int ni, int nj, int T, int variant) {
 // dropped.  An explicit request gives uniform blocks of that height, the last
 // row taking the rest.
 static bool chain_on(const misor_grid* g, int variant) {
+    if (!g->tb_persistent) return false;
+    // the split-ring passes are always chained runs (the warm-up rows they
+    // save are VALU work of a VALU-bound pass, sor_tbh.h rb_tbhc_kernel; an
+    // unchained form measured 2-15% slower, profiles/r05_hrsweep*.txt)
+    if (variant == kHrTbVariant) return true;
     const bool want = g->tb_chain > 0 ||
                       (g->tb_chain < 0 && (long long)g->loc.ni * g->loc.nj < kChainCells);
-    return want && g->tb_persistent && variant == kDefaultTbVariant;
+    return want && variant == kDefaultTbVariant;
 }
 
 // T when none was requested: 8 on large local blocks; on small ones 8 with
@@ -680,7 +687,9 @@ static void tb_geometry(const misor_grid* g, int T, SweepParams& tp) {
         // work stealing), long runs; every block row but the last a multiple
         // of the ring (MISOR_TB_CHAIN_RINGS: tuning experiments)
         const char* er = getenv("MISOR_TB_CHAIN_RINGS");
-        const int rings = er && atoi(er) > 0 ? atoi(er) : kChainRingsPerBlock;
+        const int rings = er && atoi(er) > 0 ? atoi(er)
+                          : tp.variant == kHrTbVariant ? kHrChainRingsPerBlock
+                                                       : kChainRingsPerBlock;
         int h = req > 0 ? S * std::max(1, (req + S / 2) / S) : rings * S;
         if (h > nj) h = nj;
         tp.rows_per_block = h;
@@ -727,19 +736,24 @@ static void tb_geometry(const misor_grid* g, int T, SweepParams& tp) {
 // ...): the XCD queues deal contiguous runs of it, so neighbouring columns --
 // whose strips share 4T columns -- march side by side on one XCD.
 static void drop_chain_plans(misor_grid* g) {
-    for (auto& row : g->chain_plan)
-        for (auto& pl : row) {
-            (void)hipFree(pl.main.tmpl);
-            (void)hipFree(pl.edge.tmpl);
-            pl = misor_grid::ChainPlan{};
-        }
+    for (auto& v : g->chain_plan)
+        for (auto& row : v)
+            for (auto& pl : row) {
+                (void)hipFree(pl.main.tmpl);
+                (void)hipFree(pl.edge.tmpl);
+                pl = misor_grid::ChainPlan{};
+            }
 }
 
-static int chain_plan(misor_grid* g, int Tp, int part, const misor_grid::ChainPlan** out) {
-    auto& pl = g->chain_plan[Tp][part];
+// (variant: the configured one or the split ring of the short plan; the plan
+// follows that variant's geometry: strip width, ring, block height)
+static int chain_plan(misor_grid* g, int variant, int Tp, int part,
+                      const misor_grid::ChainPlan** out) {
+    auto& pl = g->chain_plan[variant == kHrTbVariant ? 1 : 0][Tp][part];
     *out = &pl;
     if (pl.built) return MISOR_OK;
     SweepParams tp = g->tp;
+    tp.variant = variant;
     tb_geometry(g, Tp, tp);
     const int W = tb_waves(tp.variant), OW = tb_out_width(Tp, tp.variant);
     const int S = tb_ring_slots(Tp, tp.variant);
@@ -782,7 +796,9 @@ static int chain_plan(misor_grid* g, int Tp, int part, const misor_grid::ChainPl
     // The segments are cut so that each costs about (total / resident
     // workgroups): every workgroup starts one at once and they end together.
     const char* ec = getenv("MISOR_CHAIN_EDGE_COST");
-    const double E = ec && atof(ec) > 0 ? atof(ec) : kChainEdgeCost;
+    const double E = ec && atof(ec) > 0 ? atof(ec)
+                     : variant == kHrTbVariant ? kHrChainEdgeCost
+                                               : kChainEdgeCost;
     const int H = tp.rows_per_block;
     std::vector<unsigned long long> singles;
     double cost = 0;
@@ -874,6 +890,8 @@ static int configure_tb(misor_grid* g, int T, int variant, int rows) {
     if (tb_max_t(variant) == 0)  // measured slower, then not built
         return fail(MISOR_EINVAL, "TB variant %d is retired (measured slower; not built)",
                     variant);
+    if (variant == kHrTbVariant && !g->tb_persistent)
+        return fail(MISOR_EINVAL, "TB variant %d runs persistent chained passes only", variant);
     if (T > tb_max_t(variant))
         return fail(MISOR_EINVAL, "TB variant %d runs at most %d iterations per pass", variant,
                     tb_max_t(variant));
@@ -907,13 +925,26 @@ static int configure_tb(misor_grid* g, int T, int variant, int rows) {
         const char* e = getenv("MISOR_SHORT_PLAN");
         return !(e && e[0] == '0');
     }();
-    // (decomposed: on blocks of >= kShortDistCells, the two-GPU split of the
-    // bench grid, where a 10-iteration pass still costs ~1.4 T = 7 passes --
-    // 8.2 against 8.5 ms for 20 iterations, profiles/r04_blocks_splitring.txt;
-    // at 4 and 8 ranks it does not pay)
+    // Where (round 5, the chained split ring; profiles/r05_plan_ab*.txt, wall
+    // ms per iteration of 20- and 100-iteration solves against the T = 8 plan):
+    //  - blocks of [2^26, 2^28) cells, where the T = 8 passes are chained
+    //    (the 8-GPU rank block 8192 x 16384: 0.106 vs 0.123, in the pipelined
+    //    loop 0.122 vs 0.142): every solve of more than 8 iterations;
+    //  - a single rank of >= 2^29 cells (the 32768^2 bench grid: 0.676 vs 0.682
+    //    at 100 iterations, 20 iterations in 2 passes instead of 3): the same;
+    //  - a single rank of 2^28 cells, and decomposed blocks of >= 2^29 (the
+    //    two-GPU split of the bench grid): only where it saves passes, the
+    //    rule in solve_rb_from (at 100 iterations the two plans are within 1-3%);
+    //  - decomposed 2^28-cell blocks (the 4-GPU split): never (0.212 vs 0.219).
     const long long cells = (long long)g->loc.ni * g->loc.nj;
+    const bool small_chain = cells >= kHrAllCells && cells < kTsteps8Cells &&
+                             chain_on(g, variant);
+    g->short_all = small_chain || (!g->dist && cells >= 2 * kTsteps8Cells);
     g->short_plan = short_env && variant == kDefaultTbVariant && !g->tsteps_set &&
-                    !chain_on(g, variant) && cells >= (g->dist ? kShortDistCells : kTsteps8Cells);
+                    g->tb_persistent &&
+                    (g->short_all ||
+                     (!chain_on(g, variant) &&
+                      cells >= (g->dist ? kShortDistCells : kTsteps8Cells)));
     if (g->short_plan) {
         for (int Tp = 1; Tp <= kShortT; ++Tp) {
             SweepParams q = tp;
@@ -927,7 +958,8 @@ static int configure_tb(misor_grid* g, int T, int variant, int rows) {
         }
     }
     drop_chain_plans(g);  // geometry changed: rebuilt on first use
-    if (chain_on(g, variant)) {
+    const bool short_chain = g->short_plan && chain_on(g, kShortTbVariant);
+    if (chain_on(g, variant) || short_chain) {
         for (int k = 0; k < 2; ++k) {  // the edge kernels' streams
             if (g->xstream[k]) continue;
             int lo = 0, hi = 0;
@@ -944,6 +976,12 @@ static int configure_tb(misor_grid* g, int T, int variant, int rows) {
         long long most = 1;
         for (int Tp = 1; Tp <= std::max(2, Te); ++Tp) {
             SweepParams q = tp;
+            tb_geometry(g, Tp, q);
+            most = std::max(most, (long long)q.nblocks);
+        }
+        for (int Tp = 1; short_chain && Tp <= kShortT; ++Tp) {
+            SweepParams q = tp;
+            q.variant = kShortTbVariant;
             tb_geometry(g, Tp, q);
             most = std::max(most, (long long)q.nblocks);
         }
@@ -1708,10 +1746,14 @@ static int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* 
     // (profiles/r04_ab_splitring.txt): where its passes times 1.4 undercut the
     // default's pass count -- 9-10 and 17-20 iterations (the driver's
     // 20-iteration solve: 2 passes instead of 7 + 7 + 6) -- the solve takes it.
+    // With the chained split ring (round 5) a T = 10 pass costs about a T = 8
+    // one on the blocks where configure_tb sets short_all, so there every solve
+    // of more than 8 iterations takes it.
     const int todo0 = itermax - it0;
     const bool shortp = g->short_plan && effective_tsteps(g) == kDefaultTsteps &&
-                        7LL * ((todo0 + kShortT - 1) / kShortT) <
-                            5LL * ((todo0 + kDefaultTsteps - 1) / kDefaultTsteps);
+                        (g->short_all ? todo0 > kDefaultTsteps
+                                      : 7LL * ((todo0 + kShortT - 1) / kShortT) <
+                                            5LL * ((todo0 + kDefaultTsteps - 1) / kDefaultTsteps));
     const int T = shortp ? kShortT : effective_tsteps(g);
     SweepParams tpl = g->tp;  // the plan's geometry
     if (shortp) {
@@ -1742,7 +1784,7 @@ static int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* 
             if (Tp != T) tb_geometry(g, Tp, tp);  // narrower cone: wider strips
             if (tp.chain) {  // chained runs, work stealing (parts 0 / 1 and 2 concurrently)
                 const misor_grid::ChainPlan* pl = nullptr;
-                int rc = chain_plan(g, Tp, part, &pl);
+                int rc = chain_plan(g, tp.variant, Tp, part, &pl);
                 if (rc) return rc;
                 const int k = part == 2 ? 1 : 0;
                 tp.seg_cap = kChainSegCap;
@@ -2050,6 +2092,7 @@ static int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* 
     g->stats.sweeps += it - it0;
     g->stats.iters_per_pass = T;
     g->stats.tb_variant = T == 1 ? -1 : tpl.variant;
+    g->stats.chained = T > 1 && tpl.chain ? 1 : 0;
     // stopped before an iteration near the threshold: the exact tail goes on
     // from it (misor_solve_rb_n)
     if (g->st_host->near) *hand_off = true;
@@ -2333,9 +2376,13 @@ int misor_set_tuning(misor_grid* g, int key, int value) {
     }
     case MISOR_TUNE_TB_VARIANT: return configure_tb(g, g->tsteps, value, g->tb_rows_req);
     case MISOR_TUNE_TB_ROWS: return configure_tb(g, g->tsteps, g->tp.variant, value);
-    case MISOR_TUNE_TB_PERSISTENT:
+    case MISOR_TUNE_TB_PERSISTENT: {
+        const bool prev = g->tb_persistent;  // (a rejected request changes nothing)
         g->tb_persistent = value != 0;
-        return configure_tb(g, g->tsteps, g->tp.variant, g->tb_rows_req);
+        const int rc = configure_tb(g, g->tsteps, g->tp.variant, g->tb_rows_req);
+        if (rc) g->tb_persistent = prev;
+        return rc;
+    }
     case MISOR_TUNE_TB_CHAIN:
         // without an explicit T request the default rule re-picks T (chained
         // small blocks run T = 8, unchained ones T = 7)

@@ -32,7 +32,7 @@ namespace misor {
 // Padding cells are zero and never feed an interior result.
 // ---------------------------------------------------------------------------
 constexpr int kXOff = 15;
-constexpr int kMaxT = 12;                // iterations per temporally blocked pass (max)
+constexpr int kMaxT = 10;                // iterations per temporally blocked pass (max)
 constexpr int kYOff = 2 * kMaxT + 16;
 constexpr int kLanes = 64;                 // wavefront
 constexpr int kStripCells = 2 * kLanes;    // 128 columns per wave (2 per lane)
@@ -62,34 +62,31 @@ int sweep_waves(int variant);
 // temporally blocked sweep (sor_tb.hip): strips per workgroup, rows in flight
 // (x-neighbour shifts through ds_bpermute instead of DPP -- the kernel's BP
 // template flag -- measured 5% slower: profiles/r02_tune_bperm.txt)
-// columns per lane: 2 (128-column strips, rhs ring in registers, 2 waves per
-// SIMD) or 4 (256-column strips, rhs ring in LDS, 1 wave per SIMD; T <= kMaxQuadT)
-// quad variants: sched = how far the compiler may interleave steps (sor_tb.h
-// qstep), max_t = the largest T whose LDS ring fits (2T + D (+1) rows of 2 KB per wave)
+// 128-column strips (2 columns per lane), 2 waves per SIMD.
 // skew: the split-ring march in two independent stage chains per step (sor_tbh.h
 // hrs_step); hr: the split rhs ring, registers + LDS (sor_tbh.h)
 // max_t = 0: retired -- measured slower and no longer built (DESIGN.md section 4:
-// 6-8 strips exchanging edge columns through LDS, 9 the skewed register-ring
-// march, 10/11 an LDS row queue, 12 the unskewed split ring); configuring one
-// fails.  The 2-column register-ring kernels run T <= kMaxT2 (above that their
-// rhs ring spills); only the split ring (13) runs T up to kMaxT.
+// 1 / 3 eight / one strips per workgroup, 4 three rows in flight, 5 four
+// columns per lane at one wave per SIMD, 6-8 strips exchanging edge columns
+// through LDS, 9 the skewed register-ring march, 10/11 an LDS row queue, 12 the
+// unskewed split ring); configuring one fails.  The register-ring kernels run
+// T <= kMaxT2 (above that their rhs ring spills); the split ring (13) runs T up
+// to kMaxT.
 constexpr int kMaxT2 = 8;
 struct TbVariant {
-    int waves, ahead, cols, sched, max_t, skew, hr;
+    int waves, ahead, max_t, skew, hr;
 };
 constexpr TbVariant kTbVariants[] = {
-    {4, 2, 2, 0, kMaxT2}, {8, 2, 2, 0, kMaxT2}, {2, 2, 2, 0, kMaxT2}, {1, 2, 2, 0, kMaxT2},
-    {4, 3, 2, 0, kMaxT2}, {4, 2, 4, 0, 8},
-    {4, 2, 2, 0, 0},      {4, 2, 2, 0, 0},      {4, 2, 2, 0, 0},      {4, 2, 2, 0, 0},
-    {4, 2, 2, 0, 0},      {4, 2, 2, 0, 0},      {4, 2, 2, 0, 0},
-    {4, 2, 2, 0, kMaxT, 1, 1}};
+    {4, 2, kMaxT2}, {4, 2, 0}, {2, 2, kMaxT2}, {4, 2, 0}, {4, 2, 0}, {4, 2, 0}, {4, 2, 0},
+    {4, 2, 0},      {4, 2, 0}, {4, 2, 0},      {4, 2, 0}, {4, 2, 0}, {4, 2, 0},
+    {4, 2, kMaxT, 1, 1}};
 constexpr int kNumTbVariants = 14;
 constexpr int kHrTbVariant = 13;   // the skewed split ring (T = 1 unskewed)
 // the short plan of capped solves (misor_api.hip solve_rb_from)
 constexpr int kShortTbVariant = kHrTbVariant;
 constexpr int kShortT = 10;
 constexpr long long kShortDistCells = 1LL << 29;  // decomposed: local blocks at least this big
-constexpr int kQuadTbVariant = 5;
+constexpr long long kHrAllCells = 1LL << 26;      // chained blocks from here: every solve > 8
 // iterations per pass: 8 on large local blocks, 7 below kTsteps8Cells cells
 // (32768^2 0.744 vs 0.785 ms/iteration, profiles/r02_tune_t789.txt; one rank's
 // 8192 x 16384 block at 8 GPUs 0.118-0.122 at T = 7 vs 0.125 at T = 8,
@@ -128,7 +125,6 @@ __host__ __device__ constexpr int hr_slots(int T, int D, int sk = 0) {
 int tb_ring_slots(int T, int variant);
 // workgroups of a persistent pass resident on the device at once
 int tb_resident(int T, int variant);
-int tb_cols(int variant);
 int tb_max_t(int variant);
 int tb_out_width(int T, int variant);           // owned columns of one wave's strip
 int tb_nbx(int ni, int T, int variant);         // block columns of a pass of T iterations
@@ -194,6 +190,12 @@ constexpr unsigned long long kChainMask = (1ull << kChainBits) - 1;
 constexpr int kChainHead = 16;
 constexpr int kChainSegCap = 4096;       // dynamic slots per launch
 constexpr int kChainRingsPerBlock = 4;   // block height of a chained pass, in ring lengths
+// the chained split-ring pass (sor_tbh.h rb_tbhc_kernel): blocks of 8 ring
+// lengths (144 rows at T = 10), a block of a column at a physical left / right
+// side costing ~2.5 others (its strip's kSteadyEdge chunks run ~1.8x a steady
+// strip's; profiles/r05_hrsweep2_*.txt)
+constexpr int kHrChainRingsPerBlock = 8;
+constexpr double kHrChainEdgeCost = 2.5;
 // chained passes by default on local blocks below this many cells: there the
 // unchained blocks are short and their 4T warm-up rows cost most (one 8-GPU
 // rank's 8192 x 16384 of the 32768^2 bench: 0.106 vs 0.110-0.118 ms per
@@ -248,7 +250,6 @@ void launch_tb(hipStream_t s, int T, const SweepParams& prm, const double* src, 
     int tb_resident_t##N(int variant);
 MISOR_DECL_TB(1) MISOR_DECL_TB(2) MISOR_DECL_TB(3) MISOR_DECL_TB(4) MISOR_DECL_TB(5)
 MISOR_DECL_TB(6) MISOR_DECL_TB(7) MISOR_DECL_TB(8) MISOR_DECL_TB(9) MISOR_DECL_TB(10)
-MISOR_DECL_TB(11) MISOR_DECL_TB(12)
 #undef MISOR_DECL_TB
 // lexicographic Gauss-Seidel SOR, whole solve in one workgroup (lex_kernels.hip)
 void launch_solve_lex(hipStream_t s, double* p, const double* rhs, int ni, int nj,

@@ -514,9 +514,38 @@ __device__ __forceinline__ void upd2(const Lane& c, const Upd& a, const Upd& b, 
     nb = b.cc - pb;
 }
 
-// stage ta of chain a (colour QA) and stage tb of chain b (colour QB), kSteady,
-// interleaved: red of both, then black of both.  Same arithmetic as stage().
-template <int QA, int QB, bool P2>
+// the new value of colour Q's cell of a row (EM: only in an updated column,
+// stage()'s kSteadyEdge lane masks), and its residual (EM: an owned column)
+template <int Q, bool EM>
+__device__ __forceinline__ void put_new(const Lane& c, d2& row, double v) {
+    if (Q == 0) row.x = (!EM || c.up_a) ? v : row.x;
+    else        row.y = (!EM || c.up_b) ? v : row.y;
+}
+template <int Q, bool EM>
+__device__ __forceinline__ void tally_q(const Lane& c, TallyAcc& acc, double r) {
+    if (!EM) {
+        tally_steady(acc, r);
+    } else {
+        const double rm = (Q == 0 ? c.own_a : c.own_b) ? r : 0.0;  // select: NaN-safe
+        acc = __builtin_fma(rm, rm, acc);
+    }
+}
+// EM: the ghost column copies of a finished row at a physical left / right
+// side (stage()'s EDGE block, in its order)
+template <bool EM>
+__device__ __forceinline__ void ghost_cols(const Lane& c, d2& F) {
+    if (!EM) return;
+    const double f1 = from_right(F.x);  // column ib+1 (lane l+1's ia)
+    const double fl = from_left(F.y);   // column ia-1 (lane l-1's ib)
+    if (c.fix0_b) F.y = f1;
+    if (c.fixr_a) F.x = fl;
+    if (c.fixr_b) F.y = F.x;
+}
+
+// stage ta of chain a (colour QA) and stage tb of chain b (colour QB), kSteady
+// (EM: kSteadyEdge), interleaved: red of both, then black of both.  Same
+// arithmetic as stage().
+template <int QA, int QB, bool P2, bool EM = false>
 __device__ __forceinline__ void stage_pair(const Lane& c, d2& InA, d2& A_a, d2& M1_a, d2& M2_a,
                                            d2 Ra_a, d2 Rb_a, TallyAcc& acc_a, d2& InB, d2& A_b,
                                            d2& M1_b, d2& M2_b, d2 Ra_b, d2 Rb_b,
@@ -528,18 +557,20 @@ __device__ __forceinline__ void stage_pair(const Lane& c, d2& InA, d2& A_a, d2& 
     upd2<P2>(c, upd_ops<QA, true>(A_a, InA, M1_a, Ra_a, fl, fr),
              upd_ops<QB, true>(A_b, InB, M1_b, Ra_b, fl, fr), na, nb, ra, rb);
     d2 Mr_a = A_a, Mr_b = A_b;
-    if (QA == 0) Mr_a.x = na; else Mr_a.y = na;
-    if (QB == 0) Mr_b.x = nb; else Mr_b.y = nb;
-    tally_steady(acc_a, ra);
-    tally_steady(acc_b, rb);
+    put_new<QA, EM>(c, Mr_a, na);
+    put_new<QB, EM>(c, Mr_b, nb);
+    tally_q<QA, EM>(c, acc_a, ra);
+    tally_q<QB, EM>(c, acc_b, rb);
     // black: row rin-2 (M1), reading the new red row above
     upd2<P2>(c, upd_ops<QA, false>(M1_a, Mr_a, M2_a, Rb_a, fl, fr),
              upd_ops<QB, false>(M1_b, Mr_b, M2_b, Rb_b, fl, fr), na, nb, ra, rb);
     d2 F_a = M1_a, F_b = M1_b;
-    if (QA == 0) F_a.x = na; else F_a.y = na;
-    if (QB == 0) F_b.x = nb; else F_b.y = nb;
-    tally_steady(acc_a, ra);
-    tally_steady(acc_b, rb);
+    put_new<QA, EM>(c, F_a, na);
+    put_new<QB, EM>(c, F_b, nb);
+    tally_q<QA, EM>(c, acc_a, ra);
+    tally_q<QB, EM>(c, acc_b, rb);
+    ghost_cols<EM>(c, F_a);
+    ghost_cols<EM>(c, F_b);
     M2_a = F_a; M1_a = Mr_a; A_a = InA; InA = F_a;
     M2_b = F_b; M1_b = Mr_b; A_b = InB; InB = F_b;
 }
@@ -769,312 +800,6 @@ __device__ __forceinline__ void tb_block(const SweepParams& prm, const double* _
     block_partials<T, WAVES>(prm, acc, partials, L, wsum);
 }
 
-// ---------------------------------------------------------------------------
-// Four columns per lane (TbVariant::cols == 4).
-//
-// The 2-column strip above spends, per owned update, 1/(1 - 4T/128) of its
-// arithmetic on its 2T-column halo (1.33x at T = 8) and one 64-bit DPP shift
-// (two v_mov_dpp) per update: the kernel issues VALU work on ~94% of its
-// cycles (profiles/r02_pmc_tb8_32768.json), so these instructions ARE its
-// time.  Here a lane holds 4 consecutive columns c0..c3 (c0 odd): a 256-column
-// strip owns 256 - 4T of them, and of the two cells of a colour in a lane's
-// row only one has an x-neighbour in another lane, so a stage needs one DPP
-// shift per two updates.  The registers that buys -- 4 rows of 4 doubles per
-// stage -- leave no room for the rhs ring, which moves to LDS: each rhs row
-// comes in by LDS DMA (buffer_load_dwordx4 ... lds, no VGPRs), in two
-// lane-linear halves (c0 c1 | c2 c3), and a stage reads the 2 cells of a
-// colour with one ds_read2 per row.  One wave per SIMD (the ring is 16-18
-// rows x 2 KB per wave).
-//
-// The DMA writes LDS without a register dependency the compiler could track,
-// so the steady step waits for it explicitly: every step issues exactly 6
-// VMEM operations (2 p loads, 2 stores -- dropped ones in warm-up steps --, 2
-// rhs DMAs, in that order), so before stage 0 reads row n (DMA'd D steps ago)
-// `s_waitcnt vmcnt(6 (D-1) + 2)` leaves only the operations issued after it.
-// Blocks at a physical side (or of a height the ring does not divide) run as
-// 128-column strips clipped to the quad strip's own columns (tb_strip2).
-// ---------------------------------------------------------------------------
-typedef double d4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) void lds_void_t;
-
-constexpr int kQuadCells = 4 * kLanes;  // 256 columns per strip
-
-// One stage on 4 columns (x, y, z, w = c0..c3), the arithmetic of stage().
-// Q = 0: the red cells of row rr = rin-1 are c0, c2, and so are the black
-// cells of row rb = rin-2; Q = 1: c1, c3.  Rr / Rb: rhs of those cells.  The
-// residual of c0 / c1 goes to al, of c2 / c3 to ah (a lane's two halves can
-// differ in ownership when T is odd).
-template <int Q>
-__device__ __forceinline__ d4 qstage(double idx2, double idy2, double coef, d4 In, d4& A, d4& M1,
-                                     d4& M2, d2 Rr, d2 Rb, double& al, double& ah) {
-    d4 Mr = A;
-    d4 F = M1;
-    if (Q == 0) {
-        const double W0 = from_left(A.w);  // column c0 - 1: lane l-1's c3
-        {
-            const double cc = A.x;
-            const double r = Rr.x - ((m2c(A.y, cc) + W0) * idx2 + (m2c(In.x, cc) + M1.x) * idy2);
-            Mr.x = cc - coef * r;
-            al = __builtin_fma(r, r, al);
-        }
-        {
-            const double cc = A.z;
-            const double r = Rr.y - ((m2c(A.w, cc) + A.y) * idx2 + (m2c(In.z, cc) + M1.z) * idy2);
-            Mr.z = cc - coef * r;
-            ah = __builtin_fma(r, r, ah);
-        }
-        const double Wb = from_left(M1.w);
-        {
-            const double cc = M1.x;
-            const double r = Rb.x - ((m2c(M1.y, cc) + Wb) * idx2 + (m2c(Mr.x, cc) + M2.x) * idy2);
-            F.x = cc - coef * r;
-            al = __builtin_fma(r, r, al);
-        }
-        {
-            const double cc = M1.z;
-            const double r = Rb.y - ((m2c(M1.w, cc) + M1.y) * idx2 + (m2c(Mr.z, cc) + M2.z) * idy2);
-            F.z = cc - coef * r;
-            ah = __builtin_fma(r, r, ah);
-        }
-    } else {
-        const double E3 = from_right(A.x);  // column c3 + 1: lane l+1's c0
-        {
-            const double cc = A.y;
-            const double r = Rr.x - ((m2c(A.z, cc) + A.x) * idx2 + (m2c(In.y, cc) + M1.y) * idy2);
-            Mr.y = cc - coef * r;
-            al = __builtin_fma(r, r, al);
-        }
-        {
-            const double cc = A.w;
-            const double r = Rr.y - ((m2c(E3, cc) + A.z) * idx2 + (m2c(In.w, cc) + M1.w) * idy2);
-            Mr.w = cc - coef * r;
-            ah = __builtin_fma(r, r, ah);
-        }
-        const double Eb = from_right(M1.x);
-        {
-            const double cc = M1.y;
-            const double r = Rb.x - ((m2c(M1.z, cc) + M1.x) * idx2 + (m2c(Mr.y, cc) + M2.y) * idy2);
-            F.y = cc - coef * r;
-            al = __builtin_fma(r, r, al);
-        }
-        {
-            const double cc = M1.w;
-            const double r = Rb.y - ((m2c(Eb, cc) + M1.z) * idx2 + (m2c(Mr.w, cc) + M2.w) * idy2);
-            F.w = cc - coef * r;
-            ah = __builtin_fma(r, r, ah);
-        }
-    }
-    M2 = F;
-    M1 = Mr;
-    A = In;
-    return F;
-}
-
-// one 16-byte-per-lane LDS DMA (lane l's 16 bytes land at lds + 16 l); a
-// plain function: the builtin exists only for the device target
-__device__ __forceinline__ void qdma(__amdgpu_buffer_rsrc_t r, double* lds, unsigned voff,
-                                     unsigned soff) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_t*)lds, 16, voff, soff, 0, 0);
-}
-
-template <int T, int D>
-struct QMarch {
-    d4 A[T], M1[T], M2[T];
-    d4 Pq[D];          // p rows in flight
-    double al[T], ah[T];
-    d2 keep[2];
-};
-
-struct QIo {
-    __amdgpu_buffer_rsrc_t p, r, d;  // p rows from rs, rhs rows from rs - 1, dst rows from j0
-    unsigned lane;                   // lane * 32
-    unsigned st_lo, st_hi;           // store offsets of the halves (2^30: not stored)
-    unsigned row_bytes;
-    int l2;                          // 2 * lane
-    double idx2, idy2, coef;
-};
-
-// step n of a quad march: stream old row rs + n in, push it through the T
-// stages, store the row the last stage finished (WARM: dropped stores, no
-// residual kept), bring rhs row n + D into the ring.  ph = n mod S (a
-// constant in the steady chunks).
-// SCHED: where the scheduler may not move code across -- 0: every step
-// boundary, 1: every other one, 2: none inside a chunk
-template <int T, int D, int Q, bool WARM, int SCHED = 0, bool ODD = false>
-__device__ __forceinline__ void qstep(QMarch<T, D>& m, double* ringw, const QIo& io, int ph,
-                                      unsigned off_n) {
-    constexpr int S = ring_slots<T, D>();
-    const unsigned ld = off_n + (unsigned)D * io.row_bytes;
-    const d2 p0 = bload(io.p, io.lane, ld);
-    const d2 p1 = bload(io.p, io.lane + 16u, ld);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(6 * (D - 1) + 2) : "memory");
-    d4 v = m.Pq[0];
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-        const int sr = (ph - 2 * t + 4 * S) % S;
-        const int sb = (ph - 2 * t - 1 + 4 * S) % S;
-        const double* Lr = ringw + sr * kQuadCells + io.l2 + Q;
-        const double* Lb = ringw + sb * kQuadCells + io.l2 + Q;
-        const d2 Rr{Lr[0], Lr[kQuadCells / 2]};
-        const d2 Rb{Lb[0], Lb[kQuadCells / 2]};
-        v = qstage<Q>(io.idx2, io.idy2, io.coef, v, m.A[t], m.M1[t], m.M2[t], Rr, Rb, m.al[t],
-                      m.ah[t]);
-    }
-    // row rs + n - 2T = j0 + (n - 4T); the dst descriptor starts at row j0
-    const unsigned so = WARM ? 0u : off_n - 4u * T * io.row_bytes;
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, d2{v.x, v.y}), io.d,
-                                           WARM ? 0x40000000u : io.st_lo, so, 2);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, d2{v.z, v.w}), io.d,
-                                           WARM ? 0x40000000u : io.st_hi, so, 2);
-    const int sn = (ph + D) % S;
-    qdma(io.r, ringw + sn * kQuadCells, io.lane, ld);
-    qdma(io.r, ringw + sn * kQuadCells + kQuadCells / 2, io.lane + 16u, ld);
-    // the stores read their data registers after they issue (see steady_step)
-    asm volatile("" ::"v"(m.keep[0]), "v"(m.keep[1]));
-    m.keep[0] = d2{v.x, v.y};
-    m.keep[1] = d2{v.z, v.w};
-#pragma unroll
-    for (int k = 0; k + 1 < D; ++k) m.Pq[k] = m.Pq[k + 1];
-    m.Pq[D - 1] = d4{p0.x, p0.y, p1.x, p1.y};
-    if (SCHED == 0 || (SCHED == 1 && ODD)) __builtin_amdgcn_sched_barrier(0);
-}
-
-template <int T, int D, int SCHED, int Q0, int P0, int... NN>
-__device__ __forceinline__ void qchunk(QMarch<T, D>& m, double* ringw, const QIo& io,
-                                       unsigned off_n, std::integer_sequence<int, NN...>) {
-    constexpr int S = ring_slots<T, D>();
-    (qstep<T, D, Q0 ^ (NN & 1), false, SCHED, (NN & 1) != 0>(m, ringw, io, (P0 + NN) % S,
-                                                              off_n + (unsigned)NN * io.row_bytes),
-     ...);
-    __builtin_amdgcn_sched_barrier(0);
-}
-
-// an interior block (columns and rows clear of every physical side, height a
-// multiple of S) on one 256-column strip
-template <int T, int D, int SCHED, int Q0>
-__device__ __forceinline__ void quad_interior(const SweepParams& prm, const double* src,
-                                              double* dst, const double* rhs, int c_out, int j0,
-                                              int j1, int lane, double* ringw, double (&acc)[T]) {
-    constexpr int S = ring_slots<T, D>();
-    constexpr int OW4 = kQuadCells - 4 * T;
-    const long long pitch = prm.pitch;
-    const int c_ld = c_out - 2 * T;
-    const int rs = j0 - 2 * T, rend = j1 - 1 + 2 * T;
-    auto rsrc = [&](const double* b, int row0, int rows) {
-        const unsigned long long a =
-            (unsigned long long)(b + (long long)(kYOff + row0) * pitch + kXOff + c_ld);
-        const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
-        const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
-        return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo),
-                                                 (short)0, (int)((long long)rows * pitch * 8),
-                                                 0x00020000);
-    };
-    QIo io;
-    io.p = rsrc(src, rs, rend - rs + 1 + D);
-    io.r = rsrc(rhs, rs - 1, rend - rs + 1 + D);
-    io.d = rsrc(dst, j0, j1 - j0);
-    io.lane = (unsigned)lane * 32u;
-    io.row_bytes = (unsigned)(pitch * 8);
-    io.l2 = 2 * lane;
-    io.idx2 = prm.idx2;
-    io.idy2 = prm.idy2;
-    io.coef = prm.coef;
-    // owned columns [c_out, own_end]; the boundaries fall between halves
-    const int own_end = min(prm.ni, c_out + OW4 - 1);
-    const int c0 = c_ld + 4 * lane;
-    const bool own_lo = c0 >= c_out && c0 + 1 <= own_end;
-    const bool own_hi = c0 + 2 >= c_out && c0 + 3 <= own_end;
-    io.st_lo = own_lo ? io.lane : 0x40000000u;
-    io.st_hi = own_hi ? io.lane + 16u : 0x40000000u;
-
-    QMarch<T, D> m;
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-        m.A[t] = m.M1[t] = m.M2[t] = d4{0.0, 0.0, 0.0, 0.0};
-        m.al[t] = m.ah[t] = 0.0;
-    }
-    m.keep[0] = m.keep[1] = d2{0.0, 0.0};
-    // rows 0 .. D-1 (p rows rs.., rhs rows rs-1..) into the registers / ring
-#pragma unroll
-    for (int k = 0; k < D; ++k) {
-        const unsigned o = (unsigned)k * io.row_bytes;
-        const d2 a = bload(io.p, io.lane, o), b = bload(io.p, io.lane + 16u, o);
-        m.Pq[k] = d4{a.x, a.y, b.x, b.y};
-        qdma(io.r, ringw + k * kQuadCells, io.lane, o);
-        qdma(io.r, ringw + k * kQuadCells + kQuadCells / 2, io.lane + 16u, o);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // 4T warm-up steps (no residual, dropped stores), phase computed at run time
-    for (int n = 0; n < 4 * T; n += 2) {
-        qstep<T, D, Q0, true>(m, ringw, io, n % S, (unsigned)n * io.row_bytes);
-        qstep<T, D, 1 - Q0, true>(m, ringw, io, (n + 1) % S, (unsigned)(n + 1) * io.row_bytes);
-    }
-#pragma unroll
-    for (int t = 0; t < T; ++t) m.al[t] = m.ah[t] = 0.0;
-    // steady: chunks of S statically unrolled steps (S even: each starts with colour Q0)
-    constexpr int P0 = (4 * T) % S;
-    const int nchunks = (j1 - j0) / S;
-    unsigned off = 4u * T * io.row_bytes;
-    for (int k = 0; k < nchunks; ++k) {
-        qchunk<T, D, SCHED, Q0, P0>(m, ringw, io, off, std::make_integer_sequence<int, S>{});
-        off += (unsigned)S * io.row_bytes;
-    }
-    // drain the ring's DMAs before the LDS is reused
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int t = 0; t < T; ++t) acc[t] += (own_lo ? m.al[t] : 0.0) + (own_hi ? m.ah[t] : 0.0);
-}
-
-// one block of a quad pass: logical block L
-template <int T, int WAVES, int D, int SCHED>
-__device__ __forceinline__ void tb4_block(const SweepParams& prm, const double* __restrict__ src,
-                                          double* __restrict__ dst,
-                                          const double* __restrict__ rhs,
-                                          double* __restrict__ partials, const int L,
-                                          double (*wsum)[WAVES], double* ringw) {
-    constexpr int OW4 = kQuadCells - 4 * T;
-    constexpr int OW2 = kStripCells - 4 * T;
-    constexpr int S = ring_slots<T, D>();
-    const int bx = L % prm.nbx, by = L / prm.nbx;
-    int j0, j1;
-    block_rows(prm, by, j0, j1);
-    if (prm.part != 0) {  // overlapped decomposed pass: blocks clear of the halo first
-        const int lo = 1 + bx * WAVES * OW4 - 2 * T;
-        const int hi = 1 + (bx * WAVES + WAVES - 1) * OW4 - 2 * T + kQuadCells - 1;
-        const bool interior = lo >= prm.int_lo_i && hi <= prm.int_hi_i &&
-                              j0 - 2 * T >= prm.int_lo_j && j1 - 1 + 2 * T <= prm.int_hi_j;
-        if (interior != (prm.part == 1)) return;
-    }
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int ni = prm.ni;
-    const int c_out = 1 + (bx * WAVES + wave) * OW4;
-    const int c_ld = c_out - 2 * T;
-    if (L == 0) copy_corners(prm, src, dst);
-    double acc[T];
-#pragma unroll
-    for (int t = 0; t < T; ++t) acc[t] = 0.0;
-    if (c_out <= ni) {  // wave-uniform
-        const int rs = j0 - 2 * T, rend = j1 - 1 + 2 * T;
-        const bool cols_in = c_ld >= prm.upd_lo_i && c_ld + kQuadCells - 1 <= prm.upd_hi_i &&
-                             (c_out + OW4 - 1 <= ni || (ni & 1) == 0);
-        const bool rows_in = rs >= prm.upd_lo_j && rend <= prm.upd_hi_j &&
-                             (j1 - j0) % S == 0 && j1 - j0 > 0;
-        if (cols_in && rows_in) {
-            if (((prm.parity + rs) & 1) != 0)
-                quad_interior<T, D, SCHED, 1>(prm, src, dst, rhs, c_out, j0, j1, lane, ringw, acc);
-            else
-                quad_interior<T, D, SCHED, 0>(prm, src, dst, rhs, c_out, j0, j1, lane, ringw, acc);
-        } else {
-            // 128-column strips over the quad strip's own columns
-            const int own_hi = c_out + OW4 - 1;
-            for (int sc = c_out; sc <= min(ni, own_hi); sc += OW2)
-                tb_strip2<T, D, false>(prm, src, dst, rhs, sc, own_hi, j0, j1, by, lane, acc);
-        }
-    }
-    block_partials<T, WAVES>(prm, acc, partials, L, wsum);
-}
-
 // occupancy target: 2 waves per SIMD (the register file of one wave is 256
 // VGPRs; below that the compiler would rather use AGPRs and run one wave).
 //
@@ -1199,8 +924,9 @@ __device__ __forceinline__ unsigned long long chain_load(const unsigned long lon
 // slot (-1: a private range), end of the blocks it owns (own_end); sh[8] =
 // the blocks its segment had unclaimed; sh[0] = -1: no work left.  Wave 0
 // only.
-__device__ void chain_acquire(const SweepParams& prm, int* head, unsigned long long* seg,
-                              int* sh) {
+__device__ __forceinline__ void chain_acquire(const SweepParams& prm, int* head,
+                                              unsigned long long* seg,
+                                              int* sh) {
     const int lane = threadIdx.x & 63;
     const int n0 = prm.nseg0;
     // 1. the initial segments, by ticket: the home XCD's run first
@@ -1615,23 +1341,6 @@ __global__ __launch_bounds__(kLanes* WAVES, 2) void rb_tb_kernel(
     if (!force && st->done) return;
     for_each_block(prm, queue, &ticket, [&](int L) {
         tb_block<T, WAVES, D, BP, P2>(prm, src, dst, rhs, partials, L, wsum);
-    });
-}
-
-// the quad variant: one workgroup of WAVES waves per CU (the rhs rings fill
-// the LDS), so one wave per SIMD
-template <int T, int WAVES, int D, int SCHED>
-__global__ __launch_bounds__(kLanes* WAVES, 1) void rb_tb4_kernel(
-    SweepParams prm, const double* __restrict__ src, double* __restrict__ dst,
-    const double* __restrict__ rhs, double* __restrict__ partials,
-    const DevState* __restrict__ st, int force, int* __restrict__ queue) {
-    __shared__ double wsum[T][WAVES];
-    __shared__ int ticket;
-    __shared__ double ring[WAVES][ring_slots<T, D>()][kQuadCells];
-    if (!force && st->done) return;
-    double* ringw = &ring[threadIdx.x >> 6][0][0];
-    for_each_block(prm, queue, &ticket, [&](int L) {
-        tb4_block<T, WAVES, D, SCHED>(prm, src, dst, rhs, partials, L, wsum, ringw);
     });
 }
 

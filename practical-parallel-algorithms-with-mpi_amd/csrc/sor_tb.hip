@@ -8,11 +8,9 @@
 
 namespace misor {
 
-int tb_cols(int variant) { return kTbVariants[variant].cols; }
-
 int tb_max_t(int variant) { return kTbVariants[variant].max_t; }
 
-int tb_out_width(int T, int variant) { return kLanes * tb_cols(variant) - 4 * T; }
+int tb_out_width(int T, int /*variant*/) { return kStripCells - 4 * T; }
 
 int tb_waves(int variant) { return kTbVariants[variant].waves; }
 
@@ -50,9 +48,9 @@ void launch_tb(hipStream_t s, int T, const SweepParams& prm, const double* src, 
     switch (T) {
 #define C(N)                                                                \
     case N: launch_tb_t##N(s, prm, src, dst, rhs, partials, st, force, queue); break;
-    C(1) C(2) C(3) C(4) C(5) C(6) C(7) C(8) C(9) C(10) C(11)
+    C(1) C(2) C(3) C(4) C(5) C(6) C(7) C(8) C(9)
 #undef C
-    default: launch_tb_t12(s, prm, src, dst, rhs, partials, st, force, queue); break;
+    default: launch_tb_t10(s, prm, src, dst, rhs, partials, st, force, queue); break;
     }
 }
 
@@ -60,9 +58,9 @@ int tb_resident(int T, int variant) {
     switch (T) {
 #define C(N) \
     case N: return tb_resident_t##N(variant);
-    C(1) C(2) C(3) C(4) C(5) C(6) C(7) C(8) C(9) C(10) C(11)
+    C(1) C(2) C(3) C(4) C(5) C(6) C(7) C(8) C(9)
 #undef C
-    default: return tb_resident_t12(variant);
+    default: return tb_resident_t10(variant);
     }
 }
 

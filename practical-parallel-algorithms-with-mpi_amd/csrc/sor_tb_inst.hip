@@ -37,28 +37,14 @@ static int resident_chain() {
     return n;
 }
 
-template <int T, int W, int D, bool P2, int SK = 0>
-static int residenth() {
+template <int T, int W, int D, bool P2, int SK>
+static int residenthc() {
     static int n = 0;
-    if (n == 0) n = persistent_grid(rb_tbh_kernel<T, W, D, P2, SK>, kLanes * W);
-    return n;
-}
-
-template <int T, int W, int D, int SC>
-static int resident4() {
-    static int n = 0;
-    if (n == 0) n = persistent_grid(rb_tb4_kernel<T, W, D, SC>, kLanes * W);
+    if (n == 0) n = persistent_grid(rb_tbhc_kernel<T, W, D, P2, SK, 0>, kLanes * W);
     return n;
 }
 
 constexpr int kT = MISOR_TB_T;
-// a quad variant exists for T <= its max_t (its LDS ring must fit); configure_tb
-// never selects it above
-template <int V>
-constexpr bool quad_ok() {
-    return kTbVariants[V].cols == 4 && kT <= kTbVariants[V].max_t;
-}
-
 void MISOR_CAT(launch_tb_t, MISOR_TB_T)(hipStream_t s, const SweepParams& prm,
                                         const double* src, double* dst, const double* rhs,
                                         double* partials, const DevState* st, int force,
@@ -74,9 +60,23 @@ void MISOR_CAT(launch_tb_t, MISOR_TB_T)(hipStream_t s, const SweepParams& prm,
     };
     if (prm.variant == kHrTbVariant) {  // skewed (tb_ring_slots: T = 1 runs unskewed)
         constexpr int SK_ = kT >= 2 ? 1 : 0;
-        if (prm.pow2) go(rb_tbh_kernel<kT, 4, 2, true, SK_>, kLanes * 4, residenth<kT, 4, 2, true, SK_>());
-        else go(rb_tbh_kernel<kT, 4, 2, false, SK_>, kLanes * 4, residenth<kT, 4, 2, false, SK_>());
-        return;
+        {
+            // the chained split-ring pass (sor_tbh.h rb_tbhc_kernel; configure_tb
+            // keeps its passes chained and persistent): the work area gets the
+            // launch's initial segment list (as the chained pass below)
+            launch_chain_init(s, queue, prm.seg_tmpl, prm.nseg0, prm.seg_cap);
+            auto gc = [&](auto kernel, int resident) {
+                const int grid = std::min(prm.chain_blocks, std::max(8, resident - prm.reserve));
+                hipLaunchKernelGGL(kernel, dim3(grid), dim3(kLanes * 4), 0, s, prm, src, dst, rhs,
+                                   partials, st, force, queue);
+            };
+            // (one kernel for the main and the edge list: a strip at a physical
+            // side marches block by block, the workgroup's other strips chain)
+            const int res = residenthc<kT, 4, 2, false, SK_>();
+            if (prm.pow2) gc(rb_tbhc_kernel<kT, 4, 2, true, SK_, 0>, res);
+            else          gc(rb_tbhc_kernel<kT, 4, 2, false, SK_, 0>, res);
+            return;
+        }
     }
     // the 2- and 4-column register-ring kernels: T <= kMaxT2 (configure_tb)
     if constexpr (kT <= kMaxT2) {
@@ -100,45 +100,20 @@ void MISOR_CAT(launch_tb_t, MISOR_TB_T)(hipStream_t s, const SweepParams& prm,
             }
             return;
         }
-#define TB(W, DD) go(rb_tb_kernel<kT, W, DD, false>, kLanes * W, resident2<kT, W, DD, false>())
-        // must match kTbVariants (misor_internal.h)
-        switch (prm.variant) {
-        case 1: TB(8, 2); break;
-        case 2:  // 2 strips per workgroup (finer slots for small rank blocks)
+        if (prm.variant == 2) {  // 2 strips per workgroup (finer slots for small rank blocks)
             if (prm.pow2) go(rb_tb_kernel<kT, 2, 2, false, true>, kLanes * 2, resident2<kT, 2, 2, false>());
-            else TB(2, 2);
-            break;
-        case 3: TB(1, 2); break;
-        case 4: TB(4, 3); break;
-        case kQuadTbVariant: {
-            constexpr int D_ = kTbVariants[kQuadTbVariant].ahead;
-            constexpr int SC_ = kTbVariants[kQuadTbVariant].sched;
-            go(rb_tb4_kernel<kT, 4, D_, SC_>, kLanes * 4, resident4<kT, 4, D_, SC_>());
-            break;
-        }
-        default:
+            else go(rb_tb_kernel<kT, 2, 2, false, false>, kLanes * 2, resident2<kT, 2, 2, false>());
+        } else {  // the default (kTbVariants: every other built variant is 13, above)
             if (prm.pow2) go(rb_tb_kernel<kT, 4, 2, false, true>, kLanes * 4, resident2<kT, 4, 2, false>());
-            else TB(4, 2);
-            break;
+            else go(rb_tb_kernel<kT, 4, 2, false, false>, kLanes * 4, resident2<kT, 4, 2, false>());
         }
-#undef TB
     }
 }
 
 int MISOR_CAT(tb_resident_t, MISOR_TB_T)(int variant) {
-    if (variant == kHrTbVariant) return residenth<kT, 4, 2, false, kT >= 2 ? 1 : 0>();
-    if constexpr (kT <= kMaxT2) {
-        switch (variant) {
-        case 1: return resident2<kT, 8, 2, false>();
-        case 2: return resident2<kT, 2, 2, false>();
-        case 3: return resident2<kT, 1, 2, false>();
-        case 4: return resident2<kT, 4, 3, false>();
-        case kQuadTbVariant:
-            return resident4<kT, 4, kTbVariants[kQuadTbVariant].ahead,
-                             kTbVariants[kQuadTbVariant].sched>();
-        default: return resident2<kT, 4, 2, false>();
-        }
-    }
+    if (variant == kHrTbVariant) return residenthc<kT, 4, 2, false, kT >= 2 ? 1 : 0>();
+    if constexpr (kT <= kMaxT2)
+        return variant == 2 ? resident2<kT, 2, 2, false>() : resident2<kT, 4, 2, false>();
     return 0;
 }
 

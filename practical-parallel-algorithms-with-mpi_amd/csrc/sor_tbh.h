@@ -1,6 +1,7 @@
 // sor_tbh.h -- the temporally blocked sweep with a split rhs ring (TB
-// variant kHrTbVariant: rb_tbh_kernel).  Device code; included by
-// sor_tb_inst.hip after sor_tb.h, whose stage() arithmetic it runs unchanged.
+// variant kHrTbVariant: rb_tbhc_kernel, chained runs, below).  Device code;
+// included by sor_tb_inst.hip after sor_tb.h, whose stage() arithmetic it runs
+// unchanged.
 //
 // Why.  A pass of the 2-column march (sor_tb.h) costs, at 32768^2, about
 // 4.7 ms of streaming (T = 1: 4.68 ms per launch) plus ~0.19 ms per stage
@@ -19,7 +20,8 @@
 // | column b, so a stage's read of one colour's column is one conflict-free
 // ds_read_b64).  K is chosen to balance the rings: S = max(2K + D,
 // 2(T - K) + 1), even -- 12 slots at T = 10 (48 VGPRs of ring instead of 88,
-// 12 KB of LDS per wave, 96 KB per CU at two workgroups of four waves).
+// 12 KB of LDS per wave, 96 KB per CU at two workgroups of four waves; with the
+// skew of hrs_step, 18 slots: 18 KB per wave).
 //
 // Every block runs the static ring from its first step: interior blocks warm
 // up for exactly 4T steps (4T + 1 skewed) -- whole kPre chunks, then a partial
@@ -65,6 +67,7 @@ struct HrIo {
     __amdgpu_buffer_rsrc_t p, r, d;  // p rows from rs0, rhs rows from rs0 - 1, dst rows from j0
     unsigned lane;                   // lane * 16
     unsigned st_lane;                // kSteady: lane * 16 if the lane stores, else out of range
+    unsigned st_a, st_b;             // kSteadyEdge: per column (lane * 16 (+ 8) or out of range)
     unsigned row_bytes;
     lds_double* lx;                  // the wave's LDS ring (+ lane): slot s at lx + 128 s
     double* dp;                      // kEdge / kRowEdge stores: dst at row 0 of the lane's columns
@@ -115,6 +118,12 @@ __device__ __forceinline__ void hr_step(HrMarch<T, D>& m, d2* R, const Lane& c, 
     if (MODE == kSteady) {
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), io.d, io.st_lane,
                                                off_n - st_base, 2);
+    } else if (MODE == kSteadyEdge) {  // per column (hrs_step)
+        const double vx = v.x, vy = v.y;
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, vx), io.d, io.st_a,
+                                              off_n - st_base, 2);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, vy), io.d, io.st_b,
+                                              off_n - st_base, 2);
     } else if (MODE == kEdge || MODE == kRowEdge) {
         const int jw = r0 - 2 * T;  // row finished by the last stage (tb_step)
         if (jw >= c.j0 && jw < c.j1) {
@@ -191,19 +200,20 @@ __device__ __forceinline__ void hrs_step(HrMarch<T, D>& m, d2* R, const Lane& c,
     d2 v = m.Pq[0];
     d2 u = m.B;
     d2 prevM2 = m.M2[T - 1];
-    if constexpr (MODE == kSteady) {
+    if constexpr (MODE == kSteady || MODE == kSteadyEdge) {
+        constexpr bool EM = MODE == kSteadyEdge;
 #pragma unroll
         for (int k = 0; k < SKH; ++k) {
             const int ta = SKH + k, tb = k;
-            stage_pair<Q, 1 - Q, P2>(c, u, m.A[ta], m.M1[ta], m.M2[ta], rr(ta, true), rr(ta, false),
-                                     m.acc[ta], v, m.A[tb], m.M1[tb], m.M2[tb], rr(tb, true),
-                                     rr(tb, false), m.acc[tb]);
+            stage_pair<Q, 1 - Q, P2, EM>(c, u, m.A[ta], m.M1[ta], m.M2[ta], rr(ta, true),
+                                         rr(ta, false), m.acc[ta], v, m.A[tb], m.M1[tb],
+                                         m.M2[tb], rr(tb, true), rr(tb, false), m.acc[tb]);
         }
         if (T - SKH > SKH)
-            u = stage<T, Q, kSteady, false, P2, SKH>(c, T - 1, true, u, r0 - 2 * (T - 1),
-                                                     m.A[T - 1], m.M1[T - 1], m.M2[T - 1],
-                                                     rr(T - 1, true), rr(T - 1, false),
-                                                     m.acc[T - 1]);
+            u = stage<T, Q, MODE, false, P2, SKH>(c, T - 1, true, u, r0 - 2 * (T - 1),
+                                                  m.A[T - 1], m.M1[T - 1], m.M2[T - 1],
+                                                  rr(T - 1, true), rr(T - 1, false),
+                                                  m.acc[T - 1]);
     } else {
 #pragma unroll
         for (int t = SKH; t < T; ++t) {
@@ -227,6 +237,12 @@ __device__ __forceinline__ void hrs_step(HrMarch<T, D>& m, d2* R, const Lane& c,
     if (MODE == kSteady) {
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, u), io.d, io.st_lane,
                                                off_n - st_base, 2);
+    } else if (MODE == kSteadyEdge) {  // per column: owned cells and the ghost column
+        const double ux = u.x, uy = u.y;  // (scalar copies: sor_tb.h steady_step)
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, ux), io.d, io.st_a,
+                                              off_n - st_base, 2);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, uy), io.d, io.st_b,
+                                              off_n - st_base, 2);
     } else if (MODE == kEdge || MODE == kRowEdge) {
         const int jw = r0 - 2 * T;
         if (jw >= c.j0 && jw < c.j1) {
@@ -289,28 +305,24 @@ __device__ __forceinline__ void hr_run(HrMarch<T, D>& m, d2* R, const Lane& c, c
                                        int rs0, int k0, int k1, unsigned st_base, int n0 = 0) {
     constexpr int S = Hr<T, D, SK>::S;
     for (int k = k0; k < k1; ++k) {
-        const int n = n0 + (k - k0) * S;
-        hr_chunk<T, D, SK, MODE, Q0 ^ (P0 & 1), P2, P0>(m, R, c, io, rs0 + n,
-                                                        (unsigned)n * io.row_bytes, st_base,
-                                                        std::make_integer_sequence<int, S>{});
+        // (the chunk's row offset is a scalar: readfirstlane keeps the compiler
+        // from taking it for a per-lane value where the march runs inside the
+        // chained loop, hr_chain_steady -- a waterfall loop per buffer access)
+        const int n = __builtin_amdgcn_readfirstlane(n0 + (k - k0) * S);
+        hr_chunk<T, D, SK, MODE, Q0 ^ (P0 & 1), P2, P0>(
+            m, R, c, io, rs0 + n, __builtin_amdgcn_readfirstlane((unsigned)n * io.row_bytes),
+            st_base, std::make_integer_sequence<int, S>{});
     }
 }
 
-// one wave's strip (tb_strip2's geometry and lane setup) through the
-// split-ring march; lx: the wave's LDS ring
-template <int T, int D, bool P2, int SK = 0>
-__device__ __forceinline__ void hr_strip(const SweepParams& prm, const double* __restrict__ src,
-                                         double* __restrict__ dst, const double* __restrict__ rhs,
-                                         const int c_out, const int j0, const int j1, const int by,
-                                         const int lane, double (&acc)[T], lds_double* lx) {
-    constexpr int OW = kStripCells - 4 * T;
-    constexpr int S = Hr<T, D, SK>::S, WU = Hr<T, D, SK>::WU;
+// the per-lane constants of the strip whose owned columns start at c_out,
+// for block rows [j0, j1) of block row `by` (tb_strip2's lane setup)
+template <int T>
+__device__ __forceinline__ void hr_lane(const SweepParams& prm, const int c_out, const int j0,
+                                        const int j1, const int by, const int lane, Lane& c) {
     const int ni = prm.ni, nj = prm.nj;
     const int c_ld = c_out - 2 * T;
-    const long long pitch = prm.pitch;
     const int own_end = ni;
-
-    Lane c;
     c.ia = c_ld + 2 * lane;
     c.ib = c.ia + 1;
     c.up_a = c.ia >= prm.upd_lo_i && c.ia <= prm.upd_hi_i;
@@ -338,11 +350,51 @@ __device__ __forceinline__ void hr_strip(const SweepParams& prm, const double* _
     c.coef = prm.coef;
     c.bl = ((lane + 63) & 63) * 4;
     c.br = ((lane + 1) & 63) * 4;
+}
+
+// columns interior: every column of the cone an updated cell and ownership
+// uniform per lane (tb_strip2's cols_in)
+template <int T>
+__device__ __forceinline__ bool hr_cols_in(const SweepParams& prm, int c_out) {
+    constexpr int OW = kStripCells - 4 * T;
+    const int c_ld = c_out - 2 * T;
+    return c_ld >= prm.upd_lo_i && c_ld + kStripCells - 1 <= prm.upd_hi_i &&
+           (c_out + OW - 1 <= prm.ni || (prm.ni & 1) == 0);
+}
+
+// wave-uniform buffer descriptor over the strip's 128 columns of `rows` rows
+// from row0.  Every input passes through readfirstlane: a descriptor the
+// compiler cannot prove uniform (e.g. one rebuilt in a loop, hr_chain_steady)
+// gets a waterfall loop around every buffer operation (cdna_hip_programming.md
+// T20).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t hr_rsrc(const SweepParams& prm, const double* b,
+                                                         int c_ld, int row0, int rows) {
+    const long long pitch = prm.pitch;
+    const unsigned long long a =
+        (unsigned long long)(b + (long long)(kYOff + row0) * pitch + kXOff + c_ld);
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+    const int bytes = __builtin_amdgcn_readfirstlane((int)((long long)rows * pitch * 8));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo),
+                                             (short)0, bytes, 0x00020000);
+}
+
+// one wave's strip (tb_strip2's geometry and lane setup) through the
+// split-ring march; lx: the wave's LDS ring
+template <int T, int D, bool P2, int SK = 0>
+__device__ __forceinline__ void hr_strip(const SweepParams& prm, const double* __restrict__ src,
+                                         double* __restrict__ dst, const double* __restrict__ rhs,
+                                         const int c_out, const int j0, const int j1, const int by,
+                                         const int lane, double (&acc)[T], lds_double* lx) {
+    constexpr int S = Hr<T, D, SK>::S, WU = Hr<T, D, SK>::WU;
+    const int c_ld = c_out - 2 * T;
+    const long long pitch = prm.pitch;
+    Lane c;
+    hr_lane<T>(prm, c_out, j0, j1, by, lane, c);
 
     const int rs = j0 - 2 * T;  // first row of the cone
     const int rend = j1 - 1 + 2 * T;
-    const bool cols_in = c_ld >= prm.upd_lo_i && c_ld + kStripCells - 1 <= prm.upd_hi_i &&
-                         (c_out + OW - 1 <= ni || (ni & 1) == 0);
+    const bool cols_in = hr_cols_in<T>(prm, c_out);
     const bool rows_in = rs >= prm.upd_lo_j && rend <= prm.upd_hi_j && (j1 - j0) % S == 0 &&
                          j1 - j0 > 0;
     const bool steady = cols_in && rows_in;
@@ -353,19 +405,10 @@ __device__ __forceinline__ void hr_strip(const SweepParams& prm, const double* _
     const int nsteps = rend - rs0 + 1;
     const int nchunks = (nsteps + S - 1) / S;
 
-    auto rsrc = [&](const double* b, int row0, int rows) {
-        const unsigned long long a =
-            (unsigned long long)(b + (long long)(kYOff + row0) * pitch + kXOff + c_ld);
-        const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
-        const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
-        return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo),
-                                                 (short)0, (int)((long long)rows * pitch * 8),
-                                                 0x00020000);
-    };
     HrIo io;
-    io.p = rsrc(src, rs0, nsteps + D + SK);
-    io.r = rsrc(rhs, rs0 - 1, nsteps + D + SK);
-    io.d = rsrc(dst, j0, j1 - j0);
+    io.p = hr_rsrc(prm, src, c_ld, rs0, nsteps + D + SK);
+    io.r = hr_rsrc(prm, rhs, c_ld, rs0 - 1, nsteps + D + SK);
+    io.d = hr_rsrc(prm, dst, c_ld, j0, j1 - j0);
     io.lane = (unsigned)lane * 16u;
     io.st_lane = c.own_a ? (unsigned)lane * 16u : 0x40000000u;
     io.row_bytes = (unsigned)(pitch * 8);
@@ -422,54 +465,217 @@ __device__ __forceinline__ void hr_strip(const SweepParams& prm, const double* _
     for (int t = 0; t < T; ++t) acc[t] += m.acc[t];
 }
 
-// one block (bx, by) of a split-ring pass: logical block L (tb_block)
-template <int T, int WAVES, int D, bool P2, int SK>
-__device__ __forceinline__ void hr_block(const SweepParams& prm, const double* __restrict__ src,
-                                         double* __restrict__ dst, const double* __restrict__ rhs,
-                                         double* __restrict__ partials, const int L,
-                                         double (*wsum)[WAVES], lds_double* lx) {
-    constexpr int OW = kStripCells - 4 * T;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    const int bx = L % prm.nbx, by = L / prm.nbx;
+// ---------------------------------------------------------------------------
+// Chained split-ring passes (rb_tbhc_kernel): sor_tb.h's chained runs --
+// segments of block rows of one column, claimed block by block, work stealing,
+// residual partials per wave and block at fixed slots (chain_acquire,
+// chain_block_end) -- on the split-ring march.  A run of steady-able blocks
+// (a height the ring divides, the cone clear of the physical bottom / top
+// sides) warms up once, at its first block (WU steps), and then marches
+// kSteady chunks from block to block with its registers and LDS ring live:
+// the 4T + 1 warm-up steps an unchained block spends per H rows (7% of a
+// 576-row block at T = 10, all of it VALU work the VALU-bound pass pays for)
+// are spent once per run.  A strip at a physical left / right side chains the
+// same way in kSteadyEdge chunks (the paired stages with lane masks and the
+// ghost column copies); the columns with such a strip form the pass's second list
+// (sor_tb.h), run by a second launch of the same kernel beside the main one.
+// Blocks that are not steady-able are marched one by one from scratch
+// (hr_strip).
+// ---------------------------------------------------------------------------
+template <int T, int D, int SK>
+__host__ __device__ inline bool hr_chain_rows_ok(const SweepParams& prm, int j0, int j1) {
+    constexpr int S = Hr<T, D, SK>::S;
+    return j0 - 2 * T >= prm.upd_lo_j && j1 - 1 + 2 * T <= prm.upd_hi_j && (j1 - j0) % S == 0 &&
+           j1 > j0;
+}
+
+// a chained run of steady blocks on one wave's strip, from block row by;
+// colour Q of the run's first streamed row (the same at every block start: the
+// heights are multiples of the even S).  EM: a strip at a physical left /
+// right side -- kSteadyEdge chunks after a kEdge warm-up
+template <int T, int WAVES, int D, bool P2, int SK, int Q, bool EM>
+__device__ __forceinline__ void hr_chain_steady(const SweepParams& prm,
+                                                const double* __restrict__ src,
+                                                double* __restrict__ dst,
+                                                const double* __restrict__ rhs,
+                                                double* __restrict__ partials, int* sh,
+                                                unsigned long long* seg, const int c_out,
+                                                const int bx, int by, const int slot,
+                                                int own_end, const int lane, lds_double* lx) {
+    using G = Hr<T, D, SK>;
+    constexpr int S = G::S, WU = G::WU, KW = WU / S, WR = G::WR;
+    const int c_ld = c_out - 2 * T;
     int j0, j1;
     block_rows(prm, by, j0, j1);
-    if (prm.part != 0) {  // overlapped decomposed pass (tb_block)
-        const int lo = 1 + bx * WAVES * OW - 2 * T;
-        const int hi = 1 + (bx * WAVES + WAVES - 1) * OW - 2 * T + kStripCells - 1;
-        const bool interior = lo >= prm.int_lo_i && hi <= prm.int_hi_i &&
-                              j0 - 2 * T >= prm.int_lo_j && j1 - 1 + 2 * T <= prm.int_hi_j;
-        if (interior != (prm.part == 1)) return;
-    }
-    const int c_out = 1 + (bx * WAVES + wave) * OW;
-    if (L == 0) copy_corners(prm, src, dst);
-    double acc[T];
+    Lane c;
+    hr_lane<T>(prm, c_out, j0, j1, by, lane, c);
+    HrIo io;
+    io.lane = (unsigned)lane * 16u;
+    io.st_lane = c.own_a ? (unsigned)lane * 16u : 0x40000000u;
+    io.row_bytes = (unsigned)(prm.pitch * 8);
+    io.st_a = c.st_a ? (unsigned)lane * 16u : 0x40000000u;
+    io.st_b = c.st_b ? (unsigned)lane * 16u + 8u : 0x40000000u;
+    io.lx = lx + lane;
+    // kEdge stores: dst at row 0 of the lane's columns (kSteady: buffer stores)
+    io.dp = dst + (long long)kYOff * prm.pitch + kXOff + c.ia;
+    io.pitch = prm.pitch;
+    // a strip at a physical side: kEdge warm-up (its row tests keep it from
+    // tallying and storing), kSteadyEdge chunks (the paired stages with lane
+    // masks and the ghost column copies)
+    constexpr int WM = EM ? kEdge : kPre, SM = EM ? kSteadyEdge : kSteady;
+    // the descriptors of block [j0, j1): stream rows from rs0 = j0 - 2T - SK
+    // (step n streams row rs0 + n; the steady chunks of the block are steps
+    // WU .. WU + H - 1, loading up to D + SK rows past them)
+    // (plain assignments, no capturing lambda: state a lambda captures by
+    // reference can end up in private memory, whose loads are per-lane values
+    // to the compiler -- a waterfall loop around every buffer operation)
+    int rs0 = j0 - 2 * T - SK;
+    io.p = hr_rsrc(prm, src, c_ld, rs0, (j1 - j0) + WU + D + SK);
+    io.r = hr_rsrc(prm, rhs, c_ld, rs0 - 1, (j1 - j0) + WU + D + SK);
+    io.d = hr_rsrc(prm, dst, c_ld, j0, j1 - j0);
+    HrMarch<T, D> m;
+    d2 R[S];
 #pragma unroll
-    for (int t = 0; t < T; ++t) acc[t] = 0.0;
-    if (c_out <= prm.ni)
-        hr_strip<T, D, P2, SK>(prm, src, dst, rhs, c_out, j0, j1, by, lane, acc, lx);
-    block_partials<T, WAVES>(prm, acc, partials, L, wsum);
+    for (int t = 0; t < T; ++t) {
+        m.acc[t] = 0.0;
+        m.A[t] = m.M1[t] = m.M2[t] = d2{0.0, 0.0};
+    }
+    m.keep[0] = m.keep[1] = d2{0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < S; ++k) R[k] = d2{0.0, 0.0};
+    m.B = d2{0.0, 0.0};
+#pragma unroll
+    for (int k = 0; k < D; ++k) m.Pq[k] = bload(io.p, io.lane, (unsigned)(k + SK) * io.row_bytes);
+#pragma unroll
+    for (int k = 0; k < D + SK; ++k) R[k] = bload(io.r, io.lane, (unsigned)k * io.row_bytes);
+    // the warm-up of the run's first block: KW whole chunks and WR steps (hr_strip)
+    const unsigned sb = (unsigned)WU * io.row_bytes;
+    hr_run<T, D, SK, WM, Q, P2>(m, R, c, io, rs0, 0, KW, sb);
+    if constexpr (WR > 0)
+        hr_chunk<T, D, SK, WM, Q, P2, 0>(m, R, c, io, rs0 + KW * S,
+                                         (unsigned)(KW * S) * io.row_bytes, sb,
+                                         std::make_integer_sequence<int, WR>{});
+    for (;;) {
+        // the block's H / S steady chunks from ring phase WR (step WU stores row j0)
+        hr_run<T, D, SK, SM, Q, P2, WR>(m, R, c, io, rs0, 0, (j1 - j0) / S, sb, WU);
+        if (!EM && !c.own_a) {  // lanes that do not own their columns tallied garbage
+#pragma unroll
+            for (int t = 0; t < T; ++t) m.acc[t] = 0.0;
+        }
+        // (zeroes m.acc)
+        const int nb = chain_block_end<T, WAVES>(prm, m.acc, partials, by * prm.nbx + bx, sh, seg,
+                                                 slot, by, own_end);
+        if (nb < 0) break;
+        // the next block of the run continues the stream: same ring phase
+        // (H is a multiple of S), descriptors rebased at its rows
+        rs0 = __builtin_amdgcn_readfirstlane(rs0 + (j1 - j0));
+        by = nb;
+        block_rows(prm, by, j0, j1);
+        j0 = __builtin_amdgcn_readfirstlane(j0);
+        j1 = __builtin_amdgcn_readfirstlane(j1);
+        io.p = hr_rsrc(prm, src, c_ld, rs0, (j1 - j0) + WU + D + SK);
+        io.r = hr_rsrc(prm, rhs, c_ld, rs0 - 1, (j1 - j0) + WU + D + SK);
+        io.d = hr_rsrc(prm, dst, c_ld, j0, j1 - j0);
+    }
+    // (the LDS ring is the wave's own; the next run overwrites it from its
+    // warm-up on, after its first writes)
+}
+
+// one run of a chained split-ring pass: column bx from block row by (all
+// waves; sor_tb.h chain_run): runs of steady blocks chained (hr_chain_steady),
+// every other block alone (hr_strip); EDGE = 1 (an A/B form): every block
+// alone.  Every wave calls chain_block_end at every block end of the run.
+template <int T, int WAVES, int D, bool P2, int SK, int EDGE>
+__device__ __forceinline__ void hr_chain_run(const SweepParams& prm,
+                                             const double* __restrict__ src,
+                                             double* __restrict__ dst,
+                                             const double* __restrict__ rhs,
+                                             double* __restrict__ partials, int* sh,
+                                             unsigned long long* seg, int bx, int by, int slot,
+                                             int own_end, lds_double* lx) {
+    constexpr int OW = kStripCells - 4 * T;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int c_out = 1 + (bx * WAVES + wave) * OW;
+    if (bx == 0 && by == 0) copy_corners(prm, src, dst);
+    int j0, j1;
+    block_rows(prm, by, j0, j1);
+    const bool chained =
+        EDGE == 0 && c_out <= prm.ni && hr_chain_rows_ok<T, D, SK>(prm, j0, j1);
+    if (chained) {
+        // the colour of the run's first streamed row (rs0 = j0 - 2T - SK)
+        const bool q1 = ((prm.parity + j0 - 2 * T - SK) & 1) != 0;
+        if (hr_cols_in<T>(prm, c_out)) {
+            if (q1)
+                hr_chain_steady<T, WAVES, D, P2, SK, 1, false>(prm, src, dst, rhs, partials, sh,
+                                                               seg, c_out, bx, by, slot, own_end,
+                                                               lane, lx);
+            else
+                hr_chain_steady<T, WAVES, D, P2, SK, 0, false>(prm, src, dst, rhs, partials, sh,
+                                                               seg, c_out, bx, by, slot, own_end,
+                                                               lane, lx);
+        } else {
+            if (q1)
+                hr_chain_steady<T, WAVES, D, P2, SK, 1, true>(prm, src, dst, rhs, partials, sh,
+                                                              seg, c_out, bx, by, slot, own_end,
+                                                              lane, lx);
+            else
+                hr_chain_steady<T, WAVES, D, P2, SK, 0, true>(prm, src, dst, rhs, partials, sh,
+                                                              seg, c_out, bx, by, slot, own_end,
+                                                              lane, lx);
+        }
+        return;
+    }
+    // block by block from scratch (and the waves with no strip: block ends only)
+    for (;;) {
+        double acc[T];
+#pragma unroll
+        for (int t = 0; t < T; ++t) acc[t] = 0.0;
+        if (c_out <= prm.ni)
+            hr_strip<T, D, P2, SK>(prm, src, dst, rhs, c_out, j0, j1, by, lane, acc, lx);
+        by = chain_block_end<T, WAVES>(prm, acc, partials, by * prm.nbx + bx, sh, seg, slot, by,
+                                       own_end);
+        if (by < 0) return;
+        block_rows(prm, by, j0, j1);
+    }
 }
 
 }  // namespace
 
-// the split-ring pass: persistent per-XCD queues and block partials as
-// rb_tb_kernel; an LDS ring of S rows per wave.  SK: the skewed form (T >= 2)
-template <int T, int WAVES, int D, bool P2, int SK = 0>
-__global__ __launch_bounds__(kLanes* WAVES, 2) void rb_tbh_kernel(
+// the chained split-ring pass (sor_tb.h rb_tbc_kernel's work area and
+// segment lists; EDGE: the kernel of the columns at a physical left / right
+// side, launched beside the main one)
+template <int T, int WAVES, int D, bool P2, int SK, int EDGE>
+__global__ __launch_bounds__(kLanes* WAVES, 2) void rb_tbhc_kernel(
     SweepParams prm, const double* __restrict__ src, double* __restrict__ dst,
     const double* __restrict__ rhs, double* __restrict__ partials,
-    const DevState* __restrict__ st, int force, int* __restrict__ queue) {
-    __shared__ double wsum[T][WAVES];
-    __shared__ int ticket;
+    const DevState* __restrict__ st, int force, int* __restrict__ work) {
+    // sh[0..3]: the run (chain_acquire), sh[4..5]: trace clock, sh[6]: run start,
+    // sh[7]: own_end of the last claim, sh[8]: unclaimed blocks seen then
+    __shared__ __attribute__((aligned(8))) int sh[12];
     constexpr int S = Hr<T, D, SK>::S;
     __shared__ __attribute__((aligned(16))) double ring[WAVES * S * kStripCells];
     if (!force && st->done) return;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     lds_double* lx = (lds_double*)(ring + wave * S * kStripCells);
-    for_each_block(prm, queue, &ticket, [&](int L) __attribute__((always_inline)) {
-        hr_block<T, WAVES, D, P2, SK>(prm, src, dst, rhs, partials, L, wsum, lx);
-    });
+    unsigned long long* seg = reinterpret_cast<unsigned long long*>(work + kChainHead);
+    for (;;) {
+        __syncthreads();  // every wave has read the last claim of the previous run
+        if (threadIdx.x < kLanes) chain_acquire(prm, work, seg, sh);
+        if (prm.trace && threadIdx.x == 0) {
+            *reinterpret_cast<volatile unsigned long long*>(sh + 4) = wall_clock64();
+            sh[6] = 1;
+        }
+        __syncthreads();
+        const int bx = __builtin_amdgcn_readfirstlane(sh[0]);
+        const int by = __builtin_amdgcn_readfirstlane(sh[1]);
+        const int slot = __builtin_amdgcn_readfirstlane(sh[2]);
+        const int own_end = __builtin_amdgcn_readfirstlane(sh[3]);
+        __syncthreads();  // sh is rewritten by the run's block ends
+        if (bx < 0) break;
+        hr_chain_run<T, WAVES, D, P2, SK, EDGE>(prm, src, dst, rhs, partials, sh, seg, bx, by,
+                                                slot, own_end, lx);
+    }
 }
 
 }  // namespace misor

@@ -61,7 +61,8 @@ class Stats(C.Structure):
                 ("timed_sweeps", C.c_longlong), ("timed_passes", C.c_longlong),
                 ("iters_per_pass", C.c_int), ("tb_variant", C.c_int),
                 ("halo_ms", C.c_double), ("halos", C.c_longlong),
-                ("allreduce_ms", C.c_double), ("allreduces", C.c_longlong)]
+                ("allreduce_ms", C.c_double), ("allreduces", C.c_longlong),
+                ("chained", C.c_int)]
 
 
 class Desc3(C.Structure):
@@ -331,7 +332,8 @@ class Grid:
                 "timed_sweeps": s.timed_sweeps, "timed_passes": s.timed_passes,
                 "iters_per_pass": s.iters_per_pass, "tb_variant": s.tb_variant,
                 "halo_ms": s.halo_ms, "halos": s.halos,
-                "allreduce_ms": s.allreduce_ms, "allreduces": s.allreduces}
+                "allreduce_ms": s.allreduce_ms, "allreduces": s.allreduces,
+                "chained": s.chained}
 
     def reset_stats(self):
         _check(lib().misor_reset_stats(self.h))

@@ -1,11 +1,12 @@
 """Whole-field parity at the configurations the driver times (BASELINE configs
 4 and 5), every cell compared -- not windows.
 
-Config 4 (2D Poisson red-black SOR, 32768^2, bench.py --steps 20): the bench
-runs a warm-up solve of 7 iterations and one of 20, then times a third solve
-of 20 iterations (passes of the library's default T, split as evenly as the
-loop allows, misor_api.hip misor_solve_rb_n).  The test replays exactly that
-sequence on one Grid, downloads the field the timed solve starts from, and
+Config 4 (2D Poisson red-black SOR, 32768^2, bench.py --steps 20 --warmup 5,
+the driver's setting, BENCH_r04.json): the bench runs a warm-up solve of 5
+iterations and one of 20, then times a third solve of 20 iterations (the short
+pass plan: two 10-iteration passes of the split-ring kernel, TB variant 13,
+misor_api.hip solve_rb_from).  The test replays exactly that sequence on one
+Grid, asserts that the timed solve ran that kernel and plan, downloads the field the timed solve starts from, and
 checks the WHOLE 32770^2 result (ghosts included) bit for bit, and res to
 1e-12, against the multi-core restatement of solveRB
 (assignment-4/src/solver.c:179-238; oracle/oracle_mt.c, p bit-identical to
@@ -13,9 +14,12 @@ the single-thread restatement) started from that same field.  A block skipped
 or computed twice anywhere -- persistent queues, chained runs and work
 stealing decide at run time which workgroup computes which block -- fails it.
 
-Config 4 at 8 GPUs: the 4 x 2 split of bench.py --gpus 8 (one rank's block
-8192 x 16384: chained passes, pipelined loop, 2T-deep exchanges) as 8
-in-process ranks on the one GPU; the assembled field against the same oracle.
+Config 4 at 2, 4 and 8 GPUs: the splits of bench.py --gpus N (2 x 1: the short
+plan on 2^29-cell blocks; 2 x 2: 16384^2 = 2^28-cell blocks, unchained T = 8
+passes, pipelined; 4 x 2: one rank's block 8192 x 16384, chained split-ring
+passes of 10 iterations) as N
+in-process ranks on the one GPU (pipelined loop, 2T-deep exchanges); the
+assembled field against the same oracle.
 
 Config 5 at 8 GPUs: dcavity NS on the 8-rank global grid 65536 x 32768 (16384^2
 per rank, bench.py --workload ns --gpus 8), two time steps with the pressure
@@ -39,7 +43,7 @@ import pymisor as M
 pytestmark = pytest.mark.gpu
 
 OMEGA = 1.9
-STEPS, WARMUP = 20, 7  # the driver's bench setting (BENCH_r03.json)
+STEPS, WARMUP = 20, 5  # the driver's bench setting (BENCH_r04.json: --steps 20 --warmup 5)
 
 
 def host_threads():
@@ -80,10 +84,16 @@ def test_fullfield_32768_bench_sequence():
         g.solve_rb(itermax=STEPS)
         p = g.download(M.P)
         rhs = g.download(M.RHS)
+        g.enable_timing(True)  # as bench.py: per-pass events, stats from here
+        g.reset_stats()
         it, res = g.solve_rb(itermax=STEPS)  # the timed solve
-        T = g.stats()["iters_per_pass"]
+        st = g.stats()
+        T = st["iters_per_pass"]
         got = g.download(M.P)
     assert it == STEPS
+    # the kernel and plan bench.py times: two 10-iteration passes of the
+    # chained split ring (sor_tbh.h rb_tbhc_kernel)
+    assert (T, st["tb_variant"], st["timed_passes"], st["chained"]) == (10, 13, 2, 1), st
     it_ref, res_ref = orc.solve_rb_mt(p, rhs, dx, dx, OMEGA, 1e-300, STEPS, host_threads())
     del rhs
     assert it_ref == STEPS
@@ -91,10 +101,12 @@ def test_fullfield_32768_bench_sequence():
     assert abs(res - res_ref) <= 1e-12 * res_ref, (res, res_ref)
 
 
-@pytest.mark.parametrize("world", [2, 8])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_fullfield_32768_ranks(world):
-    """8 ranks: chained T = 8 passes on 2^27-cell blocks; 2 ranks: 2^29-cell
-    blocks, the short pass plan (two 10-iteration split-ring passes)"""
+    """8 ranks: 2^27-cell blocks, two 10-iteration passes of the chained split
+    ring; 4 ranks: 2^28-cell blocks, unchained persistent T = 8 passes
+    (7 + 7 + 6); 2 ranks: 2^29-cell blocks, the short pass plan (two
+    10-iteration split-ring passes)"""
     n = 32768
     dx = 1.0 / n
     cid = ("LOCAL:full%d" % world).encode()
@@ -112,7 +124,7 @@ def test_fullfield_32768_ranks(world):
                 chain = g.get_tuning(M.TUNE_TB_CHAIN)
                 st = g.stats()
                 outs[r] = [g.loc, p0, rhs, g.download(M.P), it, res, chain,
-                           (st["iters_per_pass"], st["tb_variant"])]
+                           (st["iters_per_pass"], st["tb_variant"], st["chained"])]
         except BaseException as e:
             errs.append((r, repr(e)))
 
@@ -127,8 +139,14 @@ def test_fullfield_32768_ranks(world):
     if world == 8:
         assert all(o[6] == 1 for o in outs)  # chained passes on a 2^27-cell block
         assert tuple(outs[0][0].dims) == (4, 2) and (outs[0][0].ni, outs[0][0].nj) == (8192, 16384)
-    else:
-        assert all(o[7] == (10, 13) for o in outs), [o[7] for o in outs]  # the short plan
+        # the chained split ring: T = 10 passes on the 2^27-cell blocks
+        assert all(o[7] == (10, 13, 1) for o in outs), [o[7] for o in outs]
+    elif world == 4:
+        assert all(o[6] == 0 for o in outs)  # 2^28 cells: not chained
+        assert tuple(outs[0][0].dims) == (2, 2) and (outs[0][0].ni, outs[0][0].nj) == (16384, 16384)
+        assert all(o[7] == (8, 0, 0) for o in outs), [o[7] for o in outs]
+    else:  # the short plan: 2 passes of the split ring (decomposed 2^29 blocks)
+        assert all(o[7][:2] == (10, 13) for o in outs), [o[7] for o in outs]
     p = np.empty((n + 2, n + 2))
     rhs = np.empty((n + 2, n + 2))
     got = np.empty((n + 2, n + 2))

@@ -3,14 +3,16 @@
 counts, res to 1e-12.
 
   13  the split rhs ring (sor_tbh.h): the rhs rows the later stages read move
-      from registers to an LDS ring, so T = 9 .. 12 fit the registers; every
-      block runs static-phase chunks (interior: whole warm-up chunks from a few
-      rows early; sides and ragged blocks: row-tested chunks past the block's
-      end); the march in two independent stage chains per step (hrs_step;
-      T = 1 unskewed).  It runs the short pass plan of the driver's solve.
+      from registers to an LDS ring, so T = 9, 10 fit the registers; the
+      march in two independent stage chains per step (hrs_step; T = 1
+      unskewed); chained runs of blocks (rb_tbhc_kernel: one warm-up per run,
+      registers and LDS ring live from block to block, work stealing), strips
+      at a physical left / right side in kSteadyEdge chunks, blocks that are
+      not steady-able alone in row-tested chunks.  It runs the short pass plan
+      of the driver's solve.
 
-Variants 6-12 were measured slower and are no longer built: configuring one
-fails (test_retired_variants), as does T > 8 on the register-ring kernels.
+Variants 1 and 3-12 were measured slower and are no longer built: configuring
+one fails (test_retired_variants), as does T > 8 on the register-ring kernels.
 
 The geometry runs interior blocks (static-ring chunks), the general march
 (physical sides, ragged last block rows), convergence inside a pass, the
@@ -29,7 +31,7 @@ pytestmark = pytest.mark.gpu
 
 HRS = 13
 VARIANTS = [HRS]
-RETIRED = range(6, 13)
+RETIRED = [1, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12]
 
 
 def hr_slots(T, D=2, sk=0, most=18):
@@ -72,7 +74,7 @@ def fields(ni, nj, seed):
 
 
 @pytest.mark.parametrize("variant", VARIANTS)
-@pytest.mark.parametrize("T", range(1, 13))
+@pytest.mark.parametrize("T", range(1, 11))
 @pytest.mark.parametrize("ni,nj", [(1201, 700), (2000, 1033), (1826, 600), (300, 190)])
 def test_variant_random_vs_oracle(ni, nj, T, variant):
     p, rhs = fields(ni, nj, ni + 7 * nj + T)
@@ -81,7 +83,9 @@ def test_variant_random_vs_oracle(ni, nj, T, variant):
         want = p.copy()
         it_ref, res_ref = orc.solve_rb(want, rhs, dx, dy, 1.7, 1e-300, k)
         # block rows of 3 ring lengths: interior blocks and several block rows
+        # (chained: runs of 3-ring blocks, stolen and split)
         it, res, got, st = solve(p, rhs, dx, dy, k, T, variant, rows=3 * ring(T, variant))
+        assert st["chained"] == (1 if T > 1 else 0)
         assert st["iters_per_pass"] == T
         assert it == it_ref == k
         assert np.array_equal(got, want), (k, np.argwhere(got != want)[:5])
@@ -106,7 +110,7 @@ def mid_pass_case():
 
 
 @pytest.mark.parametrize("variant", VARIANTS)
-@pytest.mark.parametrize("T", range(2, 13))
+@pytest.mark.parametrize("T", range(2, 11))
 def test_variant_converges_mid_pass(T, variant, mid_pass_case):
     """convergence inside a pass: the pass is recomputed with fewer
     iterations, so the count and p equal solveRB's"""
@@ -130,7 +134,7 @@ def test_variant_converges_mid_pass(T, variant, mid_pass_case):
 
 
 @pytest.mark.parametrize("variant", VARIANTS)
-@pytest.mark.parametrize("T", [2, 5, 8, 11])
+@pytest.mark.parametrize("T", [2, 5, 8, 10])
 @pytest.mark.parametrize("ni,nj", [(1024, 1024), (2050, 300)])
 def test_variant_pow2_spacing(ni, nj, T, variant, monkeypatch):
     """dx == dy == 2^-10: the power-of-two form of r (sor_tb.h resid<true>)
@@ -149,7 +153,7 @@ def test_variant_pow2_spacing(ni, nj, T, variant, monkeypatch):
         assert np.array_equal(got, want), (no, np.argwhere(got != want)[:5])
 
 
-@pytest.mark.parametrize("variant,T", [(HRS, 8), (HRS, 10), (HRS, 12)])
+@pytest.mark.parametrize("variant,T", [(HRS, 8), (HRS, 10)])
 def test_variant_default_geometry_large(variant, T):
     """8192^2, the automatic block height, the bench's problem 2 fields: one
     pass and a 20-iteration solve (T = 8: passes of 7 + 7 + 6; T = 10: 10 + 10)"""
@@ -221,10 +225,24 @@ def test_retired_variants(variant):
         assert g.get_tuning(M.TUNE_TB_VARIANT) == 0
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4, 5])
+def test_split_ring_needs_persistent():
+    """the split ring runs persistent chained passes only: turning persistent
+    launches off under it, or picking it with them off, is refused"""
+    with M.Grid(300, 190, 1.0 / 300, 1.0 / 190, 1.7, 1e-300, 10) as g:
+        g.set_tuning(M.TUNE_TB_VARIANT, HRS)
+        with pytest.raises(M.MisorError):
+            g.set_tuning(M.TUNE_TB_PERSISTENT, 0)
+        assert g.get_tuning(M.TUNE_TB_PERSISTENT) == 1
+        g.set_tuning(M.TUNE_TB_VARIANT, 0)
+        g.set_tuning(M.TUNE_TB_PERSISTENT, 0)
+        with pytest.raises(M.MisorError):
+            g.set_tuning(M.TUNE_TB_VARIANT, HRS)
+
+
+@pytest.mark.parametrize("variant", [0, 2])
 def test_register_ring_caps_t(variant):
-    """the register-ring kernels (and the quad one) run at most 8 iterations
-    a pass; asking for more is refused and leaves the grid as it was"""
+    """the register-ring kernels run at most 8 iterations a pass; asking for
+    more is refused and leaves the grid as it was"""
     with M.Grid(300, 190, 1.0 / 300, 1.0 / 190, 1.7, 1e-300, 10) as g:
         g.set_tuning(M.TUNE_TB_VARIANT, variant)
         T0 = g.get_tuning(M.TUNE_TSTEPS)

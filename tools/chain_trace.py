@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--shape", default="8192x16384")
     ap.add_argument("--size", type=int, default=32768, help="spacing 1/size")
     ap.add_argument("--T", type=int, default=8)
+    ap.add_argument("--variant", type=int, default=-1, help="TB variant (13: the split ring)")
     ap.add_argument("--rows", type=int, default=0)
     ap.add_argument("--passes", type=int, default=3, help="traced solves (last one kept)")
     ap.add_argument("--per-solve", type=int, default=1, help="passes per solve (the last traced)")
@@ -34,6 +35,8 @@ def main():
     g = M.Grid(ni, nj, 1.0 / a.size, 1.0 / a.size, 1.9, 1e-300, a.T * a.per_solve, device=0)
     g.poisson_init(1.0, 1.0, 2)
     g.set_tuning(M.TUNE_TB_CHAIN, 1)
+    if a.variant >= 0:
+        g.set_tuning(M.TUNE_TB_VARIANT, a.variant)
     g.set_tuning(M.TUNE_TSTEPS, a.T)
     if a.rows:
         g.set_tuning(M.TUNE_TB_ROWS, a.rows)

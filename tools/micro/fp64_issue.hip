@@ -20,7 +20,7 @@
     } while (0)
 
 template <int K, int DPP>
-__global__ void __launch_bounds__(512) chains(double* out, long long* clk, int iters, double r) {
+__global__ void __launch_bounds__(1024) chains(double* out, long long* clk, int iters, double r) {
     __shared__ double pad[18000];  // > 80 KB: one workgroup per CU
     double x[K];
 #pragma unroll
@@ -30,6 +30,10 @@ __global__ void __launch_bounds__(512) chains(double* out, long long* clk, int i
     for (int it = 0; it < iters; ++it) {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
+            if (DPP == 2) {  // one FMA per link: x = x^2 - 1.9 (chaotic on [-2, 2])
+                x[k] = __builtin_fma(x[k], x[k], -1.9);
+                continue;
+            }
             double t = __builtin_fma(-x[k], x[k], x[k]);
             if (DPP) {
                 // a 64-bit lane shift (two v_mov_b32_dpp) mixed in every link
@@ -80,7 +84,7 @@ int run(int waves, int iters, int ncu) {
     for (int i = 0; i < blocks; ++i) ghz.push_back((double)h[2 * i] / (double)h[2 * i + 1] * 0.1);
     std::sort(ghz.begin(), ghz.end());
     // FP64 wave-instructions per SIMD: waves/SIMD x iters x K x ops per link
-    const int ops = DPP ? 4 : 2;  // fma, mul (+ add, mul); dpp movs counted apart
+    const int ops = DPP == 2 ? 1 : DPP ? 4 : 2;  // fma, mul (+ add, mul); dpp movs counted apart
     const double winst = (double)(waves / 4) * iters * K * ops;
     const double ghz_med = ghz[blocks / 2];
     const double cyc = ms * 1e-3 * ghz_med * 1e9;
@@ -98,13 +102,14 @@ int main() {
     hipDeviceProp_t p;
     if (hipGetDeviceProperties(&p, 0) == hipSuccess) ncu = p.multiProcessorCount;
     printf("CUs %d\n", ncu);
-    const int iters = 200000;
-    for (int w : {4, 8}) {
-        run<1, 0>(w, iters, ncu);
-        run<2, 0>(w, iters, ncu);
-        run<4, 0>(w, iters, ncu);
+    const int iters = 100000;
+    for (int w : {4, 8, 12, 16}) {
+        run<4, 2>(w, iters, ncu);
+        run<8, 2>(w, iters, ncu);
+        run<16, 2>(w, iters, ncu);
         run<8, 0>(w, iters, ncu);
-        run<4, 1>(w, iters, ncu);
+        run<16, 0>(w, iters, ncu);
+        run<8, 1>(w, iters, ncu);
     }
     return 0;
 }

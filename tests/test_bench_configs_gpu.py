@@ -48,7 +48,12 @@ def test_benched_geometry_8192(k):
         it, res = g.solve_rb(itermax=kk)
         got = g.download(M.P)
         st = g.stats()
-    assert st["iters_per_pass"] == T
+    # one pass: T; 16 / 20 iterations on this 2^26-cell grid: the chained split
+    # ring's 10-iteration passes (misor_api.hip configure_tb short_all)
+    if k == "T":
+        assert st["iters_per_pass"] == T
+    else:
+        assert (st["iters_per_pass"], st["tb_variant"]) in ((T, 0), (10, 13)), st
     want = p.copy()
     it_ref, res_ref = orc.solve_rb(want, rhs, 1.0 / n, 1.0 / n, OMEGA, 1e-300, kk)
     assert it == it_ref == kk

@@ -172,7 +172,12 @@ int misor_poisson_init(misor_grid* g, double xlength, double ylength, int proble
 /* solveRB / solveRBA (assignment-4/src/solver.c:179-299): red-black SOR
  * with Neumann ghost copy after each iteration, until res < eps^2 or itermax.
  * *iters = iterations done (the reference prints it, :237), *res = final
- * residual (sum r^2 / (imax*jmax)).  Either output may be NULL. */
+ * residual (sum r^2 / (imax*jmax)).  Either output may be NULL.
+ * Decomposed: as the reference's MPI loop (assignment-5/skeleton/src/
+ * solver.c:603-607, an exchange opens every iteration) the solve leaves the
+ * final field's inter-rank halo to its next reader: misor_adapt_uv and a
+ * misor_download of MISOR_P exchange it first (2 deep), the next solve at its
+ * start; misor_gather reads owned cells only. */
 int misor_solve_rb(misor_grid* g, int* iters, double* res);
 /* the same with an explicit cap that overrides desc.itermax for this call */
 int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res);

@@ -322,3 +322,36 @@ def test_exchange_rank_fill(world, dims, depth):
                        if a0 <= gi <= a1 and b0 <= gj <= b1]
                 assert len(own) == 1, (gi, gj, own)
                 assert got[j, i] == code(own[0], gi, gj), (r, i, j, got[j, i], own[0])
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("T", [1, 4, 8])
+def test_halo_after_solve(world, T):
+    """A solve leaves the final field's halo to its next reader (misor_api.hip
+    p_halo): a download of p after a decomposed solve holds, in every cell of
+    the 2-deep halo, the neighbour's new value -- the whole local window of the
+    oracle's field, ghosts included -- and so does adaptUV's read of it (the
+    NS tests)"""
+    ni, nj = 300, 190
+    rng = np.random.default_rng(world * 10 + T)
+    p = rng.standard_normal((nj + 2, ni + 2))
+    rhs = rng.standard_normal((nj + 2, ni + 2))
+    want = p.copy()
+    orc.solve_rb(want, rhs, 1.0 / ni, 1.0 / nj, 1.9, 1e-300, 2 * T + 1)
+
+    def rank_fn(r, cid, dims):
+        with M.Grid(ni, nj, 1.0 / ni, 1.0 / nj, 1.9, 1e-300, 2 * T + 1, device=0, nranks=world,
+                    rank=r, comm_id=cid) as g:
+            g.set_tuning(M.TUNE_TSTEPS, T)
+            g.upload(M.P, local_window(p, g.loc))
+            g.upload(M.RHS, local_window(rhs, g.loc))
+            it, _ = g.solve_rb()
+            return g.loc, g.download(M.P), it
+
+    for loc, blk, it in run_ranks(world, rank_fn):
+        assert it == 2 * T + 1
+        w = local_window(want, loc)
+        # rows / columns 0 and n+1 of the window: the physical ghost copy or
+        # the neighbour's cells (the window's four corners left out)
+        assert np.array_equal(blk[1:-1, :], w[1:-1, :]), (loc.ioff, loc.joff)
+        assert np.array_equal(blk[:, 1:-1], w[:, 1:-1]), (loc.ioff, loc.joff)

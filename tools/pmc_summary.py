@@ -30,8 +30,19 @@ def rows(d, prefix, kernel):
     return out
 
 
+PER_PASS = [1]  # launches of one instantiation per pass (--launches-per-pass)
+
+
 def mean(v):
-    return sum(x[2] for x in v) / len(v)
+    """per pass: the mean over launches of each kernel instantiation, summed
+    over the instantiations (a chained pass of variant 0 launches its main and
+    edge kernels, rb_tbc_kernel<..., 0> and <..., 1>, once each), times the
+    launches per pass of one instantiation (the chained split ring runs its main
+    and edge lists as two launches of the same rb_tbhc_kernel)"""
+    by = {}
+    for name, _, val in v:
+        by.setdefault(name, []).append(val)
+    return sum(sum(x) / len(x) for x in by.values()) * PER_PASS[0]
 
 
 def main():
@@ -46,13 +57,16 @@ def main():
                     help="kernel name regex (default: the temporally blocked kernels, chained "
                          "rb_tbc_kernel or not, of ITERS iterations -- only full passes)")
     ap.add_argument("--rows", type=int, default=0)
+    ap.add_argument("--launches-per-pass", type=int, default=0,
+                    help="launches of one instantiation per pass (0: 2 for rb_tbhc_kernel, "
+                         "whose main and edge lists are two launches, else 1)")
     a = ap.parse_args()
     if a.iters == "all":
         ts = set()
         for path in glob.glob(os.path.join(a.dir, "**", "fetch*counter_collection.csv"),
                               recursive=True):
             for r in csv.DictReader(open(path)):
-                m = re.search(r"rb_tb[cxh]?_kernel<(\d+),", r["Kernel_Name"])
+                m = re.search(r"rb_tb(?:hc|[cxh])?_kernel<(\d+),", r["Kernel_Name"])
                 if m:
                     ts.add(int(m.group(1)))
         for t in sorted(ts):
@@ -62,8 +76,10 @@ def main():
 
 
 def summarise(a, iters, path_out):
-    kernel = a.kernel or r"rb_tb[cxh]?_kernel<%d," % iters
+    kernel = a.kernel or r"rb_tb(?:hc|[cxh])?_kernel<%d," % iters
     f = rows(a.dir, "fetch", kernel)
+    PER_PASS[0] = a.launches_per_pass or (2 if any("rb_tbhc_kernel" in x[0] for v in f.values()
+                                                   for x in v) else 1)
     w = rows(a.dir, "write", kernel)
     s = rows(a.dir, "sq", kernel)
     # full-iteration launches only (a capped solve's last pass may run fewer)
@@ -76,8 +92,10 @@ def summarise(a, iters, path_out):
     kname = fetch[0][0].split("(")[0].replace("void ", "")
     out = {
         "size": a.size, "nranks": a.nranks, "iters_per_pass": iters,
-        "kernel": kname, "chain": "rb_tbc_kernel" in kname,
+        "kernel": kname, "chain": bool(re.search(r"rb_tb(hc|c)_kernel", kname)),
         "rows_per_block": a.rows or None, "launches": len(fetch),
+        "launches_per_pass": PER_PASS[0],
+        "instantiations": sorted({x[0].split("(")[0].replace("void ", "") for x in fetch}),
         "fetch_size_kb_raw": mean(fetch), "write_size_kb": mean(write),
         "read_bytes_corrected": rd, "write_bytes": wr, "bytes_per_launch": rd + wr,
         "hbm_minimum_bytes_per_launch": hbm_min,

@@ -49,7 +49,15 @@ def main():
     ap.add_argument("--comm", action="store_true",
                     help="one-rank RCCL communicator: the decomposed, pipelined pass loop "
                          "(comm stream, all-reduce, split launches) without neighbours")
+    ap.add_argument("--sides", default=None,
+                    help="with --comm: the block's PHYSICAL sides (of LRBT; e.g. LB for "
+                         "rank 0 of the 4 x 2 split): the others are treated as bordering "
+                         "another rank (MISOR_PROXY_SIDES: halo cones, split launches, "
+                         "self-exchanges through the one-rank communicator; timing only)")
     args = ap.parse_args()
+    if args.sides is not None:
+        args.comm = True
+        os.environ["MISOR_PROXY_SIDES"] = args.sides or "-"
     if args.lib:
         M.LIBPATH = os.path.abspath(args.lib)
     n = args.size
@@ -100,8 +108,13 @@ def main():
                 g.set_tuning(M.TUNE_TB_PERSISTENT, pp)
                 g.set_tuning(M.TUNE_TB_RESERVE, rv)
                 g.set_tuning(M.TUNE_XCD_REMAP, x)
-                g.set_tuning(M.TUNE_TSTEPS, T)
-                g.set_tuning(M.TUNE_TB_VARIANT, v0 if v < 0 else v)
+                # (the variant first where T exceeds what the current one runs)
+                if T > 8:
+                    g.set_tuning(M.TUNE_TB_VARIANT, v0 if v < 0 else v)
+                    g.set_tuning(M.TUNE_TSTEPS, T)
+                else:
+                    g.set_tuning(M.TUNE_TSTEPS, T)
+                    g.set_tuning(M.TUNE_TB_VARIANT, v0 if v < 0 else v)
                 g.set_tuning(M.TUNE_TB_ROWS, r)
                 hrow[c] = g.get_tuning(M.TUNE_TB_ROWS)
                 g.reset_stats()

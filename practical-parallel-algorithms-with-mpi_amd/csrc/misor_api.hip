@@ -172,6 +172,7 @@ struct misor_grid {
     };
     struct ChainPlan {
         ChainList main, edge;
+        int reserve = -1;  // part 1 of a one-list plan: the slots it leaves to part 2
         bool built = false;
     } chain_plan[2][kMaxT + 1][3];  // [the default variant's / the split ring's][T][part]
     int* tb_work[4] = {nullptr, nullptr, nullptr, nullptr};  // main / edge x parts 0-1 / 2
@@ -814,8 +815,24 @@ static int chain_plan(misor_grid* g, int variant, int Tp, int part,
                      : variant == kHrTbVariant ? kHrChainEdgeCost
                                                : kChainEdgeCost;
     const int H = tp.rows_per_block;
+    // One list (the split ring, round 5): the edge columns' segments join the
+    // main list -- the same kernel runs both (sor_tbh.h hr_chain_run decides
+    // per strip), so one launch holds every slot and every workgroup can take
+    // or steal any segment; a separate edge launch held its slots idle once
+    // its list ran dry (profiles/r05_chain_trace_*).  And exactly one item per
+    // workgroup: the singles (non-steady block rows) first, then as many
+    // segments as workgroups are left, of equal cost -- a workgroup that
+    // finishes a single steals from the segments instead of taking a whole
+    // second one (more items than workgroups left a tail of ~one segment,
+    // half the pass on a rank block of 8192 x 16384).  MISOR_HR_PLAN=0: the
+    // two-list plan (A/B).
+    static const bool hr_one = [] {
+        const char* e = getenv("MISOR_HR_PLAN");
+        return !(e && e[0] == '0');
+    }();
+    const bool one = variant == kHrTbVariant && hr_one;
     std::vector<unsigned long long> singles;
-    double cost = 0;
+    double cost = 0, cost_singles = 0;
     long long Bm = 0, Be = 0;
     for (int bx = 0; bx < nbx; ++bx) {
         const bool ecol = edge_col(bx);
@@ -824,38 +841,79 @@ static int chain_plan(misor_grid* g, int variant, int Tp, int part,
             if (!steady(by)) {
                 singles.push_back(chain_word(bx, by, by + 1));
                 cost += E * (H + 4.0 * Tp) / H;
+                cost_singles += E * (H + 4.0 * Tp) / H;
                 ++Bm;
             } else {
                 cost += ecol ? E : 1.0;
-                ++(ecol ? Be : Bm);
+                ++(ecol && !one ? Be : Bm);
             }
         }
     }
     const int G = std::max(8, tb_resident(Tp, tp.variant));
-    const double per = std::max(1.0, cost / G);  // cost of one segment
-    std::vector<unsigned long long> edge, inner;  // inner: column-interleaved
-    std::vector<std::vector<unsigned long long>> col(nbx);
-    for (int bx = 0; bx < nbx; ++bx) {
-        const bool ecol = edge_col(bx);
-        const double c1 = ecol ? E : 1.0;
-        for (int by = 0; by < nby;) {
-            if (!in_part(bx, by) || !steady(by)) {
-                ++by;
-                continue;
+    // a pipelined pass's parts (1: interior blocks, 2: the blocks whose cone
+    // reads the halo, launched once the exchange is in): part 2 runs beside
+    // part 1 on the slots part 1 leaves free, so those are sized to its share
+    // of the pass's cost (at least MISOR_TUNE_TB_RESERVE, which also serves the
+    // exchange's kernels) and each part's items to its slots -- part 2's
+    // blocks then run as chained runs of the border columns instead of one
+    // warmed-up block per slot at the end of the pass
+    int Gp = std::max(8, G - (part == 1 ? g->tb_reserve : 0));
+    if (one && part != 0) {
+        double c12[3] = {0, 0, 0};
+        for (int bx = 0; bx < nbx; ++bx) {
+            const bool ecol = edge_col(bx);
+            for (int by = 0; by < nby; ++by)
+                c12[interior(bx, by) ? 1 : 2] +=
+                    !steady(by) ? E * (H + 4.0 * Tp) / H : ecol ? E : 1.0;
+        }
+        const int R = std::min(G / 2, std::max(g->tb_reserve,
+                                               (int)llround(G * c12[2] / (c12[1] + c12[2]))));
+        pl.reserve = R;
+        Gp = std::max(8, part == 1 ? G - R : R);
+    }
+    double per = std::max(1.0, cost / G);  // cost of one segment
+    // segments of one steady run of n blocks of cost c1 each
+    auto pieces = [&](int n, double c1) {
+        return std::min(n, std::max(1, (int)llround(n * c1 / per)));
+    };
+    auto each_run = [&](auto&& fn) {  // fn(bx, by, n, edge column)
+        for (int bx = 0; bx < nbx; ++bx) {
+            const bool ecol = edge_col(bx);
+            for (int by = 0; by < nby;) {
+                if (!in_part(bx, by) || !steady(by)) {
+                    ++by;
+                    continue;
+                }
+                int e = by;
+                while (e < nby && in_part(bx, e) && steady(e)) ++e;
+                fn(bx, by, e - by, ecol);
+                by = e;
             }
-            int e = by;
-            while (e < nby && in_part(bx, e) && steady(e)) ++e;
-            const int n = e - by;
-            const int k = std::min(n, std::max(1, (int)llround(n * c1 / per)));
-            for (int q = 0; q < k; ++q) {
-                const unsigned long long w = chain_word(
-                    bx, by + (int)((long long)n * q / k), by + (int)((long long)n * (q + 1) / k));
-                if (ecol) edge.push_back(w);
-                else col[bx].push_back(w);
+        }
+    };
+    if (one) {
+        const long long ns = (long long)singles.size();
+        if (ns < Gp / 2) {
+            per = std::max(1.0, (cost - cost_singles) / (double)(Gp - ns));
+            for (int guard = 0; guard < 200; ++guard) {  // at most Gp items in all
+                long long cnt = ns;
+                each_run([&](int, int, int n, bool ecol) { cnt += pieces(n, ecol ? E : 1.0); });
+                if (cnt <= Gp) break;
+                per *= 1.01;
             }
-            by = e;
         }
     }
+    std::vector<unsigned long long> edge, inner;  // inner: column-interleaved
+    std::vector<std::vector<unsigned long long>> col(nbx);
+    each_run([&](int bx, int by, int n, bool ecol) {
+        const int k = pieces(n, ecol ? E : 1.0);
+        for (int q = 0; q < k; ++q) {
+            const unsigned long long w = chain_word(
+                bx, by + (int)((long long)n * q / k), by + (int)((long long)n * (q + 1) / k));
+            if (ecol && !one) edge.push_back(w);
+            else col[bx].push_back(w);
+        }
+    });
     for (size_t q = 0;; ++q) {
         bool any = false;
         for (int bx = 0; bx < nbx; ++bx)
@@ -1861,6 +1919,7 @@ static int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* 
                 SweepParams tm = tp;
                 use(tm, pl->main);
                 tm.chain_edge = 0;
+                if (part == 1 && pl->reserve >= 0) tm.reserve = pl->reserve;
                 tm.reserve += pl->edge.blocks > 0 ? eg : 0;
                 const bool has_e = pl->edge.blocks > 0, has_m = pl->main.blocks > 0;
                 // (no edge list: the main kernel alone, on s)
@@ -2449,6 +2508,7 @@ int misor_set_tuning(misor_grid* g, int key, int value) {
     case MISOR_TUNE_TB_RESERVE:
         if (value < 0) return fail(MISOR_EINVAL, "reserve must be >= 0");
         g->tb_reserve = value;
+        drop_chain_plans(g);  // (the one-list plans count the workgroups left)
         return MISOR_OK;
     case MISOR_TUNE_NEAR_BAND:
         g->near_exp = value;

@@ -20,7 +20,9 @@ Fixtures:
                            oracle/_ref/libref3d.so) on its dcavity/canal .par at reduced
                            grids, 16 time steps: per-step iterations, p, u, v, w, t
   ns_seq_dcavity_lex_short.npz  the reference's own NS (assignment-5/sequential, its
-                           lexicographic `solve`) on its dcavity.par, te=0.05
+                           lexicographic `solve`) on its dcavity.par, te=0.05: p, u, v,
+                           t, and the per-step iteration counts of the restatement
+                           (iters_oracle: the shipped solve() reports none)
 plus reference data files copied verbatim (they are the reference's own
 fixtures): a4_p.dat, a4_init.dat, and assignment-5/sequential's dcavity.par,
 pressure.dat and velocity.dat (seq_*; the committed output of its te=10 run).
@@ -48,9 +50,18 @@ def lex_fixtures():
     for name in ("dcavity.par", "pressure.dat", "velocity.dat"):
         shutil.copyfile(os.path.join(SEQ, name), os.path.join(HERE, "seq_" + name))
     te = 0.05
-    n, iters, p, u, v, t = orc.ref_ns(os.path.join(SEQ, "dcavity.par"), te=te, solver=0)
+    n, _, p, u, v, t = orc.ref_ns(os.path.join(SEQ, "dcavity.par"), te=te, solver=0)
+    # per-step iteration counts: the reference's shipped solve() reports none
+    # (oracle/ref_glue.c), so they come from the restatement -- whose fields
+    # are checked against these reference fields bit for bit (test_oracle.py)
+    prm = orc.read_par(os.path.join(SEQ, "dcavity.par"))
+    prm["te"] = te
+    ns = orc.NS(prm)
+    n_o, iters_o, _ = ns.run(solver=0)
+    assert n_o == n and np.array_equal(ns.p, p) and np.array_equal(ns.u, u)
     np.savez_compressed(os.path.join(HERE, "ns_seq_dcavity_lex_short.npz"), steps=n,
-                        p=p, u=u, v=v, t=t, te=te)
+                        iters_oracle=np.asarray(iters_o, dtype=np.int32), p=p, u=u, v=v, t=t,
+                        te=te)
     print("ns_seq_dcavity_lex_short.npz", n, "steps")
 
 

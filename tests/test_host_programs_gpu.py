@@ -75,7 +75,10 @@ def test_exe_ns_decomposed_matches_single(golden, tmp_path, par, ranks):
     velocity.dat as on one GPU and takes the same pressure iterations per step"""
     name = par[3:]
     txt = open(os.path.join(golden, par)).read()
-    txt = re.sub(r"(?m)^te .*$", "te       0.3", txt)
+    # (dcavity on 4 in-process ranks: ~0.2 s a step on its small grid -- the
+    # transport's per-pass host barriers -- so a shorter run)
+    te = 0.15 if (par, ranks) == ("a6_dcavity.par", 4) else 0.3
+    txt = re.sub(r"(?m)^te .*$", "te       %r" % te, txt)
     runs = {}
     for n in (1, ranks):
         d = tmp_path / ("r%d" % n)

@@ -75,7 +75,8 @@ def test_lex_iteration_counts(n):
 def test_lex_ns_sequential_dcavity(golden):
     """the reference's own NS (assignment-5/sequential, lexicographic solve) on
     its dcavity.par for 400 steps: fields vs the reference build, per-step
-    iterations vs the oracle"""
+    iterations vs the restatement's (iters_oracle of the fixture: the shipped
+    solve() reports none; tests/golden/make_golden.py)"""
     z = np.load(os.path.join(golden, "ns_seq_dcavity_lex_short.npz"))
     prm = orc.read_par(os.path.join(golden, "seq_dcavity.par"))
     prm["te"] = float(z["te"])
@@ -83,10 +84,8 @@ def test_lex_ns_sequential_dcavity(golden):
     steps, iters, t = D.run(g, prm, solver="lex")
     fields = {k: g.download(fid) for k, fid in (("p", M.P), ("u", M.U), ("v", M.V))}
     g.close()
-    ns = orc.NS(prm)
-    steps_o, iters_o, t_o = ns.run(solver=0)
-    assert steps == steps_o == int(z["steps"])
-    assert np.array_equal(iters, iters_o)
+    assert steps == int(z["steps"])
+    assert np.array_equal(iters, z["iters_oracle"]), np.argwhere(iters != z["iters_oracle"])[:5]
     for k in ("p", "u", "v"):
         err = np.abs(fields[k] - z[k]).max() / np.abs(z[k]).max()
         assert err <= 1e-12, (k, err)

@@ -165,6 +165,9 @@ def test_lex_ns_oracle_vs_reference_fixture(golden):
     assert steps == int(z["steps"])
     for k in ("p", "u", "v"):
         assert np.array_equal(getattr(ns, k), z[k]), k
+    # the per-step iteration counts the GPU test checks against (the shipped
+    # solve() reports none: they are this run's, tests/golden/make_golden.py)
+    assert np.array_equal(iters, z["iters_oracle"])
 
 
 @pytest.mark.parametrize("ni,nj,threads", [(37, 23, 3), (64, 64, 8), (100, 100, 4), (9, 5, 8)])

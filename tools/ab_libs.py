@@ -40,14 +40,15 @@ def main():
                 print(out.stderr[-2000:], file=sys.stderr)
                 raise SystemExit("child failed for %s" % c)
             d = json.loads(out.stdout.strip().splitlines()[-1])
-            res.setdefault(c, []).append(d["ms_iter"])
+            res.setdefault(c, []).append((d["ms_iter"], d.get("wall_iter", 0.0)))
             hashes.add((T, d["hash"]))
         print("round %d done" % r, file=sys.stderr, flush=True)
     cells = float(a.ni or a.size) * (a.nj or a.size)
-    for c, ms in res.items():
-        ms = sorted(ms)
-        print("%-60s ms/iter med %.4f min %.4f  MLUP/s %.0f" % (
-            c, ms[len(ms) // 2], ms[0], cells / (ms[len(ms) // 2] * 1e-3) / 1e6))
+    for c, v in res.items():
+        ms = sorted(x[0] for x in v)
+        wl = sorted(x[1] for x in v)
+        print("%-60s ms/iter (events) med %.4f min %.4f | wall med %.4f  MLUP/s (wall) %.0f" % (
+            c, ms[len(ms) // 2], ms[0], wl[len(wl) // 2], cells / (wl[len(wl) // 2] * 1e-3) / 1e6))
     by_t = {}
     for t, h in hashes:
         by_t.setdefault(t, set()).add(h)

@@ -131,11 +131,133 @@ __global__ __launch_bounds__(kLexThreads) void lex_solve_kernel(
     }
 }
 
+// The same solve as ONE wave with no barriers (round 5), for grids whose p
+// fits the LDS and has at most 64 * kLexWaveG rows (the reference's 100 x 100
+// .par grids): lane L owns rows L + 1, L + 65, ... and row j trails row j - 1
+// by one step -- cell (i, j) is updated at step (i - 1) + (j - 1) -- so at
+// every step its NEW left neighbour is the lane's own store of the step
+// before, its NEW lower neighbour the store of lane L - 1 (lane 63 for the
+// next row group) of the step before, and its right and upper neighbours are
+// still OLD: exactly the lexicographic order, with no workgroup barrier
+// between the diagonals (one wave's LDS operations execute in program order).
+// rhs is loaded one step ahead.  Per-cell expression: lex_cell.
+constexpr int kLexWaveG = 4;
+
+template <bool XORDER, int GM>
+__global__ __launch_bounds__(64) void lex_wave_kernel(double* __restrict__ p_glob,
+                                                      const double* __restrict__ rhs_glob, int ni,
+                                                      int nj, long long pitch, double idx2,
+                                                      double idy2, double factor, double cells,
+                                                      DevState* st) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int lane = threadIdx.x;
+    double* const pg = p_glob + (long long)kYOff * pitch + kXOff;  // cell (0,0) in HBM
+    const double* const rg = rhs_glob + (long long)kYOff * pitch + kXOff;
+    const long long W = ni + 2;
+    double* const P = lds;
+    const long long ncell = W * (nj + 2);
+    for (long long k = lane; k < ncell; k += 64) {
+        const int i = (int)(k % W), j = (int)(k / W);
+        P[k] = pg[(long long)j * pitch + i];
+    }
+    const double epssq = st->epssq;
+    const int itermax = st->itermax;
+    const int nsteps = ni + nj - 1;
+    double res = 1.0;
+    int it = 0;
+    while ((res >= epssq) && (it < itermax)) {
+        double acc = 0.0;
+        // rhs of each row's cell at step 0: i = 2 - j (row 1 only)
+        double rn[GM];
+#pragma unroll
+        for (int g = 0; g < GM; ++g) {
+            const int j = lane + 1 + 64 * g, i = 2 - j;
+            rn[g] = (j <= nj && i >= 1) ? rg[(long long)j * pitch + i] : 0.0;
+        }
+        for (int s = 0; s < nsteps; ++s) {
+            double rc[GM];
+#pragma unroll
+            for (int g = 0; g < GM; ++g) {
+                rc[g] = rn[g];
+                const int j = lane + 1 + 64 * g, i = s + 3 - j;  // next step's cell
+                rn[g] = (j <= nj && i >= 1 && i <= ni) ? rg[(long long)j * pitch + i] : 0.0;
+            }
+#pragma unroll
+            for (int g = 0; g < GM; ++g) {
+                const int j = lane + 1 + 64 * g, i = s + 2 - j;
+                if (j <= nj && i >= 1 && i <= ni) {
+                    const long long k = (long long)j * W + i;
+                    const double c = P[k];
+                    double xt, yt;
+                    if (XORDER) {  // assignment-5/sequential/src/solver.c:162-164
+                        xt = (P[k + 1] - 2.0 * c) + P[k - 1];
+                        yt = (P[k + W] - 2.0 * c) + P[k - W];
+                    } else {  // assignment-4/src/solver.c:149-151
+                        xt = (P[k - 1] - 2.0 * c) + P[k + 1];
+                        yt = (P[k - W] - 2.0 * c) + P[k + W];
+                    }
+                    const double r = rc[g] - (xt * idx2 + yt * idy2);
+                    P[k] = c - (factor * r);
+                    acc += r * r;
+                }
+            }
+            // the next step reads what this one stored (other lanes' rows)
+            asm volatile("" ::: "memory");
+        }
+        // Neumann ghost copy: rows, then columns (corners untouched)
+        for (int i = 1 + lane; i <= ni; i += 64) {
+            P[i] = P[W + i];
+            P[(long long)(nj + 1) * W + i] = P[(long long)nj * W + i];
+        }
+        asm volatile("" ::: "memory");
+        for (int j = 1 + lane; j <= nj; j += 64) {
+            P[(long long)j * W] = P[(long long)j * W + 1];
+            P[(long long)j * W + ni + 1] = P[(long long)j * W + ni];
+        }
+        asm volatile("" ::: "memory");
+        res = wave_sum(acc) / cells;
+        ++it;
+    }
+    for (long long k = lane; k < ncell; k += 64) {
+        const int i = (int)(k % W), j = (int)(k / W);
+        pg[(long long)j * pitch + i] = P[k];
+    }
+    if (lane == 0) {
+        st->it = it;
+        st->res = res;
+        st->done = 1;
+    }
+}
+
 void launch_solve_lex(hipStream_t s, double* p, const double* rhs, int ni, int nj,
                       long long pitch, double idx2, double idy2, double factor, double cells,
                       int xorder, DevState* st) {
     const size_t need = sizeof(double) * (32 + (size_t)(ni + 2) * (nj + 2));
     const int use_lds = need <= 160 * 1024;
+    static const bool wave = [] {  // MISOR_LEX_WAVE=0: the workgroup form (A/B)
+        const char* e = getenv("MISOR_LEX_WAVE");
+        return !(e && e[0] == '0');
+    }();
+    if (wave && use_lds && nj <= 64 * kLexWaveG) {
+        const size_t lb = sizeof(double) * (size_t)(ni + 2) * (nj + 2);
+        auto go = [&](auto kernel) {
+            (void)hipFuncSetAttribute((const void*)kernel,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
+            hipLaunchKernelGGL(kernel, dim3(1), dim3(64), lb, s, p, rhs, ni, nj, pitch, idx2,
+                               idy2, factor, cells, st);
+        };
+        const int G = (nj + 63) / 64;
+        if (xorder) {
+            if (G <= 1) go(lex_wave_kernel<true, 1>);
+            else if (G <= 2) go(lex_wave_kernel<true, 2>);
+            else go(lex_wave_kernel<true, kLexWaveG>);
+        } else {
+            if (G <= 1) go(lex_wave_kernel<false, 1>);
+            else if (G <= 2) go(lex_wave_kernel<false, 2>);
+            else go(lex_wave_kernel<false, kLexWaveG>);
+        }
+        return;
+    }
     const int diag = ni < nj ? ni : nj;
     const int nt = std::min(kLexThreads, std::max(64, (diag + 63) / 64 * 64));
     const size_t lds = use_lds ? need : sizeof(double) * 32;

@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 o=gpurun_out/r5f_plan.txt
 : > $o
-timeout -k 10 400 python -u -m pytest tests/test_tb_variants_gpu.py tests/test_fullfield_gpu.py -x -q --timeout 300 --timeout-method thread > gpurun_out/r5f_tests.log 2>&1 || { tail -30 gpurun_out/r5f_tests.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests/test_lex_gpu.py tests/test_tb_variants_gpu.py tests/test_fullfield_gpu.py tests/test_decomposed_gpu.py -x -q --durations=5 --timeout 300 --timeout-method thread > gpurun_out/r5f_tests.log 2>&1 || { tail -30 gpurun_out/r5f_tests.log; exit 1; }
 tail -2 gpurun_out/r5f_tests.log
 for sh in "--ni 8192 --nj 16384" "--ni 16384 --nj 8192" "--ni 16384 --nj 16384" ""; do
 echo "== $sh" | tee -a $o

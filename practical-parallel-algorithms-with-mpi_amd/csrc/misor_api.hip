@@ -157,7 +157,8 @@ struct misor_grid {
     bool tb_persistent = true;    // MISOR_TUNE_TB_PERSISTENT: work-queue launches
     int tb_reserve = kTbReserve;  // MISOR_TUNE_TB_RESERVE: slots a pipelined interior launch
                                   // leaves to the communication / edge-block streams
-    int* tb_queue = nullptr;      // 8 per-XCD block counters of a persistent launch
+    bool finish_merge = true;     // finish2 in one launch (tb_queue[9]: its counter)
+    int* tb_queue = nullptr;      // 8 per-XCD block counters of a persistent launch + its exit count
     // chained passes (sor_tb.h rb_tbc_kernel; MISOR_TUNE_TB_CHAIN): the initial
     // segment list of every pass length and part (0: whole pass, 1: interior
     // blocks, 2: edge blocks of a pipelined decomposed pass), and two work
@@ -815,22 +816,25 @@ static int chain_plan(misor_grid* g, int variant, int Tp, int part,
                      : variant == kHrTbVariant ? kHrChainEdgeCost
                                                : kChainEdgeCost;
     const int H = tp.rows_per_block;
-    // One list (the split ring, round 5): the edge columns' segments join the
-    // main list -- the same kernel runs both (sor_tbh.h hr_chain_run decides
-    // per strip), so one launch holds every slot and every workgroup can take
-    // or steal any segment; a separate edge launch held its slots idle once
-    // its list ran dry (profiles/r05_chain_trace_*).  And exactly one item per
-    // workgroup: the singles (non-steady block rows) first, then as many
-    // segments as workgroups are left, of equal cost -- a workgroup that
-    // finishes a single steals from the segments instead of taking a whole
-    // second one (more items than workgroups left a tail of ~one segment,
-    // half the pass on a rank block of 8192 x 16384).  MISOR_HR_PLAN=0: the
-    // two-list plan (A/B).
-    static const bool hr_one = [] {
+    // Plan forms of the split ring (MISOR_HR_PLAN, A/B experiments; round 5):
+    //  0: main and edge lists, segments of cost / resident workgroups;
+    //  1: one list -- the edge columns' segments join the main list (the same
+    //     kernel runs both, sor_tbh.h hr_chain_run decides per strip), exactly
+    //     one item per workgroup (the singles first, then as many segments as
+    //     workgroups are left) -- measured 1-3% SLOWER than 0 at 32768^2 and
+    //     on the 8-GPU rank block (profiles/r05_hr_plan_ab.txt): edge-column
+    //     blocks ran 1.4x longer among the main list's;
+    //  2 (default): the two lists of 0 with the pipelined pass's part-2 slots
+    //     sized to its cost share (below): the 8-GPU rank block's pipelined
+    //     loop 0.130-0.135 against 0.145-0.147 ms per iteration with physical
+    //     left and bottom sides, 0.130-0.131 against 0.136-0.138 with the bottom
+    //     one only (profiles/r05_reserve_ab.txt).
+    static const int hr_plan = [] {
         const char* e = getenv("MISOR_HR_PLAN");
-        return !(e && e[0] == '0');
+        return e ? atoi(e) : 2;
     }();
-    const bool one = variant == kHrTbVariant && hr_one;
+    const bool one = variant == kHrTbVariant && hr_plan == 1;
+    const bool sized = variant == kHrTbVariant && (hr_plan == 1 || hr_plan == 2) && part != 0;
     std::vector<unsigned long long> singles;
     double cost = 0, cost_singles = 0;
     long long Bm = 0, Be = 0;
@@ -857,8 +861,8 @@ static int chain_plan(misor_grid* g, int variant, int Tp, int part,
     // exchange's kernels) and each part's items to its slots -- part 2's
     // blocks then run as chained runs of the border columns instead of one
     // warmed-up block per slot at the end of the pass
-    int Gp = std::max(8, G - (part == 1 ? g->tb_reserve : 0));
-    if (one && part != 0) {
+    int Gp = G;
+    if (sized) {
         double c12[3] = {0, 0, 0};
         for (int bx = 0; bx < nbx; ++bx) {
             const bool ecol = edge_col(bx);
@@ -871,7 +875,7 @@ static int chain_plan(misor_grid* g, int variant, int Tp, int part,
         pl.reserve = R;
         Gp = std::max(8, part == 1 ? G - R : R);
     }
-    double per = std::max(1.0, cost / G);  // cost of one segment
+    double per = std::max(1.0, cost / Gp);  // cost of one segment
     // segments of one steady run of n blocks of cost c1 each
     auto pieces = [&](int n, double c1) {
         return std::min(n, std::max(1, (int)llround(n * c1 / per)));
@@ -892,6 +896,7 @@ static int chain_plan(misor_grid* g, int variant, int Tp, int part,
         }
     };
     if (one) {
+        if (!sized) Gp = std::max(8, G - (part == 1 ? g->tb_reserve : 0));
         const long long ns = (long long)singles.size();
         if (ns < Gp / 2) {
             per = std::max(1.0, (cost - cost_singles) / (double)(Gp - ns));
@@ -1202,7 +1207,8 @@ int misor_create(misor_grid** out, const misor_desc* d) {
         tp.int_lo_j = sp.ghost_bottom ? -kBig : 1;
         tp.int_hi_j = sp.ghost_top ? kBig : L.nj;
     }
-    if (hipMalloc(&g->tb_queue, 8 * sizeof(int)) != hipSuccess ||
+    if (hipMalloc(&g->tb_queue, 16 * sizeof(int)) != hipSuccess ||
+        hipMemsetAsync(g->tb_queue, 0, 16 * sizeof(int), g->stream) != hipSuccess ||
         hipMalloc(&g->st, sizeof(DevState)) != hipSuccess ||
         hipHostMalloc(&g->st_host, sizeof(DevState), hipHostMallocDefault) != hipSuccess)
         CREATE_FAIL(MISOR_ENOMEM, "state allocation failed");
@@ -1297,6 +1303,9 @@ int misor_create(misor_grid** out, const misor_desc* d) {
     {
         const char* e = getenv("MISOR_FINISH2");
         g->finish2 = !(e && e[0] == '0');
+        // the loop test in the partial-sum launch's last workgroup (A/B: 0)
+        e = getenv("MISOR_FINISH_MERGE");
+        g->finish_merge = !(e && e[0] == '0');
         e = getenv("MISOR_NS_FUSE");  // A/B switch (bench.py --workload ns)
         g->ns_fuse = !(e && e[0] == '0');
     }
@@ -2143,7 +2152,8 @@ static int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* 
                 launch_decide(g->stream, g->st, Tk, cells);
             } else if (g->finish2) {
                 launch_finish2(g->stream, g->partials, nparts_of(Tk), Tk, g->st, cells,
-                               g->partials + 2 * (long long)g->partials_cap);
+                               g->partials + 2 * (long long)g->partials_cap,
+                               g->finish_merge ? g->tb_queue + 9 : nullptr);
             } else {
                 launch_finish(g->stream, g->partials, nparts_of(Tk), Tk, g->st, cells, 1);
             }

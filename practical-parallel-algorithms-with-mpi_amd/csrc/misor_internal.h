@@ -236,8 +236,10 @@ void launch_decide(hipStream_t s, DevState* st, int T, double cells);
 // single-rank loop test in two levels (chunk sums, then the finish kernel over
 // kFinishChunks values per stage); scratch holds kMaxT * kFinishChunks doubles
 constexpr int kFinishChunks = 32;
+// count: a zeroed device int -- the partial-sum launch's last workgroup then
+// runs the loop test itself (one launch); nullptr: a second, finish launch
 void launch_finish2(hipStream_t s, const double* partials, int nparts, int T, DevState* st,
-                    double cells, double* scratch);
+                    double cells, double* scratch, int* count);
 // queue: 8 device ints (zeroed by the launch) for a persistent launch whose
 // workgroups take blocks from per-XCD queues; nullptr: one workgroup per block
 void launch_tb(hipStream_t s, int T, const SweepParams& prm, const double* src, double* dst,

@@ -323,13 +323,18 @@ __global__ __launch_bounds__(kLanes* WAVES) void rb_sweep_kernel(
 // per SIMD) could wait for a whole CU to drain; on the decomposed pipeline this
 // kernel runs on the comm stream beside the next pass's sweep.
 constexpr int kFinishThreads = 256;
-__global__ __launch_bounds__(kFinishThreads) void rb_finish_kernel(
-    const double* __restrict__ partials, int n, int T, DevState* st, double cells, int decide) {
+// SC1: the partials were handed over by other workgroups of the same launch
+// (rb_partsum_kernel's last workgroup): relaxed agent-scope loads (sc1)
+template <bool SC1>
+__device__ __forceinline__ void finish_body(const double* __restrict__ partials, int n, int T,
+                                            DevState* st, double cells, int decide,
+                                            double (&sh)[kMaxT][kFinishThreads],
+                                            double (&tot)[kMaxT]) {
     constexpr int NT = kFinishThreads;
-    __shared__ double sh[kMaxT][NT];
-    __shared__ double tot[kMaxT];
-    if (st->done) return;
     const int t = threadIdx.x;
+    auto ld = [&](const double* q) {
+        return SC1 ? __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *q;
+    };
     // all T groups in one strided pass, four strides per trip with separate
     // accumulators (4T independent loads in flight per thread), combined in a
     // fixed order
@@ -342,17 +347,17 @@ __global__ __launch_bounds__(kFinishThreads) void rb_finish_kernel(
         for (int g = 0; g < kMaxT; ++g) {
             if (g < T) {
                 const double* q = partials + (long long)g * n + k;
-                s[g] += q[0];
-                s1[g] += q[NT];
-                s2[g] += q[2 * NT];
-                s3[g] += q[3 * NT];
+                s[g] += ld(q);
+                s1[g] += ld(q + NT);
+                s2[g] += ld(q + 2 * NT);
+                s3[g] += ld(q + 3 * NT);
             }
         }
     }
     for (; k < n; k += NT) {
 #pragma unroll
         for (int g = 0; g < kMaxT; ++g)
-            if (g < T) s[g] += partials[(long long)g * n + k];
+            if (g < T) s[g] += ld(partials + (long long)g * n + k);
     }
 #pragma unroll
     for (int g = 0; g < kMaxT; ++g) s[g] = (s[g] + s1[g]) + (s2[g] + s3[g]);
@@ -398,14 +403,29 @@ __global__ __launch_bounds__(kFinishThreads) void rb_finish_kernel(
     }
 }
 
+__global__ __launch_bounds__(kFinishThreads) void rb_finish_kernel(
+    const double* __restrict__ partials, int n, int T, DevState* st, double cells, int decide) {
+    __shared__ double sh[kMaxT][kFinishThreads];
+    __shared__ double tot[kMaxT];
+    if (st->done) return;
+    finish_body<false>(partials, n, T, st, cells, decide, sh, tot);
+}
+
 // Single-rank loop test, first level: workgroup (c, g) sums chunk c of stage
 // g's per-workgroup partials in a fixed order (strided by thread, then a
 // tree), so the finish kernel reads kFinishChunks values per stage instead of
 // one per sweep workgroup (14k at 32768^2: 65 -> ~10 us per pass)
+// count != nullptr: the launch's last workgroup also runs the loop test
+// (rb_finish_kernel, one launch per pass instead of two); T, cells: its
+// arguments
 __global__ __launch_bounds__(256) void rb_partsum_kernel(const double* __restrict__ partials,
                                                          int n, const DevState* __restrict__ st,
-                                                         double* __restrict__ out) {
+                                                         double* __restrict__ out, int* count,
+                                                         int T, double cells) {
     __shared__ double sh[256];
+    __shared__ int is_last;
+    // (st->done is the same for the whole launch: only its last workgroup
+    // writes it, after every other one's add)
     if (st->done) return;
     const int c = blockIdx.x, g = blockIdx.y, t = threadIdx.x;
     const int lo = (int)((long long)n * c / kFinishChunks);
@@ -427,16 +447,42 @@ __global__ __launch_bounds__(256) void rb_partsum_kernel(const double* __restric
     }
     if (t < 64) {
         const double v = wave_sum(sh[t]);
-        if (t == 0) out[g * kFinishChunks + c] = v;
+        if (t == 0) {
+            if (!count) {
+                out[g * kFinishChunks + c] = v;
+            } else {
+                // hand-off to the launch's last workgroup (MISOR_MICROARCH.md
+                // valid forms, row 1): an sc1 store, drained, then one lane's
+                // agent-scope add to one counter; the workgroup whose add came
+                // last reads every value with sc1 loads
+                __hip_atomic_store(out + g * kFinishChunks + c, v, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const int k = __hip_atomic_fetch_add(count, 1, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+                is_last = k == (int)(gridDim.x * gridDim.y) - 1;
+            }
+        }
+    }
+    if (!count) return;
+    __syncthreads();
+    if (!is_last) return;
+    // the loop test of the pass (rb_finish_kernel), then the counter for the next
+    {
+        __shared__ double fsh[kMaxT][kFinishThreads];
+        __shared__ double tot[kMaxT];
+        finish_body<true>(out, kFinishChunks, T, const_cast<DevState*>(st), cells, 1, fsh, tot);
+        if (t == 0) __hip_atomic_store(count, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
 void launch_finish2(hipStream_t s, const double* partials, int nparts, int T, DevState* st,
-                    double cells, double* scratch) {
+                    double cells, double* scratch, int* count) {
     hipLaunchKernelGGL(rb_partsum_kernel, dim3(kFinishChunks, T), dim3(256), 0, s, partials,
-                       nparts, st, scratch);
-    hipLaunchKernelGGL(rb_finish_kernel, dim3(1), dim3(kFinishThreads), 0, s, scratch,
-                       kFinishChunks, T, st, cells, 1);
+                       nparts, st, scratch, count, T, cells);
+    if (!count)
+        hipLaunchKernelGGL(rb_finish_kernel, dim3(1), dim3(kFinishThreads), 0, s, scratch,
+                           kFinishChunks, T, st, cells, 1);
 }
 
 int sweep_waves(int variant) { return kSweepVariants[variant].waves; }

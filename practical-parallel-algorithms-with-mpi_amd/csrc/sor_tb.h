@@ -1338,10 +1338,23 @@ __global__ __launch_bounds__(kLanes* WAVES, 2) void rb_tb_kernel(
     const DevState* __restrict__ st, int force, int* __restrict__ queue) {
     __shared__ double wsum[T][WAVES];
     __shared__ int ticket;
-    if (!force && st->done) return;
-    for_each_block(prm, queue, &ticket, [&](int L) {
-        tb_block<T, WAVES, D, BP, P2>(prm, src, dst, rhs, partials, L, wsum);
-    });
+    if (force || !st->done) {
+        for_each_block(prm, queue, &ticket, [&](int L) {
+            tb_block<T, WAVES, D, BP, P2>(prm, src, dst, rhs, partials, L, wsum);
+        });
+    }
+    // Persistent launch: the queue resets itself for the next one (instead of
+    // a memset launch before every pass).  queue[8] counts the workgroups that
+    // are done with the ticket counters -- every one of them, those that found
+    // the solve done included -- and the last one zeroes all nine.  Its
+    // atomics (agent scope) come after every other workgroup's last ticket:
+    // each of those took its returned value before leaving the loop.
+    if (queue && threadIdx.x == 0) {
+        if (atomicAdd(&queue[8], 1) == (int)gridDim.x - 1) {
+#pragma unroll
+            for (int x = 0; x < 9; ++x) atomicExch(&queue[x], 0);
+        }
+    }
 }
 
 

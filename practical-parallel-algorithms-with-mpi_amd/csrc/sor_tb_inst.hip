@@ -51,10 +51,8 @@ void MISOR_CAT(launch_tb_t, MISOR_TB_T)(hipStream_t s, const SweepParams& prm,
                                         int* queue) {
     auto go = [&](auto kernel, int threads, int resident) {
         int grid = prm.nblocks;
-        if (queue) {
-            (void)hipMemsetAsync(queue, 0, 8 * sizeof(int), s);
-            grid = std::min(grid, std::max(8, resident - prm.reserve));
-        }
+        // (queue: zero at creation, reset by the kernel's last workgroup)
+        if (queue) grid = std::min(grid, std::max(8, resident - prm.reserve));
         hipLaunchKernelGGL(kernel, dim3(grid), dim3(threads), 0, s, prm, src, dst, rhs, partials,
                            st, force, queue);
     };

@@ -135,12 +135,13 @@ __global__ __launch_bounds__(kLexThreads) void lex_solve_kernel(
 // fits the LDS and has at most 64 * kLexWaveG rows (the reference's 100 x 100
 // .par grids): lane L owns rows L + 1, L + 65, ... and row j trails row j - 1
 // by one step -- cell (i, j) is updated at step (i - 1) + (j - 1) -- so at
-// every step its NEW left neighbour is the lane's own store of the step
-// before, its NEW lower neighbour the store of lane L - 1 (lane 63 for the
-// next row group) of the step before, and its right and upper neighbours are
-// still OLD: exactly the lexicographic order, with no workgroup barrier
-// between the diagonals (one wave's LDS operations execute in program order).
-// rhs is loaded one step ahead.  Per-cell expression: lex_cell.
+// every step its NEW left neighbour is the lane's own result of the step
+// before (a register), its NEW lower neighbour the result of lane L - 1 (lane
+// 63 of the row group below, for lane 0) of the step before (a DPP lane
+// rotation), and its right and upper neighbours are still OLD: exactly the
+// lexicographic order, with no barrier and no LDS round trip on the step's
+// dependency chain.  The old operands and rhs are loaded one step ahead; the
+// new values go to LDS for the next sweep.  Per-cell expression: lex_cell's.
 constexpr int kLexWaveG = 4;
 
 template <bool XORDER, int GM>
@@ -165,45 +166,77 @@ __global__ __launch_bounds__(64) void lex_wave_kernel(double* __restrict__ p_glo
     const int nsteps = ni + nj - 1;
     double res = 1.0;
     int it = 0;
+    // the operands of a row's cell at one step: rhs and the OLD values of the
+    // cell, its right and upper neighbours, and the ghosts a first column /
+    // first row reads (left P(0, j), lower P(i, 0)); loaded one step ahead --
+    // nothing this sweep writes before that step changes them
+    struct Ops {
+        double rh, c, r, u, gl, gd;
+    };
+    auto load_ops = [&](int i, int j) {
+        Ops o{0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+        if (j <= nj && i >= 1 && i <= ni) {
+            const long long k = (long long)j * W + i;
+            o.rh = rg[(long long)j * pitch + i];
+            o.c = P[k];
+            o.r = P[k + 1];
+            o.u = P[k + W];
+            o.gl = P[k - 1];  // (a ghost only where i == 1)
+            o.gd = P[k - W];  // (a ghost only where j == 1)
+        }
+        return o;
+    };
     while ((res >= epssq) && (it < itermax)) {
         double acc = 0.0;
-        // rhs of each row's cell at step 0: i = 2 - j (row 1 only)
-        double rn[GM];
+        Ops nx[GM];
+        double prev[GM];  // each row's result of the previous step: its NEW P(i-1, j)
 #pragma unroll
         for (int g = 0; g < GM; ++g) {
-            const int j = lane + 1 + 64 * g, i = 2 - j;
-            rn[g] = (j <= nj && i >= 1) ? rg[(long long)j * pitch + i] : 0.0;
+            const int j = lane + 1 + 64 * g;
+            nx[g] = load_ops(2 - j, j);
+            prev[g] = 0.0;
         }
         for (int s = 0; s < nsteps; ++s) {
-            double rc[GM];
+            Ops cur[GM];
 #pragma unroll
             for (int g = 0; g < GM; ++g) {
-                rc[g] = rn[g];
-                const int j = lane + 1 + 64 * g, i = s + 3 - j;  // next step's cell
-                rn[g] = (j <= nj && i >= 1 && i <= ni) ? rg[(long long)j * pitch + i] : 0.0;
+                cur[g] = nx[g];
+                const int j = lane + 1 + 64 * g;
+                nx[g] = load_ops(s + 3 - j, j);  // next step's cell (i + 1, j)
             }
+            // NEW P(i, j - 1): lane L - 1's result of the previous step (lane 63's
+            // of the row group below for lane 0) -- a DPP lane rotation
+            double rot[GM];
+#pragma unroll
+            for (int g = 0; g < GM; ++g)
+                rot[g] = __hiloint2double(
+                    __builtin_amdgcn_mov_dpp(__double2hiint(prev[g]), 0x13C, 0xf, 0xf, false),
+                    __builtin_amdgcn_mov_dpp(__double2loint(prev[g]), 0x13C, 0xf, 0xf, false));
 #pragma unroll
             for (int g = 0; g < GM; ++g) {
                 const int j = lane + 1 + 64 * g, i = s + 2 - j;
                 if (j <= nj && i >= 1 && i <= ni) {
-                    const long long k = (long long)j * W + i;
-                    const double c = P[k];
+                    const Ops& o = cur[g];
+                    const double lft = i == 1 ? o.gl : prev[g];
+                    const double dwn = j == 1 ? o.gd : (lane == 0 ? rot[g > 0 ? g - 1 : 0] : rot[g]);
+                    const double c = o.c;
                     double xt, yt;
                     if (XORDER) {  // assignment-5/sequential/src/solver.c:162-164
-                        xt = (P[k + 1] - 2.0 * c) + P[k - 1];
-                        yt = (P[k + W] - 2.0 * c) + P[k - W];
+                        xt = (o.r - 2.0 * c) + lft;
+                        yt = (o.u - 2.0 * c) + dwn;
                     } else {  // assignment-4/src/solver.c:149-151
-                        xt = (P[k - 1] - 2.0 * c) + P[k + 1];
-                        yt = (P[k - W] - 2.0 * c) + P[k + W];
+                        xt = (lft - 2.0 * c) + o.r;
+                        yt = (dwn - 2.0 * c) + o.u;
                     }
-                    const double r = rc[g] - (xt * idx2 + yt * idy2);
-                    P[k] = c - (factor * r);
+                    const double r = o.rh - (xt * idx2 + yt * idy2);
+                    const double v = c - (factor * r);
+                    P[(long long)j * W + i] = v;
+                    prev[g] = v;
                     acc += r * r;
                 }
             }
-            // the next step reads what this one stored (other lanes' rows)
-            asm volatile("" ::: "memory");
         }
+        asm volatile("" ::: "memory");
         // Neumann ghost copy: rows, then columns (corners untouched)
         for (int i = 1 + lane; i <= ni; i += 64) {
             P[i] = P[W + i];

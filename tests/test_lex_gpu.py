@@ -42,10 +42,8 @@ def test_lex_poisson_par_reproduces_committed_pdat(golden):
                                    (139, 139), (3, 257), (20, 300), (150, 141), (301, 40)])
 @pytest.mark.parametrize("xorder", [0, 1])
 def test_lex_random_fields_vs_oracle(ni, nj, xorder):
-    """up to 256 rows in LDS: the single-wave form (lex_wave_kernel; 65 / 129
-    rows: the lane 63 -> lane 0 hand-off between row groups); (3,257) and
-    (20,300): the workgroup form in LDS; (150,141) and (301,40) do not fit in
-    LDS: the HBM-resident workgroup form"""
+    """p in LDS (workgroup sized to the longest diagonal: 64 .. 1024 threads);
+    (150,141) and (301,40) do not fit in LDS: the HBM-resident form"""
     rng = np.random.default_rng(ni * 31 + nj + xorder)
     p = rng.standard_normal((nj + 2, ni + 2))
     rhs = rng.standard_normal((nj + 2, ni + 2))

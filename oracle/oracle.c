@@ -379,6 +379,11 @@ int orc_ns_run(orc_ns* s, int solver, int max_steps, int* iters, int cap,
         if (solver == 1)
             it = orc_solve_rb(s->imax, s->jmax, s->dx, s->dy, s->omega, s->eps,
                               s->itermax, s->p, s->rhs, NULL);
+        else if (solver == 2) /* the same solveRB on 16 threads over row bands
+                               * (oracle_mt.c: p bit-identical, the residual summed
+                               * in another order) -- large grids in the tests */
+            it = orc_solve_rb_mt(s->imax, s->jmax, s->dx, s->dy, s->omega, s->eps,
+                                 s->itermax, s->p, s->rhs, NULL, 16);
         else
             it = orc_solve_lex(s->imax, s->jmax, s->dx, s->dy, s->omega, s->eps,
                                s->itermax, 1, s->p, s->rhs, NULL);

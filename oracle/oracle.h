@@ -84,7 +84,8 @@ void orc_ns_adapt_uv(orc_ns* s);
 double orc_ns_max_element(const orc_ns* s, const double* m);
 /* Main loop of assignment-5/sequential/src/main.c:43-60.  solver: 0 =
  * lexicographic solve (the shipped NS), 1 = red-black solveRB (the composed
- * RB-NS oracle).  Runs until t > te or max_steps steps (max_steps
+ * RB-NS oracle), 2 = that solveRB on 16 threads (orc_solve_rb_mt:
+ * p bit-identical, the residual summed in another order).  Runs until t > te or max_steps steps (max_steps
  * < 0: unlimited).  iters[k] = pressure iterations of step k (if iters and
  * k < cap).  Returns the number of steps; *t_out = final t. */
 int orc_ns_run(orc_ns* s, int solver, int max_steps, int* iters, int cap,

@@ -186,3 +186,16 @@ def test_multicore_solve_rb_matches_single_thread(ni, nj, threads):
         p3, _ = orc.poisson_init(ni, nj, 1.0, 1.0, 2)
         it3, _ = orc.solve_rb_mt(p3, rhs, 0.01, 0.01, 1.9, 1e-6, 1000000, threads)
         assert it3 == 2388
+
+
+def test_ns_run_threaded_solve_matches(golden):
+    """orc_ns_run's solver 2 (solveRB on 16 threads, used for the 16384^2
+    config-5 check) gives the fields and per-step iterations of solver 1"""
+    prm = orc.read_par(os.path.join(golden, "a6_dcavity.par"))
+    prm.update(imax=301, jmax=203, itermax=40)
+    a, b = orc.NS(prm), orc.NS(prm)
+    sa, ia, _ = a.run(solver=1, max_steps=6)
+    sb, ib, _ = b.run(solver=2, max_steps=6)
+    assert sa == sb == 6 and list(ia) == list(ib)
+    for k in ("p", "u", "v"):
+        assert np.array_equal(getattr(a, k), getattr(b, k)), k

@@ -546,7 +546,7 @@ __global__ __launch_bounds__(NT, 1) void k3_resident1(G3 g, double* __restrict__
     static_assert(NT % 256 == 0 && PZ % 2 == 0 && PZ % G == 0 && G % 2 == 0, "thread layout");
     __shared__ double L[kTcells];
     __shared__ double sh[NW];
-    __shared__ double sh_S;
+    __shared__ double sh_W[4];
     __shared__ int sh_flag;
     // built once: the shell's black cells to receive (LDS index | ghost-face bits
     // << 16, global offset) and the inner layer's red cells (LDS index | ghost
@@ -797,19 +797,17 @@ __global__ __launch_bounds__(NT, 1) void k3_resident1(G3 g, double* __restrict__
         // the sum of all partials, by wave 0 in rblock_sum's order (the wave
         // tree of partials 64 w .. 64 w + 63, then w = 0, 1, ...): every
         // workgroup gets the same bits
-        if (t < 64) {
-            double S = 0.0;
-#pragma unroll
-            for (int w = 0; w < 4; ++w) {
-                const int k = t + 64 * w;
-                const double v = !(mode & 1024) && k < (int)gridDim.x ? xload(part + k) : 0.0;
-                S = w == 0 ? rwave_sum(v) : S + rwave_sum(v);
-            }
-            if (t == 0) sh_S = S;
+        // (waves 0-3 one chunk of 64 partials each, lane 0's wave tree; the
+        // chunks added in order after the barrier: the bits of wave 0 doing all
+        // four in turn, without their four loads and trees in series on it)
+        if (t < 256) {
+            const double v = !(mode & 1024) && t < (int)gridDim.x ? xload(part + t) : 0.0;
+            const double ws = rwave_sum(v);
+            if ((t & 63) == 0) sh_W[t >> 6] = ws;
         }
         if (!(mode & 2)) receive(xm);
         __syncthreads();
-        res = (res + sh_S) / cells;
+        res = (res + (((sh_W[0] + sh_W[1]) + sh_W[2]) + sh_W[3])) / cells;
         ++it;
         done = !((res >= epssq) && (it < itermax));
     }

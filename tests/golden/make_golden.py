@@ -19,6 +19,7 @@ Fixtures:
   ns3d_dcavity_short.npz / ns3d_canal_short.npz  the reference's 3D NS (assignment-6/src,
                            oracle/_ref/libref3d.so) on its dcavity/canal .par at reduced
                            grids, 16 time steps: per-step iterations, p, u, v, w, t
+  ns_seq_dcavity_lex_100.npz    the same run to te=0.0125 (100 steps): p, u, v, t
   ns_seq_dcavity_lex_short.npz  the reference's own NS (assignment-5/sequential, its
                            lexicographic `solve`) on its dcavity.par, te=0.05: p, u, v,
                            t, and the per-step iteration counts of the restatement
@@ -63,6 +64,12 @@ def lex_fixtures():
                         iters_oracle=np.asarray(iters_o, dtype=np.int32), p=p, u=u, v=v, t=t,
                         te=te)
     print("ns_seq_dcavity_lex_short.npz", n, "steps")
+    # a shorter run of the same (te = 0.0125, 100 steps) for the host-program test
+    te = 0.0125
+    n, _, p, u, v, t = orc.ref_ns(os.path.join(SEQ, "dcavity.par"), te=te, solver=0)
+    np.savez_compressed(os.path.join(HERE, "ns_seq_dcavity_lex_100.npz"), steps=n, p=p, u=u,
+                        v=v, t=t, te=te)
+    print("ns_seq_dcavity_lex_100.npz", n, "steps")
 
 
 def ns3d_fixtures():

@@ -113,8 +113,9 @@ def test_exe_poisson_lexicographic_reproduces_committed_pdat(golden, tmp_path):
 
 def test_exe_ns_lexicographic_short(golden, tmp_path):
     """MISOR_SOLVER=lex: the reference's sequential NS on its dcavity.par
-    (400 steps) -> pressure.dat / velocity.dat of the reference build's fields"""
-    z = np.load(os.path.join(golden, "ns_seq_dcavity_lex_short.npz"))
+    (100 steps; the 400-step run is test_lex_gpu.py's) -> pressure.dat /
+    velocity.dat of the reference build's fields"""
+    z = np.load(os.path.join(golden, "ns_seq_dcavity_lex_100.npz"))
     txt = open(os.path.join(golden, "seq_dcavity.par")).read()
     txt = re.sub(r"(?m)^te .*$", "te       %r" % float(z["te"]), txt)
     (tmp_path / "dcavity.par").write_text(txt)

@@ -269,11 +269,12 @@ def test_canal_decomposed(golden, nranks):
 
 @pytest.mark.parametrize("nranks", [2, 4])
 def test_dcavity_decomposed(golden, nranks):
-    """2 ranks: the whole short run (230 steps); 4 ranks: its first 80 steps
-    (normalizePressure at step 0 included; the in-process transport's per-pass
-    host barriers make the small-grid 4-rank run ~0.2 s a step)"""
+    """2 ranks: the first 120 of the short run's 230 steps, 4 ranks: its first
+    40 (normalizePressure at step 0 and 100 included for 2; the in-process
+    transport's per-pass host barriers make a small-grid decomposed step
+    ~0.1-0.2 s); the whole run on one rank: test_dcavity_short_run"""
     assert_same_as_single(golden, "ns_dcavity_rb_short.npz", "a6_dcavity.par", nranks,
-                          -1 if nranks == 2 else 80)
+                          120 if nranks == 2 else 40)
 
 
 def test_dcavity_full_run(golden):

@@ -1977,13 +1977,15 @@ static int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* 
     // concurrently; the exchange of dst's halo for pass k+1 starts on cstream as
     // soon as the edge blocks are done, and so overlaps the interior blocks.
     const bool pipelined = g->dist && g->overlap && T > 1;
+    // (the exchange of the first source follows the first pass's interior
+    // launch on the host: RCCL's host side of a grouped send / receive takes
+    // ~0.1 ms, which the interior blocks need not wait for --
+    // profiles/r05_decomposed_loop_trace.csv)
+    bool first_x = pipelined;
     if (pipelined) {
         HIPCHK(hipEventRecord(g->ev_s, g->stream));  // state upload, rhs halo, prior work
         HIPCHK(hipStreamWaitEvent(g->cstream, g->ev_s, 0));
         HIPCHK(hipStreamWaitEvent(g->estream, g->ev_s, 0));
-        int rc = exchange(g, pbuf(g, cur0), depth, g->cstream);
-        if (rc) return rc;
-        HIPCHK(hipEventRecord(g->ev_x, g->cstream));
     }
     // passes plan the iterations still to do (it0 of them are done: a solve
     // resumed after an exact tail)
@@ -2051,6 +2053,12 @@ static int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* 
                 if (rc_) return rc_;
             }
             HIPCHK(hipEventRecord(g->ev_i[k & 1], g->stream));
+            if (first_x) {  // src's halo for the first pass
+                first_x = false;
+                int rc = exchange(g, pbuf(g, cur0), depth, g->cstream);
+                if (rc) return rc;
+                HIPCHK(hipEventRecord(g->ev_x, g->cstream));
+            }
             // edge blocks: after the interior blocks of pass k-1, the edge blocks
             // of k-1 (this stream) and the exchange of src's halo (which follows
             // decide k-2 on cstream)
@@ -2072,7 +2080,16 @@ static int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* 
                 HIPCHK(hipEventRecord(g->ev_x, g->cstream));
             }
             HIPCHK(hipStreamWaitEvent(g->cstream, g->ev_i[k & 1], 0));
-            launch_finish(g->cstream, part, nparts_of(Tk), Tk, g->st, cells, 0);
+            // the pass's residual sums for the all-reduce: the two-level sum (many
+            // workgroups, the last one writing st->sum) -- one workgroup summing
+            // every block partial took 70-100 us, after the last pass on the
+            // solve's critical path (profiles/r05_decomposed_loop_trace.csv)
+            if (g->finish_merge)
+                launch_finish2(g->cstream, part, nparts_of(Tk), Tk, g->st, cells,
+                               g->partials + 2 * (long long)g->partials_cap, g->tb_queue + 10,
+                               0);
+            else
+                launch_finish(g->cstream, part, nparts_of(Tk), Tk, g->st, cells, 0);
             rc = allreduce(g, g->st->sum, Tk, 0, g->cstream);
             if (rc) return rc;
             launch_decide(g->cstream, g->st, Tk, cells);
@@ -2153,7 +2170,7 @@ static int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* 
             } else if (g->finish2) {
                 launch_finish2(g->stream, g->partials, nparts_of(Tk), Tk, g->st, cells,
                                g->partials + 2 * (long long)g->partials_cap,
-                               g->finish_merge ? g->tb_queue + 9 : nullptr);
+                               g->finish_merge ? g->tb_queue + 9 : nullptr, 1);
             } else {
                 launch_finish(g->stream, g->partials, nparts_of(Tk), Tk, g->st, cells, 1);
             }

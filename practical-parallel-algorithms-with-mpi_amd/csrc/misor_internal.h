@@ -237,9 +237,10 @@ void launch_decide(hipStream_t s, DevState* st, int T, double cells);
 // kFinishChunks values per stage); scratch holds kMaxT * kFinishChunks doubles
 constexpr int kFinishChunks = 32;
 // count: a zeroed device int -- the partial-sum launch's last workgroup then
-// runs the loop test itself (one launch); nullptr: a second, finish launch
+// runs the loop test itself (one launch); nullptr: a second, finish launch.
+// decide 0: only the sums into st->sum (decomposed: all-reduce, then decide)
 void launch_finish2(hipStream_t s, const double* partials, int nparts, int T, DevState* st,
-                    double cells, double* scratch, int* count);
+                    double cells, double* scratch, int* count, int decide);
 // queue: 8 device ints (zeroed by the launch) for a persistent launch whose
 // workgroups take blocks from per-XCD queues; nullptr: one workgroup per block
 void launch_tb(hipStream_t s, int T, const SweepParams& prm, const double* src, double* dst,

@@ -421,7 +421,7 @@ __global__ __launch_bounds__(kFinishThreads) void rb_finish_kernel(
 __global__ __launch_bounds__(256) void rb_partsum_kernel(const double* __restrict__ partials,
                                                          int n, const DevState* __restrict__ st,
                                                          double* __restrict__ out, int* count,
-                                                         int T, double cells) {
+                                                         int T, double cells, int decide) {
     __shared__ double sh[256];
     __shared__ int is_last;
     // (st->done is the same for the whole launch: only its last workgroup
@@ -471,18 +471,19 @@ __global__ __launch_bounds__(256) void rb_partsum_kernel(const double* __restric
     {
         __shared__ double fsh[kMaxT][kFinishThreads];
         __shared__ double tot[kMaxT];
-        finish_body<true>(out, kFinishChunks, T, const_cast<DevState*>(st), cells, 1, fsh, tot);
+        finish_body<true>(out, kFinishChunks, T, const_cast<DevState*>(st), cells, decide, fsh,
+                          tot);
         if (t == 0) __hip_atomic_store(count, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
 void launch_finish2(hipStream_t s, const double* partials, int nparts, int T, DevState* st,
-                    double cells, double* scratch, int* count) {
+                    double cells, double* scratch, int* count, int decide) {
     hipLaunchKernelGGL(rb_partsum_kernel, dim3(kFinishChunks, T), dim3(256), 0, s, partials,
-                       nparts, st, scratch, count, T, cells);
+                       nparts, st, scratch, count, T, cells, decide);
     if (!count)
         hipLaunchKernelGGL(rb_finish_kernel, dim3(1), dim3(kFinishThreads), 0, s, scratch,
-                           kFinishChunks, T, st, cells, 1);
+                           kFinishChunks, T, st, cells, decide);
 }
 
 int sweep_waves(int variant) { return kSweepVariants[variant].waves; }

@@ -205,6 +205,8 @@ struct misor_grid {
     hipStream_t estream = nullptr;  // edge blocks of a pipelined pass
     hipEvent_t ev_s = nullptr, ev_x = nullptr, ev_d = nullptr, ev_e = nullptr;
     hipEvent_t ev_i[2] = {}, ev_dk[2] = {};  // interior blocks / decide of pass k, by k & 1
+    hipEvent_t ev_e2[2] = {};                // edge blocks of pass k on cstream, by k & 1
+    bool p2_cstream = true;                  // MISOR_P2_CSTREAM (the pipelined loop's part 2)
     double* sendbuf = nullptr;
     double* recvbuf = nullptr;
     double* gbuf = nullptr;  // misor_gather: this rank's owned block, packed
@@ -330,6 +332,7 @@ void misor_destroy(misor_grid* g) {
     for (int b = 0; b < 2; ++b) {
         if (g->ev_i[b]) (void)hipEventDestroy(g->ev_i[b]);
         if (g->ev_dk[b]) (void)hipEventDestroy(g->ev_dk[b]);
+        if (g->ev_e2[b]) (void)hipEventDestroy(g->ev_e2[b]);
     }
     if (g->ev_s) (void)hipEventDestroy(g->ev_s);
     if (g->ev_x) (void)hipEventDestroy(g->ev_x);
@@ -1251,6 +1254,7 @@ int misor_create(misor_grid** out, const misor_desc* d) {
                   hipStreamCreateWithPriority(&g->estream, hipStreamNonBlocking, prio_hi) ==
                       hipSuccess;
         for (hipEvent_t* e : {&g->ev_s, &g->ev_x, &g->ev_d, &g->ev_e, &g->ev_i[0], &g->ev_i[1],
+                              &g->ev_e2[0], &g->ev_e2[1],
                               &g->ev_dk[0], &g->ev_dk[1]})
             ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
         if (!ok) CREATE_FAIL(MISOR_EHIP, "comm stream/event creation failed");
@@ -1306,6 +1310,8 @@ int misor_create(misor_grid** out, const misor_desc* d) {
         // the loop test in the partial-sum launch's last workgroup (A/B: 0)
         e = getenv("MISOR_FINISH_MERGE");
         g->finish_merge = !(e && e[0] == '0');
+        e = getenv("MISOR_P2_CSTREAM");  // A/B: 0 = part 2 on its own stream
+        g->p2_cstream = !(e && e[0] == '0');
         e = getenv("MISOR_NS_FUSE");  // A/B switch (bench.py --workload ns)
         g->ns_fuse = !(e && e[0] == '0');
     }
@@ -2053,6 +2059,53 @@ static int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* 
                 if (rc_) return rc_;
             }
             HIPCHK(hipEventRecord(g->ev_i[k & 1], g->stream));
+            if (g->p2_cstream) {
+                // Part 2 (the blocks whose cone reads the halo) on the comm
+                // stream, right behind what it waits for: pass k+1's part 2 is
+                // enqueued here, after pass k's exchange, loop test and part 1
+                // (its source is pass k's result), so no cross-stream wait
+                // stands between the exchange and it.  (On a stream of its own,
+                // waiting for the exchange on the comm stream and the interior
+                // blocks on this one, the second pass's part 2 started ~0.5 ms
+                // late on the 8-GPU rank block: profiles/r05_decomposed_loop_trace*.)
+                int rc = MISOR_OK;
+                if (first_x) {  // the solve's first pass: src's halo, then its part 2
+                    first_x = false;
+                    rc = exchange(g, const_cast<double*>(src), depth, g->cstream);
+                    if (rc) return rc;
+                    rc = pass(g->cstream, 2, src, dst, Tk, 0, part);
+                    if (rc) return rc;
+                    HIPCHK(hipEventRecord(g->ev_e2[k & 1], g->cstream));
+                }
+                if (k + 1 < max_passes) {  // dst's halo (part 2 of pass k, above, wrote its send region)
+                    rc = exchange(g, dst, depth, g->cstream);
+                    if (rc) return rc;
+                }
+                HIPCHK(hipStreamWaitEvent(g->cstream, g->ev_i[k & 1], 0));
+                if (g->finish_merge)
+                    launch_finish2(g->cstream, part, nparts_of(Tk), Tk, g->st, cells,
+                                   g->partials + 2 * (long long)g->partials_cap,
+                                   g->tb_queue + 10, 0);
+                else
+                    launch_finish(g->cstream, part, nparts_of(Tk), Tk, g->st, cells, 0);
+                rc = allreduce(g, g->st->sum, Tk, 0, g->cstream);
+                if (rc) return rc;
+                launch_decide(g->cstream, g->st, Tk, cells);
+                HIPCHK(hipEventRecord(g->ev_dk[k & 1], g->cstream));
+                if (k + 1 < max_passes) {  // pass k+1's part 2: after both parts of pass k
+                    const long long k1 = k + 1;
+                    double* part1 = g->partials + (k1 & 1) * (long long)g->partials_cap;
+                    rc = pass(g->cstream, 2, dst, pbuf(g, cur0 + k1 + 1), t_of(k1), 0, part1);
+                    if (rc) return rc;
+                    HIPCHK(hipEventRecord(g->ev_e2[k1 & 1], g->cstream));
+                }
+                // pass k+1's interior blocks read what part 2 of pass k wrote
+                HIPCHK(hipStreamWaitEvent(g->stream, g->ev_e2[k & 1], 0));
+                if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b + 1], g->stream));
+                if (b == batch - 1)  // the host reads the loop state after the last decide
+                    HIPCHK(hipStreamWaitEvent(g->stream, g->ev_dk[k & 1], 0));
+                continue;
+            }
             if (first_x) {  // src's halo for the first pass
                 first_x = false;
                 int rc = exchange(g, pbuf(g, cur0), depth, g->cstream);

@@ -1012,10 +1012,12 @@ static int configure_tb(misor_grid* g, int T, int variant, int rows) {
     //    loop 0.122 vs 0.142): every solve of more than 8 iterations;
     //  - a single rank of >= 2^29 cells (the 32768^2 bench grid: 0.676 vs 0.682
     //    at 100 iterations, 20 iterations in 2 passes instead of 3): the same;
-    //  - a single rank of 2^28 cells, and decomposed blocks of >= 2^29 (the
-    //    two-GPU split of the bench grid): only where it saves passes, the
-    //    rule in solve_rb_from (at 100 iterations the two plans are within 1-3%);
-    //  - decomposed 2^28-cell blocks (the 4-GPU split): never (0.212 vs 0.219).
+    //  - a single rank of 2^28 cells, and decomposed blocks of >= 2^28 (the
+    //    two- and four-GPU splits of the bench grid): only where it saves
+    //    passes, the rule in solve_rb_from (at 100 iterations the two plans are
+    //    within 1-3%; the 4-GPU rank block through the pipelined loop of round
+    //    5, 20 iterations: 0.2247-0.2250 vs 0.2317-0.2327 ms per iteration,
+    //    profiles/r05_plan_ab_ranks.txt -- round 4's loop measured the opposite).
     const long long cells = (long long)g->loc.ni * g->loc.nj;
     const bool small_chain = cells >= kHrAllCells && cells < kTsteps8Cells &&
                              chain_on(g, variant);

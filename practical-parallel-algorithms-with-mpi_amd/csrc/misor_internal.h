@@ -85,7 +85,7 @@ constexpr int kHrTbVariant = 13;   // the skewed split ring (T = 1 unskewed)
 // the short plan of capped solves (misor_api.hip solve_rb_from)
 constexpr int kShortTbVariant = kHrTbVariant;
 constexpr int kShortT = 10;
-constexpr long long kShortDistCells = 1LL << 29;  // decomposed: local blocks at least this big
+constexpr long long kShortDistCells = 1LL << 28;  // decomposed: local blocks at least this big
 constexpr long long kHrAllCells = 1LL << 26;      // chained blocks from here: every solve > 8
 // iterations per pass: 8 on large local blocks, 7 below kTsteps8Cells cells
 // (32768^2 0.744 vs 0.785 ms/iteration, profiles/r02_tune_t789.txt; one rank's

@@ -166,30 +166,9 @@ __device__ bool rgrid_sync(Bar3* bar, unsigned n, int* sh_flag, int mode) {
     return *sh_flag == 0;
 }
 
-// rgrid_sync in two halves (the exchange-by-atomics modes, bits 3 / 4): arrive
-// (every wave's stores acknowledged, then thread 0 counts the workgroup in)
-// and wait; the workgroup may compute in between anything that reads no
-// exchanged data and writes none
-__device__ void rgrid_arrive(Bar3* bar, unsigned n, int mode) {
-    __builtin_amdgcn_s_waitcnt(0);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        if (mode & 32) {
-            const unsigned x = blockIdx.x & 7, nb = gridDim.x;
-            const unsigned cx = (nb - x + 7) / 8;
-            const unsigned old = __hip_atomic_fetch_add(&bar->xcd[16 * x], 1u, __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT);
-            if (old + 1 == n * cx)
-                __hip_atomic_fetch_add(&bar->count, 1u, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            __hip_atomic_fetch_add(&bar->count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-}
-
-// rgrid_arrive with the workgroup's residual partial folded in: every wave has
+// rgrid_sync's arrival half (the exchange-by-atomics modes, bits 3 / 4: the
+// workgroup may compute in between anything that reads no exchanged data and
+// writes none) with the workgroup's residual partial folded in: every wave has
 // put its wave sum in sh[]; after the arrival barrier thread 0 adds them in
 // wave order (rblock_sum's order), stores the partial (relaxed agent-scope,
 // acknowledged before the arrival counts) and arrives -- one workgroup

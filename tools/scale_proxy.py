@@ -96,7 +96,7 @@ def main():
         v0 = g.get_tuning(M.TUNE_TB_VARIANT)
         g.solve_rb(itermax=args.sweeps)  # the first timed solve of a process runs slow
         res = {c: ([], []) for c in combos}
-        hrow = {}
+        hrow, tgot = {}, {}
         applied = None
         for _ in range(args.rounds):
             for c in combos:
@@ -109,7 +109,7 @@ def main():
                     g.synchronize()
                     wall = time.perf_counter() - t0
                     st = g.stats()
-                    assert st["iters_per_pass"] == T
+                    tgot[c] = st["iters_per_pass"]  # (a balanced split of the solve: <= T)
                     res[c][0].append(st["sweep_ms"] / max(st["timed_sweeps"], 1))
                     res[c][1].append(wall * 1e3 / args.sweeps)
                     continue
@@ -139,7 +139,7 @@ def main():
                 g.synchronize()
                 wall = time.perf_counter() - t0
                 st = g.stats()
-                assert st["iters_per_pass"] == T
+                tgot[c] = st["iters_per_pass"]  # (a balanced split of the solve: <= T)
                 res[c][0].append(st["sweep_ms"] / max(st["timed_sweeps"], 1))
                 res[c][1].append(wall * 1e3 / args.sweeps)
         for c in combos:
@@ -153,8 +153,9 @@ def main():
                 base = ms * N
             eff = base / (N * ms)
             print("%-2d %-12s %2d %2d %5d %10.4f %10.4f %10.0f %6.3f  remap=%d persistent=%d "
-                  "reserve=%d chain=%d" % (N, "%dx%d" % (ni, nj), T, v, hrow[c], ms, wall, mlups,
-                                           eff, x, pp, rv, ch), flush=True)
+                  "reserve=%d chain=%d T/pass=%d" % (N, "%dx%d" % (ni, nj), T, v, hrow[c], ms, wall,
+                                                      mlups, eff, x, pp, rv, ch, tgot[c]),
+                  flush=True)
         g.close()
 
 

@@ -16,7 +16,7 @@ stealing decide at run time which workgroup computes which block -- fails it.
 
 Config 4 at 2, 4 and 8 GPUs: the splits of bench.py --gpus N (2 x 1: the short
 plan on 2^29-cell blocks; 2 x 2: 16384^2 = 2^28-cell blocks, the short plan
-unchained, pipelined; 4 x 2: one rank's block 8192 x 16384, chained split-ring
+(chained split ring), pipelined; 4 x 2: one rank's block 8192 x 16384, chained split-ring
 passes of 10 iterations) as N
 in-process ranks on the one GPU (pipelined loop, 2T-deep exchanges); the
 assembled field against the same oracle.
@@ -105,7 +105,7 @@ def test_fullfield_32768_bench_sequence():
 def test_fullfield_32768_ranks(world):
     """8 ranks: 2^27-cell blocks, two 10-iteration passes of the chained split
     ring; 4 ranks (2^28-cell blocks) and 2 ranks (2^29): the short pass plan
-    (two unchained 10-iteration split-ring passes)"""
+    (two 10-iteration split-ring passes)"""
     n = 32768
     dx = 1.0 / n
     cid = ("LOCAL:full%d" % world).encode()
@@ -141,9 +141,10 @@ def test_fullfield_32768_ranks(world):
         # the chained split ring: T = 10 passes on the 2^27-cell blocks
         assert all(o[7] == (10, 13, 1) for o in outs), [o[7] for o in outs]
     elif world == 4:
-        assert all(o[6] == 0 for o in outs)  # 2^28 cells: not chained
+        assert all(o[6] == 0 for o in outs)  # 2^28 cells: T = 8 passes would not be chained
         assert tuple(outs[0][0].dims) == (2, 2) and (outs[0][0].ni, outs[0][0].nj) == (16384, 16384)
-        assert all(o[7] == (10, 13, 0) for o in outs), [o[7] for o in outs]
+        # the short plan: two chained split-ring passes
+        assert all(o[7] == (10, 13, 1) for o in outs), [o[7] for o in outs]
     else:  # the short plan: 2 passes of the split ring (decomposed 2^29 blocks)
         assert all(o[7][:2] == (10, 13) for o in outs), [o[7] for o in outs]
     p = np.empty((n + 2, n + 2))

@@ -27,6 +27,16 @@ struct CLay {
     }
 };
 
+// a store the kernel never reads back (NT: nontemporal, streamed past the
+// caches).  fg_rhs / adapt_absmax store NT by default (MISOR_NS_NT=0: plain
+// stores): config 5's fg_rhs 1.93 vs 1.97 ms, adapt_absmax unchanged, the step
+// 22.26 vs 22.36 ms over three alternated pairs (profiles/r05_ns_nt_ab.txt)
+template <bool NT, class V>
+__device__ __forceinline__ void put(V* p, V v) {
+    if (NT) __builtin_nontemporal_store(v, p);
+    else    *p = v;
+}
+
 constexpr int kTx = 64, kTy = 4;
 
 }  // namespace
@@ -254,6 +264,15 @@ __device__ __forceinline__ double g_val(const FgArgs& a, const Uv3& S, const Uv3
 // algorithmic 16 B/cell, profiles/r03_pmc_ns16384_base.json.)
 constexpr int kFgW = 256, kFgRows = 64;
 
+static bool ns_nt() {
+    static const bool on = [] {
+        const char* e = getenv("MISOR_NS_NT");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+
+template <bool NT>
 __global__ __launch_bounds__(kFgW) void fg_rhs_kernel(CLay u, CLay v, Lay f, Lay g, Lay rhs,
                                                       int ni, int nj, FgArgs a, int wl, int wr,
                                                       int wb, int wt, int nbx, int nblocks) {
@@ -296,8 +315,8 @@ __global__ __launch_bounds__(kFgW) void fg_rhs_kernel(CLay u, CLay v, Lay f, Lay
         // boundary of F / G (:426-435) overrides the interior value
         if (wr && i == ni) fv = C.uc;
         if (wt && j == nj) gv = C.vc;
-        f(i, j) = fv;
-        g(i, j) = gv;
+        put<NT>(&f(i, j), fv);
+        put<NT>(&g(i, j), gv);
         if (wl && i == 1) f(0, j) = C.um;
         if (wb && j == 1) g(i, 0) = S.vc;
         if (has_fl && has_gp) {
@@ -305,7 +324,7 @@ __global__ __launch_bounds__(kFgW) void fg_rhs_kernel(CLay u, CLay v, Lay f, Lay
             const double fl = i == 1 ? C.um
                                      : f_val(a, C.um, C.uc, uww, N.um, S.um, C.vm, C.vc, S.vm,
                                              S.vc);
-            rhs(i, j) = a.idt * ((fv - fl) * a.idx + (gv - gprev) * a.idy);  // :131-133
+            put<NT>(&rhs(i, j), a.idt * ((fv - fl) * a.idx + (gv - gprev) * a.idy));  // :131-133
         }
         gprev = gv;
         has_gp = true;
@@ -325,7 +344,7 @@ void launch_compute_fg_rhs(const NsLaunch& L, const double* u, const double* v, 
     const NsParams& P = L.prm;
     FgArgs a{P.dt, 1.0 / P.re, 1.0 / P.dx, 1.0 / P.dy, P.gamma, P.gx, P.gy,
              1.0 / P.dx, 1.0 / P.dy, 1.0 / P.dt};
-    hipLaunchKernelGGL(fg_rhs_kernel, dim3(grid), dim3(kFgW), 0, L.s, CLay{u, L.pitch},
+    hipLaunchKernelGGL(ns_nt() ? fg_rhs_kernel<true> : fg_rhs_kernel<false>, dim3(grid), dim3(kFgW), 0, L.s, CLay{u, L.pitch},
                        CLay{v, L.pitch}, Lay{f, L.pitch}, Lay{g, L.pitch}, Lay{rhs, L.pitch},
                        L.ni, L.nj, a, L.wall_left, L.wall_right, L.wall_bottom, L.wall_top, nbx,
                        nblocks);
@@ -495,7 +514,7 @@ typedef double ad2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ ad2 ld2(const double* q) { return *reinterpret_cast<const ad2*>(q); }
 
-template <int kAR>
+template <int kAR, bool NT>
 __global__ __launch_bounds__(kRedThreads) void adapt_absmax_kernel(CLay f, CLay g, CLay p, Lay u,
                                                                    Lay v, int ni, int nj,
                                                                    double fx, double fy, Region R,
@@ -530,8 +549,8 @@ __global__ __launch_bounds__(kRedThreads) void adapt_absmax_kernel(CLay f, CLay 
                 const double a1 = fv[q].y - (pe[q] - pc[q].y) * fx;
                 const double b0 = gv[q].x - (pc[q + 1].x - pc[q].x) * fy;
                 const double b1 = gv[q].y - (pc[q + 1].y - pc[q].y) * fy;
-                *reinterpret_cast<ad2*>(u.a + o) = ad2{a0, a1};
-                *reinterpret_cast<ad2*>(v.a + o) = ad2{b0, b1};
+                put<NT>(reinterpret_cast<ad2*>(u.a + o), ad2{a0, a1});
+                put<NT>(reinterpret_cast<ad2*>(v.a + o), ad2{b0, b1});
                 mu = fmax(mu, fmax(fabs(a0), fabs(a1)));
                 mv = fmax(mv, fmax(fabs(b0), fabs(b1)));
             }
@@ -605,8 +624,10 @@ void launch_adapt_absmax(const NsLaunch& L, const double* f, const double* g, co
         const char* e = getenv("MISOR_ADAPT_ROWS");
         return e && atoi(e) == 4 ? 4 : e && atoi(e) == 2 ? 2 : 8;
     }();
-    auto k = rows == 8 ? adapt_absmax_kernel<8> : rows == 2 ? adapt_absmax_kernel<2>
-                                                            : adapt_absmax_kernel<4>;
+    auto k = ns_nt() ? adapt_absmax_kernel<8, true>
+             : rows == 8 ? adapt_absmax_kernel<8, false>
+             : rows == 2 ? adapt_absmax_kernel<2, false>
+                         : adapt_absmax_kernel<4, false>;
     hipLaunchKernelGGL(k, dim3(reduce_blocks(L.ni, L.nj)), dim3(kRedThreads), 0,
                        L.s, CLay{f, L.pitch}, CLay{g, L.pitch}, CLay{p, L.pitch},
                        Lay{u, L.pitch}, Lay{v, L.pitch}, L.ni, L.nj, L.prm.dt / L.prm.dx,

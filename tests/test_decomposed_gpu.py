@@ -355,3 +355,35 @@ def test_halo_after_solve(world, T):
         # the neighbour's cells (the window's four corners left out)
         assert np.array_equal(blk[1:-1, :], w[1:-1, :]), (loc.ioff, loc.joff)
         assert np.array_equal(blk[:, 1:-1], w[:, 1:-1]), (loc.ioff, loc.joff)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("p2c", ["0", "1"])
+def test_part2_stream_forms(world, p2c, monkeypatch):
+    """The pipelined loop's two arrangements of part 2 (MISOR_P2_CSTREAM, read
+    at misor_create: 1 = on the communication stream right behind its exchange,
+    the default; 0 = on its own stream behind event waits) give the oracle's
+    field, bit for bit, over several passes and a partial last one"""
+    monkeypatch.setenv("MISOR_P2_CSTREAM", p2c)
+    ni, nj, T = 420, 260, 4
+    sweeps = 3 * T + 1
+    rng = np.random.default_rng(world * 7 + int(p2c))
+    p = rng.standard_normal((nj + 2, ni + 2))
+    rhs = rng.standard_normal((nj + 2, ni + 2))
+    want = p.copy()
+    orc.solve_rb(want, rhs, 1.0 / ni, 1.0 / nj, 1.7, 1e-300, sweeps)
+
+    def rank_fn(r, cid, dims):
+        with M.Grid(ni, nj, 1.0 / ni, 1.0 / nj, 1.7, 1e-300, sweeps, device=0, nranks=world,
+                    rank=r, comm_id=cid) as g:
+            g.set_tuning(M.TUNE_TSTEPS, T)
+            assert g.get_tuning(M.TUNE_OVERLAP) == 1
+            g.upload(M.P, local_window(p, g.loc))
+            g.upload(M.RHS, local_window(rhs, g.loc))
+            it, _ = g.solve_rb()
+            return g.loc, g.download(M.P), it
+
+    for loc, blk, it in run_ranks(world, rank_fn):
+        assert it == sweeps
+        w = local_window(want, loc)
+        assert np.array_equal(blk[1:-1, 1:-1], w[1:-1, 1:-1]), (loc.ioff, loc.joff)

@@ -707,8 +707,9 @@ static void tb_geometry(const misor_grid* g, int T, SweepParams& tp) {
         // of the ring (MISOR_TB_CHAIN_RINGS: tuning experiments)
         const char* er = getenv("MISOR_TB_CHAIN_RINGS");
         const int rings = er && atoi(er) > 0 ? atoi(er)
-                          : tp.variant == kHrTbVariant ? kHrChainRingsPerBlock
-                                                       : kChainRingsPerBlock;
+                          : tp.variant == kHrTbVariant
+                              ? (g->dist ? kHrChainRingsDist : kHrChainRingsPerBlock)
+                              : kChainRingsPerBlock;
         int h = req > 0 ? S * std::max(1, (req + S / 2) / S) : rings * S;
         if (h > nj) h = nj;
         tp.rows_per_block = h;
@@ -816,7 +817,7 @@ static int chain_plan(misor_grid* g, int variant, int Tp, int part,
     // workgroups): every workgroup starts one at once and they end together.
     const char* ec = getenv("MISOR_CHAIN_EDGE_COST");
     const double E = ec && atof(ec) > 0 ? atof(ec)
-                     : variant == kHrTbVariant ? kHrChainEdgeCost
+                     : variant == kHrTbVariant ? (g->dist ? kHrChainEdgeCostDist : kHrChainEdgeCost)
                                                : kChainEdgeCost;
     const int H = tp.rows_per_block;
     // Plan forms of the split ring (MISOR_HR_PLAN, A/B experiments; round 5):

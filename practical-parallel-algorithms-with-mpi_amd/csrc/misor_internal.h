@@ -196,6 +196,15 @@ constexpr int kChainRingsPerBlock = 4;   // block height of a chained pass, in r
 // strip's; profiles/r05_hrsweep2_*.txt)
 constexpr int kHrChainRingsPerBlock = 8;
 constexpr double kHrChainEdgeCost = 2.5;
+// the same on a decomposed rank's block (its passes split in two parts around
+// the halo exchange): 10 ring lengths (180 rows) and an edge-column block at 3
+// others -- wall ms per iteration of the pipelined loop, alternated on one box
+// (profiles/r05_rank_geometry_ab.txt): the 8-GPU rank block with physical
+// left + bottom sides 0.121 against 0.139 at 8 / 2.5, bottom only 0.125 vs
+// 0.127, the 4-GPU block 0.204 vs 0.230, the 2-GPU block unchanged (sweeps:
+// r05_edge_rings_ab*.txt; a single rank, without the split, stays at 144 rows)
+constexpr int kHrChainRingsDist = 10;
+constexpr double kHrChainEdgeCostDist = 3.0;
 // chained passes by default on local blocks below this many cells: there the
 // unchained blocks are short and their 4T warm-up rows cost most (one 8-GPU
 // rank's 8192 x 16384 of the 32768^2 bench: 0.106 vs 0.110-0.118 ms per

@@ -46,6 +46,23 @@ the solve timed alone; falls back to the C restatement
 (oracle/liboracle.so, kind "port") when _ref is absent.
 cpu_baseline_multicore: the restatement over the cores the job is granted
 (pthreads over row bands), same grid, 10 sweeps per run, best of 3 and median.
+cpu_baseline_mpi: the reference's own MPI pressure solve
+(assignment-5/skeleton/src/solver.c:586-661: a halo exchange and a residual
+MPI_Allreduce per iteration; compiled from its sources with MPICH by
+oracle/Makefile `mpi`) under mpirun on the granted host cores, 8192^2, best
+of 3 and median; {"mpi": "absent"} where mpirun or the build is missing.
+The CPU baselines run on rank 0 at every N (rank 0's own block at N > 1).
+
+N > 1: one process per GPU.  Under torch.distributed.run (the driver) the
+launcher's RANK / LOCAL_RANK / WORLD_SIZE are used and WORLD_SIZE must equal
+--gpus (else exit 2); without a launcher, --gpus N > 1 spawns the N workers
+itself (this parent never touches the GPU: each worker selects its device
+before its first GPU call) and exits with their worst status.  Before timing,
+every N > 1 run solves a 2048^2 grid decomposed over the same ranks, gathers p
+on rank 0 and compares it bit for bit with a single-domain solve there
+(`parity`); `rccl_ranks` is the rank count of the bench grid's communicator
+as RCCL reports it (ncclCommCount).  --dry-run stops each worker before any
+GPU call and prints the rank assignment (tests/test_bench_cpu.py).
 """
 from __future__ import annotations
 
@@ -267,10 +284,26 @@ def run_ns(args, world, rank, local_rank, dist, torch):
     elapsed = time.perf_counter() - t0
     st = g.stats()
     solve_ms = st["sweep_ms"]
+    # per launch, HIP events on the library's stream: the solve's passes, the
+    # fused computeFG + computeRHS, the fused adaptUV + max |u|, |v| partials
+    pass_ms = st["sweep_ms"] / max(st["timed_passes"], 1)
+    fg_ms = st["ns_ms"][0] / max(st["ns_calls"][0], 1)
+    ad_ms = st["ns_ms"][1] / max(st["ns_calls"][1], 1)
+    T_ns, passes_ns = st["iters_per_pass"], st["timed_passes"]
+    # normalizePressure runs every 100 steps (main.c:49): in the warm-up step
+    # 0, not in the timed steps -- timed here, after the timed region, on
+    # the field the steps left (3 calls)
+    g.reset_stats()
+    for _ in range(3):
+        g.call("normalize_pressure")
+    g.synchronize()
+    st2 = g.stats()
+    norm_ms = st2["ns_ms"][2] / max(st2["ns_calls"][2], 1)
     if dist is not None:
-        tt = torch.tensor([elapsed, solve_ms], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([elapsed, solve_ms, pass_ms, fg_ms, ad_ms, norm_ms],
+                          dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed, solve_ms = tt.tolist()
+        elapsed, solve_ms, pass_ms, fg_ms, ad_ms, norm_ms = tt.tolist()
     cells = float(imax) * float(jmax)
     out = {
         "metric": "dcavity NS weak scaling: pressure-solve MLUP/s within full time steps",
@@ -295,8 +328,90 @@ def run_ns(args, world, rank, local_rank, dist, torch):
         "solve_kernel_ms_per_step": round(solve_ms / args.steps, 3),
         "other_ms_per_step": round(elapsed / args.steps * 1e3 - solve_ms / args.steps, 3),
     }
+    # rooflines per launch (HBM, 8 TB/s): the dominant kernel -- the solve's
+    # pass, 24 B per local cell (p in, rhs in, p out) -- and every streaming
+    # kernel of the step with its algorithmic bytes per cell:
+    # fg_rhs 40 (u, v in; f, g, rhs out), adapt_absmax 40 (f, g, p in; u, v
+    # out), normalizePressure 32 (max |p| 8, exact sum 8, subtract 16).  traffic:
+    # the committed PMC summary of this command (tools/ns_pmc_summary.py)
+    lc = float(g.loc.ni) * float(g.loc.nj)
+    pm = ns_pmc_summary(args.size, world)
+    kp = pm.get("kernels", {})
+
+    def roof(nbytes, ms, kname):
+        ach = nbytes / (ms * 1e-3) / 1e9 if ms > 0 else None
+        tr = kp.get(kname, {}).get("bytes_per_launch")
+        return {"bound": "hbm", "achieved": round(ach, 1) if ach else None, "peak": PEAK_GBS,
+                "unit": "GB/s", "frac": round(ach / PEAK_GBS, 4) if ach else None,
+                "traffic": tr, "traffic_ratio": round(tr / nbytes, 4) if tr else None,
+                "kernel_ms": round(ms, 4), "bytes_per_launch": nbytes}
+
+    solve_kernel = pm.get("solve_kernel") or "rb_tb_kernel"
+    out["roofline"] = dict(roof(24.0 * lc, pass_ms, solve_kernel),
+                           kernel="pressure solve pass (%s, %d iterations per pass, %d passes in "
+                                  "the timed steps)" % (solve_kernel, T_ns, passes_ns))
+    out["kernels"] = {
+        "fg_rhs_kernel": dict(roof(40.0 * lc, fg_ms, "fg_rhs_kernel"),
+                              what="computeFG + computeRHS fused (solver.c:360-436, 122-138)"),
+        "adapt_absmax_kernel": dict(roof(40.0 * lc, ad_ms, "adapt_absmax_kernel"),
+                                    what="adaptUV + the next dt's max |u|, |v| (:438-455, "
+                                         ":193-202)"),
+        "normalize_pressure": dict(roof(32.0 * lc, norm_ms, "normalize_pressure"),
+                                   what="normalizePressure (:204-217): absmax2 + exact_sum + "
+                                        "sub_mean, timed after the timed steps (3 calls)"),
+    }
+    if pm:
+        out["roofline"]["traffic_source"] = pm.get("file")
+    if rank == 0 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline_ns(g.loc.ni, g.loc.nj)
+        except Exception as e:  # reported, never fatal for the GPU number
+            out["cpu_baseline"] = {"value": None, "error": repr(e)}
     g.close()
     return out
+
+
+def ns_pmc_summary(size, nranks):
+    """the committed PMC summary of bench.py --workload ns at this size
+    (tools/ns_pmc_summary.py), latest in name order, or {}"""
+    best = {}
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_ns*.json"))):
+        try:
+            d = json.load(open(path))
+        except Exception:
+            continue
+        if d.get("size") == size and d.get("nranks", 1) == nranks and "kernels" in d:
+            best = dict(d, file=os.path.basename(path))
+    return best
+
+
+def cpu_baseline_ns(ni, nj, itermax=3, steps=1):
+    """The reference's own NS step (assignment-5/sequential/src/main.c:43-60:
+    computeTimestep, BCs, computeFG, computeRHS, normalizePressure, solveRB of
+    assignment-4 -- the composed RB-NS oracle of SURVEY 0.4 -- and adaptUV;
+    oracle/_ref/libref.so) on one host core, on the bench's dcavity grid
+    (rank 0's block at N > 1), a bounded sample: `steps` step(s) with the
+    solve capped at `itermax` iterations.  value = cells x iterations / step
+    time of the sample; the solve's time per iteration and the rest of the
+    step are reported beside it."""
+    import orc
+
+    if not orc.have_ref():
+        return {"value": None, "kind": "reference", "error": "oracle/_ref/libref.so not built"}
+    par = os.path.join(ROOT, "tests", "golden", "a6_dcavity.par")
+    n, solve_s, step_s, sweeps = orc.ref_ns_timed(par, ni, nj, itermax, steps)
+    cells = float(ni) * float(nj)
+    per_it = solve_s / max(sweeps, 1)
+    other = (step_s - solve_s) / max(n, 1)
+    return {"value": round(cells * sweeps / step_s / 1e6, 2), "unit": "MLUP/s", "cores": 1,
+            "kind": "reference", "cpu": cpu_model(),
+            "solve_s_per_iteration": round(per_it, 4),
+            "solve_MLUPs": round(cells / per_it / 1e6, 2),
+            "other_s_per_step": round(other, 3),
+            "sample": "the reference's NS step (sequential solver.c + assignment-4 solveRB, "
+                      "oracle/_ref) on %dx%d dcavity, %d step(s) with the solve capped at %d "
+                      "iterations (%.2f s; %.2f s of it in solveRB), 1 host core, "
+                      "initSolver untimed" % (ni, nj, n, itermax, step_s, solve_s)}
 
 
 # assignment-6/dcavity.par (the 3D solver's own configuration)
@@ -541,6 +656,138 @@ def run_poisson_local(args, N):
     return out
 
 
+def spawn_workers(n, dry_run):
+    """--gpus N > 1 without a launcher: start N workers of this script with the
+    environment torch.distributed.run would give them (RANK, LOCAL_RANK,
+    WORLD_SIZE, MASTER_ADDR 127.0.0.1, a free MASTER_PORT).  This process never
+    imports torch or touches the GPU; it waits for the workers, stops the rest
+    when one fails, and returns their worst exit status.  Rank 0's stdout is
+    this script's stdout (the JSON line), the other ranks' goes to stderr; with
+    --dry-run every worker's line is collected into one JSON line."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        out = subprocess.PIPE if dry_run else (None if r == 0 else sys.stderr)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env, stdout=out))
+    rcs = [None] * n
+    outs = [b""] * n
+    if dry_run:
+        for r, p in enumerate(procs):
+            outs[r], _ = p.communicate(timeout=120)
+            rcs[r] = p.returncode
+    else:
+        while any(rc is None for rc in rcs):
+            for r, p in enumerate(procs):
+                if rcs[r] is None:
+                    rcs[r] = p.poll()
+            if any(rc not in (None, 0) for rc in rcs):  # one failed: stop the others
+                for r, p in enumerate(procs):
+                    if rcs[r] is None:
+                        p.terminate()
+                for r, p in enumerate(procs):
+                    if rcs[r] is None:
+                        try:
+                            rcs[r] = p.wait(timeout=30)
+                        except subprocess.TimeoutExpired:
+                            p.kill()
+                            rcs[r] = p.wait()
+                break
+            time.sleep(0.2)
+    worst = max((abs(rc) for rc in rcs), default=0)
+    if dry_run:
+        workers = [json.loads(o.decode().strip().splitlines()[-1]) for o in outs if o.strip()]
+        print(json.dumps({"dry_run": True, "spawned": n, "master_port": port,
+                          "exit_codes": rcs, "workers": workers}), flush=True)
+    elif worst:
+        log("bench workers exited with %s" % rcs)
+    return worst
+
+
+def parity_check(world, rank, local_rank, dist, n=2048, iters=30):
+    """Before timing an N > 1 run: a n^2 problem-2 solve of `iters` iterations
+    decomposed over the same ranks (its own RCCL communicator), p gathered on
+    rank 0 (misor_gather, the skeleton's collectResult) and compared bit for
+    bit with a single-domain solve of the same grid on rank 0's GPU, with the
+    iteration counts and residuals.  Returns the record on rank 0, else None."""
+    import numpy as np
+    import pymisor as M
+
+    obj = [M.comm_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    g = M.Grid(n, n, 1.0 / n, 1.0 / n, 1.9, 1e-300, iters, device=local_rank, nranks=world,
+               rank=rank, comm_id=obj[0])
+    g.poisson_init(1.0, 1.0, 2)
+    it, res = g.solve_rb()
+    nr = g.comm_ranks()
+    dims = "%dx%d" % tuple(g.loc.dims)
+    p = g.gather(M.P)
+    g.close()
+    if rank != 0:
+        return None
+    with M.Grid(n, n, 1.0 / n, 1.0 / n, 1.9, 1e-300, iters, device=local_rank) as g1:
+        g1.poisson_init(1.0, 1.0, 2)
+        it1, res1 = g1.solve_rb()
+        ref = g1.download(M.P)
+    same = bool(np.array_equal(p, ref))
+    return {"grid": "%dx%d" % (n, n), "decomposition": dims, "iterations": [it, it1],
+            "p_bit_identical_to_1_rank": same and it == it1,
+            "res_rel_diff": abs(res - res1) / abs(res1) if res1 else abs(res - res1),
+            "rccl_ranks": nr,
+            "note": "gathered p of the decomposed RCCL solve vs a single-domain solve on rank 0, "
+                    "before the timed region"}
+
+
+def cpu_baseline_mpi(cores, n=8192, sweeps=50, runs=3):
+    """The reference's MPI pressure solve (assignment-5/skeleton/src/solver.c:
+    586-661: per iteration an exchange of p, MPI_Neighbor_alltoallw :155, a
+    lexicographic sweep and MPI_Allreduce of the residual :651), built from its
+    own sources with MPICH (oracle/Makefile `mpi`, driver oracle/ref_mpi_glue.c),
+    under mpirun with `cores` ranks on this host, n^2 problem-2 fields, `sweeps`
+    iterations per run; the north star's communication-pattern CPU baseline.
+    {"mpi": "absent"} when mpirun or the build is missing."""
+    import shutil
+    import subprocess
+
+    exe = os.path.join(ROOT, "oracle", "_ref", "ref-skel-solve")
+    mpirun = "/opt/conda/bin/mpirun" if os.path.exists("/opt/conda/bin/mpirun") else \
+        shutil.which("mpirun")
+    if not mpirun or not os.path.exists(exe):
+        return {"value": None, "mpi": "absent",
+                "mpirun": mpirun, "build": os.path.exists(exe)}
+    cmd = [mpirun, "-launcher", "fork", "-np", str(cores), exe, str(n), str(n), str(sweeps),
+           str(runs)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd="/tmp")
+    if r.returncode != 0:
+        return {"value": None, "mpi": mpirun, "error": (r.stderr or r.stdout)[-400:]}
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    return {"value": d["mlups_best"], "median": d["mlups_median"], "unit": "MLUP/s",
+            "cores": cores, "ranks": d["ranks"], "dims": d["dims"], "kind": "reference",
+            "mpi": mpirun, "cpu": cpu_model(),
+            "sample": "assignment-5/skeleton solve (lexicographic SOR, halo exchange + "
+                      "MPI_Allreduce every iteration) on %dx%d, %d sweeps per run, best of %d "
+                      "(%.2f s; median %.2f s), mpirun -np %d (MPICH, one rank per core)"
+                      % (n, n, sweeps, runs, d["best_s"], d["median_s"], cores)}
+
+
+def granted_cores():
+    """the cores this process may run on at once: the affinity mask capped by a
+    cgroup CPU quota and OMP_NUM_THREADS (the GPU box lists its whole machine in
+    the mask but grants a share of it, stated in OMP_NUM_THREADS)"""
+    aff = len(os.sched_getaffinity(0))
+    quota = cgroup_cpus()
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return max(1, min(aff, 256, quota or 256, int(omp) if omp.isdigit() and int(omp) > 0 else 256))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -567,13 +814,29 @@ def main():
                          "decomposed path's plumbing; not a scaling measurement)")
     ap.add_argument("--check", action="store_true",
                     help="with --local-ranks: gathered p bit for bit against one rank")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="stop before any GPU call; print this worker's rank assignment")
+    ap.add_argument("--no-parity", action="store_true",
+                    help="N > 1: skip the pre-timing 2048^2 decomposed-vs-single parity solve")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher: this process spawns the N workers and never touches the GPU
+        sys.exit(spawn_workers(args.gpus, args.dry_run))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        log("warning: WORLD_SIZE=%d but --gpus %d" % (world, args.gpus))
+        log("error: WORLD_SIZE=%d but --gpus %d: launch one process per GPU "
+            "(torch.distributed.run --nproc-per-node %d, or no launcher at all)"
+            % (world, args.gpus, args.gpus))
+        sys.exit(2)
+    if args.dry_run:
+        print(json.dumps({"rank": rank, "local_rank": local_rank, "world_size": world,
+                          "gpus": args.gpus, "master_addr": os.environ.get("MASTER_ADDR"),
+                          "master_port": os.environ.get("MASTER_PORT"),
+                          "device": "cuda:%d" % local_rank}), flush=True)
+        return
 
     import torch
 
@@ -626,6 +889,10 @@ def main():
         g.set_tuning(M.TUNE_TSTEPS, args.tsteps)
     g.poisson_init(float(pdims[0]), float(pdims[1]), 2)
     local_cells = g.loc.ni * g.loc.nj
+    rccl_ranks = g.comm_ranks() if world > 1 else None
+    parity = None
+    if world > 1 and not args.no_parity:
+        parity = parity_check(world, rank, local_rank, dist)
 
     def barrier():
         torch.cuda.synchronize()
@@ -778,22 +1045,38 @@ def main():
         out["roofline"]["valu"] = valu
         if valu["valu_busy_per_simd"] >= 0.85:
             out["roofline"]["bound"] = "valu"
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        # the bench's own grid: the fields the device holds after the timed solve
-        hp, hrhs = g.download(M.P), g.download(M.RHS)
-        try:
-            out["cpu_baseline"] = cpu_baseline(hp, hrhs)
-        except Exception as e:  # reported, never fatal for the GPU number
-            out["cpu_baseline"] = {"value": None, "error": repr(e)}
-        try:
-            out["cpu_baseline_multicore"] = cpu_baseline_multicore(hp, hrhs)
-        except Exception as e:
-            out["cpu_baseline_multicore"] = {"value": None, "error": repr(e)}
-        del hp, hrhs
-        for key in ("cpu_baseline", "cpu_baseline_multicore"):
-            cb = out[key]
-            out["config"][key + "_sample"] = "%s; %s cores (%s)" % (
-                cb.get("sample"), cb.get("cores"), cb.get("kind"))
+    if world > 1:
+        out["rccl_ranks"] = rccl_ranks
+        if parity is not None:
+            out["parity"] = parity
+    if not args.no_cpu_baseline:
+        # the bench's own grid (rank 0's block at N > 1): the fields the device
+        # holds after the timed solve.  (A download of p exchanges its halo
+        # first on a decomposed grid, a collective: every rank takes part.)
+        hp = g.download(M.P)
+        if rank == 0:
+            hrhs = g.download(M.RHS)
+            try:
+                out["cpu_baseline"] = cpu_baseline(hp, hrhs)
+            except Exception as e:  # reported, never fatal for the GPU number
+                out["cpu_baseline"] = {"value": None, "error": repr(e)}
+            try:
+                out["cpu_baseline_multicore"] = cpu_baseline_multicore(hp, hrhs)
+            except Exception as e:
+                out["cpu_baseline_multicore"] = {"value": None, "error": repr(e)}
+            del hrhs
+            try:
+                out["cpu_baseline_mpi"] = cpu_baseline_mpi(granted_cores())
+            except Exception as e:
+                out["cpu_baseline_mpi"] = {"value": None, "error": repr(e)}
+            for key in ("cpu_baseline", "cpu_baseline_multicore", "cpu_baseline_mpi"):
+                cb = out[key]
+                out["config"][key + "_sample"] = "%s; %s cores (%s)" % (
+                    cb.get("sample"), cb.get("cores"), cb.get("kind"))
+            if world > 1:
+                out["config"]["cpu_baseline_block"] = "rank 0's block %dx%d" % (
+                    hp.shape[1] - 2, hp.shape[0] - 2)
+        del hp
     g.close()
     if dist is not None:
         dist.barrier()

@@ -119,6 +119,13 @@ typedef struct {
     long long allreduces;   /* all-reduces covered by allreduce_ms */
     int chained;            /* 1: the last multi-block solve's passes were chained runs
                              * (sor_tb.h rb_tbc_kernel / sor_tbh.h rb_tbhc_kernel) */
+    /* NS step kernels, timing on: HIP events on the grid stream around each
+     * launch.  [0] computeFG (+ the fused computeRHS, ns_kernels.hip
+     * fg_rhs_kernel), [1] adaptUV (+ the next dt's max |u|, |v| partials,
+     * adapt_absmax_kernel), [2] normalizePressure (max |p|, exact sum,
+     * subtract: absmax2 + finish_reduce, exact_sum, sub_mean kernels) */
+    double ns_ms[3];
+    long long ns_calls[3];
 } misor_stats;
 
 const char* misor_last_error(void);
@@ -160,6 +167,11 @@ int misor_gather(misor_grid* g, int field, double* host_global);
 int misor_exchange(misor_grid* g, int field, int depth);
 /* number of visible GPUs (host programs map rank -> device) */
 int misor_device_count(int* n);
+/* ranks of the grid's communicator as its transport counts them: ncclCommCount
+ * of the RCCL communicator (MPI_Comm_size of the reference's solver->comm,
+ * assignment-5/skeleton/src/solver.c:408,452), the member count of an
+ * in-process group, 1 for a single-rank grid */
+int misor_comm_ranks(const misor_grid* g, int* n);
 /* fill a field (incl. ghosts) with a constant; initSolver of NS (solver.c:92-99) */
 int misor_fill(misor_grid* g, int field, double value);
 
@@ -216,7 +228,9 @@ enum {
     MISOR_TUNE_TSTEPS = 6,         /* iterations per pass over HBM, 1..12: 1 = single-
                                     * iteration sweep kernel, T >= 2 = temporally blocked
                                     * kernel (T iterations per read of p and rhs); the
-                                    * iteration count and every bit of p are unchanged */
+                                    * iteration count and every bit of p are unchanged.
+                                    * A request binds every pass to T (no short pass
+                                    * plan); <= 0 returns to the default rule */
     MISOR_TUNE_TB_VARIANT = 7,     /* temporally blocked kernel: 0..4 strips per workgroup x
                                     * rows in flight */
     MISOR_TUNE_TB_ROWS = 8,        /* temporally blocked kernel: rows per block; <= 0: auto

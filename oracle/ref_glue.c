@@ -243,6 +243,69 @@ int refns_run(const char* par, double te, int max_steps, int solver, int* iters,
     return nt;
 }
 
+static double now_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+/* The CPU baseline of bench.py --workload ns: `steps`
+ * time steps of the composed RB-NS loop above (the reference's functions,
+ * assignment-5/sequential/src/main.c:43-60 with assignment-4's solveRB) on the
+ * .par's problem resized to imax x jmax with the solve capped at itermax;
+ * initSolver is not timed (as main.c:51 starts its clock after it).  Returns
+ * the steps run; *solve_s = seconds inside solveRB, *step_s = seconds of the
+ * whole steps, *sweeps = iterations done. */
+int refns_timed(const char* par, int imax, int jmax, int itermax, int steps, double* solve_s,
+                double* step_s, long long* sweeps)
+{
+    Parameter prm;
+    Solver s;
+    initParameter(&prm);
+    prm.name = NULL;
+    readParameter(&prm, par);
+    prm.imax = imax;
+    prm.jmax = jmax;
+    prm.itermax = itermax;
+    initSolver(&s, &prm);
+
+    A4Solver a4;
+    memset(&a4, 0, sizeof a4);
+    a4.dx = s.dx; a4.dy = s.dy; a4.imax = s.imax; a4.jmax = s.jmax;
+    a4.p = s.p; a4.rhs = s.rhs; a4.eps = s.eps; a4.omega = s.omega;
+    a4.itermax = s.itermax;
+
+    double tsolve = 0.0, tstep = 0.0;
+    long long it_all = 0;
+    int nt = 0;
+    for (; nt < steps; ++nt) {
+        const double t0 = now_s();
+        if (s.tau > 0.0) computeTimestep(&s);
+        setBoundaryConditions(&s);
+        setSpecialBoundaryCondition(&s);
+        computeFG(&s);
+        computeRHS(&s);
+        if (nt % 100 == 0) normalizePressure(&s);
+        const double t1 = now_s();
+        capture_begin();
+        a4_solveRB(&a4);
+        char* out = capture_end();
+        const double t2 = now_s();
+        it_all += atoi(out);
+        free(out);
+        adaptUV(&s);
+        tsolve += t2 - t1;
+        tstep += now_s() - t0;
+    }
+    *solve_s = tsolve;
+    *step_s = tstep;
+    *sweeps = it_all;
+    free(s.u); free(s.v); free(s.p); free(s.rhs); free(s.f); free(s.g);
+    free(prm.name);
+    return nt;
+}
+
 /* writeResult of the sequential NS (pressure.dat, velocity.dat in cwd) after
  * a run -- used to regenerate the committed .dat format */
 int refns_run_and_write(const char* par, double te, int solver)

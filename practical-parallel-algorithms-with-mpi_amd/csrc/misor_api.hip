@@ -135,7 +135,7 @@ struct misor_grid {
     SweepParams sp{};
     int nbx = 0, nby = 0, nparts = 0, partials_cap = 0;
     double* partials = nullptr;  // two slots of partials_cap doubles (by pass parity)
-    bool finish2 = true;  // single rank: two-level loop test (MISOR_FINISH2=0: one kernel)
+    bool finish2 = true;  // single rank: two-level loop test (MISOR_TUNE_FINISH2 = 0: one kernel)
     DevState* st = nullptr;
     DevState* st_host = nullptr;  // pinned
     int last_iters = 0;
@@ -157,7 +157,6 @@ struct misor_grid {
     bool tb_persistent = true;    // MISOR_TUNE_TB_PERSISTENT: work-queue launches
     int tb_reserve = kTbReserve;  // MISOR_TUNE_TB_RESERVE: slots a pipelined interior launch
                                   // leaves to the communication / edge-block streams
-    bool finish_merge = true;     // finish2 in one launch (tb_queue[9]: its counter)
     int* tb_queue = nullptr;      // 8 per-XCD block counters of a persistent launch + its exit count
     // chained passes (sor_tb.h rb_tbc_kernel; MISOR_TUNE_TB_CHAIN): the initial
     // segment list of every pass length and part (0: whole pass, 1: interior
@@ -173,7 +172,7 @@ struct misor_grid {
     };
     struct ChainPlan {
         ChainList main, edge;
-        int reserve = -1;  // part 1 of a one-list plan: the slots it leaves to part 2
+        int reserve = -1;  // part 1 of a pipelined pass: the slots it leaves to part 2
         bool built = false;
     } chain_plan[2][kMaxT + 1][3];  // [the default variant's / the split ring's][T][part]
     int* tb_work[4] = {nullptr, nullptr, nullptr, nullptr};  // main / edge x parts 0-1 / 2
@@ -202,11 +201,12 @@ struct misor_grid {
     std::shared_ptr<LocalGroup> local;                   // in-process transport
     bool overlap = true;            // exchange on cstream while the interior sweeps
     hipStream_t cstream = nullptr;  // communication stream
-    hipStream_t estream = nullptr;  // edge blocks of a pipelined pass
-    hipEvent_t ev_s = nullptr, ev_x = nullptr, ev_d = nullptr, ev_e = nullptr;
+    hipEvent_t ev_s = nullptr, ev_x = nullptr, ev_d = nullptr;
     hipEvent_t ev_i[2] = {}, ev_dk[2] = {};  // interior blocks / decide of pass k, by k & 1
     hipEvent_t ev_e2[2] = {};                // edge blocks of pass k on cstream, by k & 1
-    bool p2_cstream = true;                  // MISOR_P2_CSTREAM (the pipelined loop's part 2)
+#ifdef MISOR_PROXY
+    bool proxy = false;  // MISOR_PROXY_SIDES: a measurement proxy, fields meaningless
+#endif
     double* sendbuf = nullptr;
     double* recvbuf = nullptr;
     double* gbuf = nullptr;  // misor_gather: this rank's owned block, packed
@@ -230,6 +230,10 @@ struct misor_grid {
     bool timing = false;
     std::vector<hipEvent_t> ev;
     misor_stats stats{};
+    // NS kernel timing (misor_stats.ns_ms): start/stop event pairs by kernel
+    // group, resolved by misor_get_stats (or when a pool is full)
+    std::vector<hipEvent_t> nev[3];
+    size_t nev_used[3] = {0, 0, 0};
 };
 
 // pressure buffer x (mod np)
@@ -326,9 +330,6 @@ void misor_destroy(misor_grid* g) {
     (void)hipFree(g->rsq);
     if (g->cstream) (void)hipStreamSynchronize(g->cstream);
     if (g->cstream) (void)hipStreamDestroy(g->cstream);
-    if (g->estream) (void)hipStreamSynchronize(g->estream);
-    if (g->estream) (void)hipStreamDestroy(g->estream);
-    if (g->ev_e) (void)hipEventDestroy(g->ev_e);
     for (int b = 0; b < 2; ++b) {
         if (g->ev_i[b]) (void)hipEventDestroy(g->ev_i[b]);
         if (g->ev_dk[b]) (void)hipEventDestroy(g->ev_dk[b]);
@@ -339,6 +340,8 @@ void misor_destroy(misor_grid* g) {
     if (g->ev_d) (void)hipEventDestroy(g->ev_d);
     for (auto e : g->ev) (void)hipEventDestroy(e);
     for (auto& v : g->cev)
+        for (auto e : v) (void)hipEventDestroy(e);
+    for (auto& v : g->nev)
         for (auto e : v) (void)hipEventDestroy(e);
     for (hipEvent_t e : {g->lx_pk, g->lx_cp, g->la_val[0], g->la_val[1], g->la_rd[0], g->la_rd[1],
                          g->la_cmb[0], g->la_cmb[1]})
@@ -645,8 +648,6 @@ static int pick_tb_rows(int ni, int nj, int T, int variant) {
     const long long nbx = tb_nbx(ni, T, variant);
     const int S = tb_ring_slots(T, variant);
     auto on_ring = [&](int h) { return S * std::max(1, (h + S / 2) / S); };
-    const char* e = getenv("MISOR_TB_TARGET_ROWS");  // tuning experiments (tools/)
-    if (e && atoi(e) > 0) return on_ring(atoi(e));
     // the tallest of the ladder that still gives the launch ~6 blocks per
     // resident workgroup (3000 blocks)
     int h = kTbRowLadder[0];
@@ -704,10 +705,8 @@ static void tb_geometry(const misor_grid* g, int T, SweepParams& tp) {
     if (tp.chain) {
         // chained passes: short blocks (the unit of residual partials and of
         // work stealing), long runs; every block row but the last a multiple
-        // of the ring (MISOR_TB_CHAIN_RINGS: tuning experiments)
-        const char* er = getenv("MISOR_TB_CHAIN_RINGS");
-        const int rings = er && atoi(er) > 0 ? atoi(er)
-                          : tp.variant == kHrTbVariant
+        // of the ring
+        const int rings = tp.variant == kHrTbVariant
                               ? (g->dist ? kHrChainRingsDist : kHrChainRingsPerBlock)
                               : kChainRingsPerBlock;
         int h = req > 0 ? S * std::max(1, (req + S / 2) / S) : rings * S;
@@ -721,11 +720,8 @@ static void tb_geometry(const misor_grid* g, int T, SweepParams& tp) {
     }
     int h = req > 0 ? req : pick_tb_rows(g->loc.ni, nj, T, tp.variant);
     if (h > nj) h = nj;
-    // MISOR_TB_SMALL_ROWS / MISOR_TB_BAND_ROUNDS: tuning experiments (tools/geom_sweep.py)
-    const char* es = getenv("MISOR_TB_SMALL_ROWS");
-    const char* eb = getenv("MISOR_TB_BAND_ROUNDS");
-    const int small_rows = es && atoi(es) > 0 ? atoi(es) : kTbSmallRows;
-    const double band_rounds = eb && atof(eb) >= 0 ? atof(eb) : kTbSmallRounds;
+    const int small_rows = kTbSmallRows;
+    const double band_rounds = kTbSmallRounds;
     const int hs = S * std::max(1, (small_rows + S / 2) / S);
     int nbig = 0, ns = 0;
     if (req > 0 || hs >= h || nj < 4 * hs) {  // uniform blocks, the last takes the rest
@@ -815,32 +811,21 @@ static int chain_plan(misor_grid* g, int variant, int Tp, int part,
     // steady-able (a segment of its own) that much plus its 4T warm-up rows.
     // The segments are cut so that each costs about (total / resident
     // workgroups): every workgroup starts one at once and they end together.
-    const char* ec = getenv("MISOR_CHAIN_EDGE_COST");
-    const double E = ec && atof(ec) > 0 ? atof(ec)
-                     : variant == kHrTbVariant ? (g->dist ? kHrChainEdgeCostDist : kHrChainEdgeCost)
-                                               : kChainEdgeCost;
+    const double E = variant == kHrTbVariant ? (g->dist ? kHrChainEdgeCostDist : kHrChainEdgeCost)
+                                             : kChainEdgeCost;
     const int H = tp.rows_per_block;
-    // Plan forms of the split ring (MISOR_HR_PLAN, A/B experiments; round 5):
-    //  0: main and edge lists, segments of cost / resident workgroups;
-    //  1: one list -- the edge columns' segments join the main list (the same
-    //     kernel runs both, sor_tbh.h hr_chain_run decides per strip), exactly
-    //     one item per workgroup (the singles first, then as many segments as
-    //     workgroups are left) -- measured 1-3% SLOWER than 0 at 32768^2 and
-    //     on the 8-GPU rank block (profiles/r05_hr_plan_ab.txt): edge-column
-    //     blocks ran 1.4x longer among the main list's;
-    //  2 (default): the two lists of 0 with the pipelined pass's part-2 slots
-    //     sized to its cost share (below): the 8-GPU rank block's pipelined
-    //     loop 0.130-0.135 against 0.145-0.147 ms per iteration with physical
-    //     left and bottom sides, 0.130-0.131 against 0.136-0.138 with the bottom
-    //     one only (profiles/r05_reserve_ab.txt).
-    static const int hr_plan = [] {
-        const char* e = getenv("MISOR_HR_PLAN");
-        return e ? atoi(e) : 2;
-    }();
-    const bool one = variant == kHrTbVariant && hr_plan == 1;
-    const bool sized = variant == kHrTbVariant && (hr_plan == 1 || hr_plan == 2) && part != 0;
+    // The split ring's plan (round 5): main and edge lists, segments of cost /
+    // resident workgroups, and the pipelined pass's part-2 slots sized to its
+    // cost share (below): the 8-GPU rank block's pipelined loop 0.130-0.135
+    // against 0.145-0.147 ms per iteration with physical left and bottom
+    // sides, 0.130-0.131 against 0.136-0.138 with the bottom one only
+    // (profiles/r05_reserve_ab.txt).  One list for both kinds of column with
+    // exactly one item per workgroup measured 1-3% slower at 32768^2 and on
+    // the 8-GPU rank block (profiles/r05_hr_plan_ab.txt: edge-column blocks ran
+    // 1.4x longer among the main list's) and was removed.
+    const bool sized = variant == kHrTbVariant && part != 0;
     std::vector<unsigned long long> singles;
-    double cost = 0, cost_singles = 0;
+    double cost = 0;
     long long Bm = 0, Be = 0;
     for (int bx = 0; bx < nbx; ++bx) {
         const bool ecol = edge_col(bx);
@@ -849,11 +834,10 @@ static int chain_plan(misor_grid* g, int variant, int Tp, int part,
             if (!steady(by)) {
                 singles.push_back(chain_word(bx, by, by + 1));
                 cost += E * (H + 4.0 * Tp) / H;
-                cost_singles += E * (H + 4.0 * Tp) / H;
                 ++Bm;
             } else {
                 cost += ecol ? E : 1.0;
-                ++(ecol && !one ? Be : Bm);
+                ++(ecol ? Be : Bm);
             }
         }
     }
@@ -899,19 +883,6 @@ static int chain_plan(misor_grid* g, int variant, int Tp, int part,
             }
         }
     };
-    if (one) {
-        if (!sized) Gp = std::max(8, G - (part == 1 ? g->tb_reserve : 0));
-        const long long ns = (long long)singles.size();
-        if (ns < Gp / 2) {
-            per = std::max(1.0, (cost - cost_singles) / (double)(Gp - ns));
-            for (int guard = 0; guard < 200; ++guard) {  // at most Gp items in all
-                long long cnt = ns;
-                each_run([&](int, int, int n, bool ecol) { cnt += pieces(n, ecol ? E : 1.0); });
-                if (cnt <= Gp) break;
-                per *= 1.01;
-            }
-        }
-    }
     std::vector<unsigned long long> edge, inner;  // inner: column-interleaved
     std::vector<std::vector<unsigned long long>> col(nbx);
     each_run([&](int bx, int by, int n, bool ecol) {
@@ -919,7 +890,7 @@ static int chain_plan(misor_grid* g, int variant, int Tp, int part,
         for (int q = 0; q < k; ++q) {
             const unsigned long long w = chain_word(
                 bx, by + (int)((long long)n * q / k), by + (int)((long long)n * (q + 1) / k));
-            if (ecol && !one) edge.push_back(w);
+            if (ecol) edge.push_back(w);
             else col[bx].push_back(w);
         }
     });
@@ -1002,10 +973,6 @@ static int configure_tb(misor_grid* g, int T, int variant, int rows) {
     // The short plan (solve_rb_from): a single-rank solve capped at few
     // iterations runs them in fewer, longer passes of the split-ring kernel
     // when that saves a pass; its geometries share the partials
-    static const bool short_env = [] {
-        const char* e = getenv("MISOR_SHORT_PLAN");
-        return !(e && e[0] == '0');
-    }();
     // Where (round 5, the chained split ring; profiles/r05_plan_ab*.txt, wall
     // ms per iteration of 20- and 100-iteration solves against the T = 8 plan):
     //  - blocks of [2^26, 2^28) cells, where the T = 8 passes are chained
@@ -1023,7 +990,7 @@ static int configure_tb(misor_grid* g, int T, int variant, int rows) {
     const bool small_chain = cells >= kHrAllCells && cells < kTsteps8Cells &&
                              chain_on(g, variant);
     g->short_all = small_chain || (!g->dist && cells >= 2 * kTsteps8Cells);
-    g->short_plan = short_env && variant == kDefaultTbVariant && !g->tsteps_set &&
+    g->short_plan = variant == kDefaultTbVariant && !g->tsteps_set &&
                     g->tb_persistent &&
                     (g->short_all ||
                      (!chain_on(g, variant) &&
@@ -1105,14 +1072,17 @@ int misor_create(misor_grid** out, const misor_desc* d) {
     misor_local L{};
     int rc = misor_decompose(nranks, nranks == 1 ? 0 : d->rank, d->imax, d->jmax, d->dims, &L);
     if (rc) return rc;
-    // Measurement proxy (tools/scale_proxy.py --sides): one rank on a one-rank
-    // communicator whose sides NOT named in MISOR_PROXY_SIDES (of "LRBT") are
-    // treated as bordering another rank -- rank 0 itself: the exchange sends
-    // each halo region to itself, sizes matching, contents meaningless -- so the
-    // block runs the pass loop of a rank of a larger decomposition (split
-    // launches, 2T-deep halo cones, exchanges, all-reduce) on one GPU.  Timing
-    // only: the field it computes is not the reference's.
+    // Measurement proxy, in an experiment build only (make ab B=build_proxy
+    // L=lib_proxy XFLAGS=-DMISOR_PROXY; tools/scale_proxy.py --sides): one rank
+    // on a one-rank communicator whose sides NOT named in MISOR_PROXY_SIDES (of
+    // "LRBT") are treated as bordering another rank -- rank 0 itself: the
+    // exchange sends each halo region to itself, sizes matching, contents
+    // meaningless -- so the block runs the pass loop of a rank of a larger
+    // decomposition (split launches, 2T-deep halo cones, exchanges, all-reduce)
+    // on one GPU.  Timing only: the field it computes is not the reference's,
+    // so misor_download / misor_gather refuse it (MISOR_ESTATE).
     bool proxy = false;
+#ifdef MISOR_PROXY
     if (nranks == 1 && d->comm_id) {
         const char* ps = getenv("MISOR_PROXY_SIDES");
         if (ps) {
@@ -1122,8 +1092,12 @@ int misor_create(misor_grid** out, const misor_desc* d) {
                 if (!strchr(ps, sides[k])) L.neighbours[k] = 0;
         }
     }
+#endif
 
     misor_grid* g = new misor_grid();
+#ifdef MISOR_PROXY
+    g->proxy = proxy;
+#endif
     g->desc = *d;
     g->desc.nranks = nranks;
     g->loc = L;
@@ -1183,8 +1157,7 @@ int misor_create(misor_grid** out, const misor_desc* d) {
         // power-of-two spacing (sor_tb.h resid<true>): 1/dx^2 == 1/dy^2 == 2^m, m >= 0
         int e = 0;
         const double mant = frexp(sp.idx2, &e);
-        const char* no = getenv("MISOR_NO_POW2");  // A/B switch (tools/ab_env.py)
-        sp.pow2 = sp.idx2 == sp.idy2 && mant == 0.5 && e >= 1 && !(no && no[0] == '1');
+        sp.pow2 = sp.idx2 == sp.idy2 && mant == 0.5 && e >= 1;
     }
     if (d->variant == MISOR_SOLVE_RBA) {
         const double factor = 0.5 * (dx2 * dy2) / (dx2 + dy2);  // solver.c:250
@@ -1253,10 +1226,8 @@ int misor_create(misor_grid** out, const misor_desc* d) {
         int prio_lo = 0, prio_hi = 0;
         (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
         bool ok = hipStreamCreateWithPriority(&g->cstream, hipStreamNonBlocking, prio_hi) ==
-                      hipSuccess &&
-                  hipStreamCreateWithPriority(&g->estream, hipStreamNonBlocking, prio_hi) ==
-                      hipSuccess;
-        for (hipEvent_t* e : {&g->ev_s, &g->ev_x, &g->ev_d, &g->ev_e, &g->ev_i[0], &g->ev_i[1],
+                  hipSuccess;
+        for (hipEvent_t* e : {&g->ev_s, &g->ev_x, &g->ev_d, &g->ev_i[0], &g->ev_i[1],
                               &g->ev_e2[0], &g->ev_e2[1],
                               &g->ev_dk[0], &g->ev_dk[1]})
             ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
@@ -1306,17 +1277,6 @@ int misor_create(misor_grid** out, const misor_desc* d) {
             if (ncclCommInitRank(&g->comm, nranks, id, d->rank) != ncclSuccess)
                 CREATE_FAIL(MISOR_ECOMM, "ncclCommInitRank failed");
         }
-    }
-    {
-        const char* e = getenv("MISOR_FINISH2");
-        g->finish2 = !(e && e[0] == '0');
-        // the loop test in the partial-sum launch's last workgroup (A/B: 0)
-        e = getenv("MISOR_FINISH_MERGE");
-        g->finish_merge = !(e && e[0] == '0');
-        e = getenv("MISOR_P2_CSTREAM");  // A/B: 0 = part 2 on its own stream
-        g->p2_cstream = !(e && e[0] == '0');
-        e = getenv("MISOR_NS_FUSE");  // A/B switch (bench.py --workload ns)
-        g->ns_fuse = !(e && e[0] == '0');
     }
     if (configure_tb(g, default_tsteps(g, kDefaultTbVariant), kDefaultTbVariant, 0) != MISOR_OK)
         CREATE_FAIL(MISOR_ENOMEM, "%s", g_err.c_str());
@@ -1396,8 +1356,21 @@ int misor_upload(misor_grid* g, int field, const double* host) {
     return MISOR_OK;
 }
 
+#ifdef MISOR_PROXY
+#define PROXYCHK(g)                                                                        \
+    do {                                                                                   \
+        if ((g)->proxy)                                                                    \
+            return fail(MISOR_ESTATE, "a MISOR_PROXY_SIDES grid holds no meaningful field"); \
+    } while (0)
+#else
+#define PROXYCHK(g) \
+    do {            \
+    } while (0)
+#endif
+
 int misor_download(misor_grid* g, int field, double* host) {
     if (!g || !host || !field_ptr(g, field)) return fail(MISOR_EINVAL, "bad download");
+    PROXYCHK(g);
     HIPCHK(hipSetDevice(g->device));
     if (field == MISOR_P) {  // the local block with a consistent halo
         int rc = p_halo(g);
@@ -1433,6 +1406,7 @@ static OwnedBlock owned_block(const misor_local& L) {
 
 int misor_gather(misor_grid* g, int field, double* host) {
     if (!g || !field_ptr(g, field)) return fail(MISOR_EINVAL, "bad gather");
+    PROXYCHK(g);
     const int rank = g->dist ? g->desc.rank : 0;
     if (rank == 0 && !host) return fail(MISOR_EINVAL, "gather: rank 0 needs the global array");
     if (g->desc.nranks == 1) return misor_download(g, field, host);
@@ -1559,6 +1533,20 @@ int misor_exchange(misor_grid* g, int field, int depth) {
 int misor_device_count(int* n) {
     if (!n) return fail(MISOR_EINVAL, "null argument");
     HIPCHK(hipGetDeviceCount(n));
+    return MISOR_OK;
+}
+
+int misor_comm_ranks(const misor_grid* g, int* n) {
+    if (!g || !n) return fail(MISOR_EINVAL, "null argument");
+    if (g->comm) {
+        NCCLCHK(ncclCommCount(g->comm, n));
+    } else if (g->local) {
+        *n = g->local->n;
+    } else if (g->comm_dead) {
+        return fail(MISOR_ECOMM, "the communicator was aborted by an earlier error");
+    } else {
+        *n = 1;
+    }
     return MISOR_OK;
 }
 
@@ -1918,18 +1906,13 @@ static int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* 
                     for (int x = 0; x < 9; ++x) q.seg_run[x] = L.run[x];
                 };
                 const int eg = pl->edge.nseg0;  // edge workgroups: one per initial segment
-                // Where the two kernels run.  Default (3): the main kernel forked to
-                // xstream, the edge kernel on s.  The other way round (0: edge on
-                // xstream, launched first; 1: launched after the main one) the edge
-                // kernel's 16-odd workgroups did not start until the main kernel's
-                // workgroups retired, in every pass of a multi-pass solve but the
-                // first, though its slots were free (profiles/r03_chain_xmode.txt:
-                // 8.5-8.9 ms per 32768^2 pass against 6.0); 2: both on s, serialised.
-                // MISOR_CHAIN_XMODE: experiments.
-                static const int xmode = [] {
-                    const char* e = getenv("MISOR_CHAIN_XMODE");
-                    return e ? atoi(e) : 3;
-                }();
+                // Where the two kernels run: the main kernel forked to xstream,
+                // the edge kernel on s.  The other way round (the edge kernel on
+                // xstream, launched first or after the main one) its 16-odd
+                // workgroups did not start until the main kernel's workgroups
+                // retired, in every pass of a multi-pass solve but the first,
+                // though its slots were free (profiles/r03_chain_xmode.txt: 8.5-8.9
+                // ms per 32768^2 pass against 6.0).
                 SweepParams te = tp;
                 use(te, pl->edge);
                 te.chain_edge = 1;
@@ -1941,20 +1924,16 @@ static int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* 
                 tm.reserve += pl->edge.blocks > 0 ? eg : 0;
                 const bool has_e = pl->edge.blocks > 0, has_m = pl->main.blocks > 0;
                 // (no edge list: the main kernel alone, on s)
-                const bool fork = has_e && has_m && xmode != 2;
-                hipStream_t es = fork && xmode != 3 ? g->xstream[k] : s;
-                hipStream_t ms = fork && xmode == 3 ? g->xstream[k] : s;
+                const bool fork = has_e && has_m;
+                hipStream_t ms = fork ? g->xstream[k] : s;
                 if (fork) {
                     HIPCHK(hipEventRecord(g->ev_fork[k], s));
                     HIPCHK(hipStreamWaitEvent(g->xstream[k], g->ev_fork[k], 0));
                 }
-                auto launch_e = [&]() {
-                    launch_tb(es, Tp, te, src, dst, rhs, partials, g->st, force, g->tb_work[2 + k]);
-                };
-                if (has_e && xmode != 1) launch_e();
+                if (has_e)
+                    launch_tb(s, Tp, te, src, dst, rhs, partials, g->st, force, g->tb_work[2 + k]);
                 if (has_m)
                     launch_tb(ms, Tp, tm, src, dst, rhs, partials, g->st, force, g->tb_work[k]);
-                if (has_e && xmode == 1) launch_e();
                 if (fork) {
                     HIPCHK(hipEventRecord(g->ev_join[k], g->xstream[k]));
                     HIPCHK(hipStreamWaitEvent(s, g->ev_join[k], 0));
@@ -1981,10 +1960,10 @@ static int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* 
     // pass k-2 -- so pass k waits for the loop test of pass k-2 only (a pass that
     // overshoots convergence is recomputed from its source), and the all-reduce
     // + loop test of pass k-1 run while pass k sweeps.  Within a pass the
-    // interior blocks (main stream) and the edge blocks (estream: those whose
-    // cone reads src's halo; they alone write dst's send region) run
-    // concurrently; the exchange of dst's halo for pass k+1 starts on cstream as
-    // soon as the edge blocks are done, and so overlaps the interior blocks.
+    // interior blocks (part 1, main stream) and the edge blocks (part 2, on
+    // cstream: those whose cone reads src's halo; they alone write dst's send
+    // region) run concurrently; the exchange of dst's halo for pass k+1 follows
+    // the edge blocks on cstream, and so overlaps the interior blocks.
     const bool pipelined = g->dist && g->overlap && T > 1;
     // (the exchange of the first source follows the first pass's interior
     // launch on the host: RCCL's host side of a grouped send / receive takes
@@ -1994,7 +1973,6 @@ static int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* 
     if (pipelined) {
         HIPCHK(hipEventRecord(g->ev_s, g->stream));  // state upload, rhs halo, prior work
         HIPCHK(hipStreamWaitEvent(g->cstream, g->ev_s, 0));
-        HIPCHK(hipStreamWaitEvent(g->estream, g->ev_s, 0));
     }
     // passes plan the iterations still to do (it0 of them are done: a solve
     // resumed after an exact tail)
@@ -2006,18 +1984,10 @@ static int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* 
     // nearly as much with fewer iterations (a T' = 4 pass at 32768^2 is
     // HBM-bound at 5.06 ms against 5.41 for T = 8), so 20 iterations run as
     // 7 + 7 + 6 rather than 8 + 8 + 4.  A solve that converges earlier stops
-    // at the same iteration either way.  MISOR_EVEN_PASSES=0 (A/B): T, T, ...,
-    // and the rest last.
-    static const bool even = [] {
-        const char* e = getenv("MISOR_EVEN_PASSES");
-        return !(e && e[0] == '0');
-    }();
-    const long long base = even ? todo / max_passes : T;
-    const long long extra = even ? todo % max_passes : 0;
-    auto t_of = [&](long long k) -> int {
-        if (!even) return k == max_passes - 1 ? (int)(todo - k * T) : T;
-        return (int)(base + (k < extra ? 1 : 0));
-    };
+    // at the same iteration either way.
+    const long long base = todo / max_passes;
+    const long long extra = todo % max_passes;
+    auto t_of = [&](long long k) -> int { return (int)(base + (k < extra ? 1 : 0)); };
     auto nparts_of = [&](int Tk) -> int {
         if (T == 1 || Tk == T) return nparts;
         SweepParams tp = tpl;
@@ -2025,12 +1995,8 @@ static int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* 
         return tb_parts(tp);
     };
     // iterations covered by the first p passes, and the passes that cover `it`
-    auto covered = [&](long long p) -> long long {
-        if (!even) return std::min(p * T, (long long)todo);
-        return p * base + std::min(p, extra);
-    };
+    auto covered = [&](long long p) -> long long { return p * base + std::min(p, extra); };
     auto passes_for = [&](long long it) -> long long {
-        if (!even) return std::min((it + T - 1) / T, max_passes);
         const long long head = extra * (base + 1);  // iterations of the longer passes
         if (it <= head) return (it + base) / (base + 1);
         return std::min(extra + (it - head + base - 1) / base, max_passes);
@@ -2062,96 +2028,55 @@ static int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* 
                 if (rc_) return rc_;
             }
             HIPCHK(hipEventRecord(g->ev_i[k & 1], g->stream));
-            if (g->p2_cstream) {
-                // Part 2 (the blocks whose cone reads the halo) on the comm
-                // stream, right behind what it waits for: pass k+1's part 2 is
-                // enqueued here, after pass k's exchange, loop test and part 1
-                // (its source is pass k's result), so no cross-stream wait
-                // stands between the exchange and it.  (On a stream of its own,
-                // waiting for the exchange on the comm stream and the interior
-                // blocks on this one, the second pass's part 2 started ~0.5 ms
-                // late on the 8-GPU rank block: profiles/r05_decomposed_loop_trace*.)
-                int rc = MISOR_OK;
-                if (first_x) {  // the solve's first pass: src's halo, then its part 2
-                    first_x = false;
-                    rc = exchange(g, const_cast<double*>(src), depth, g->cstream);
-                    if (rc) return rc;
-                    rc = pass(g->cstream, 2, src, dst, Tk, 0, part);
-                    if (rc) return rc;
-                    HIPCHK(hipEventRecord(g->ev_e2[k & 1], g->cstream));
-                }
-                if (k + 1 < max_passes) {  // dst's halo (part 2 of pass k, above, wrote its send region)
-                    rc = exchange(g, dst, depth, g->cstream);
-                    if (rc) return rc;
-                }
-                HIPCHK(hipStreamWaitEvent(g->cstream, g->ev_i[k & 1], 0));
-                if (g->finish_merge)
-                    launch_finish2(g->cstream, part, nparts_of(Tk), Tk, g->st, cells,
-                                   g->partials + 2 * (long long)g->partials_cap,
-                                   g->tb_queue + 10, 0);
-                else
-                    launch_finish(g->cstream, part, nparts_of(Tk), Tk, g->st, cells, 0);
-                rc = allreduce(g, g->st->sum, Tk, 0, g->cstream);
-                if (rc) return rc;
-                launch_decide(g->cstream, g->st, Tk, cells);
-                HIPCHK(hipEventRecord(g->ev_dk[k & 1], g->cstream));
-                if (k + 1 < max_passes) {  // pass k+1's part 2: after both parts of pass k
-                    const long long k1 = k + 1;
-                    double* part1 = g->partials + (k1 & 1) * (long long)g->partials_cap;
-                    rc = pass(g->cstream, 2, dst, pbuf(g, cur0 + k1 + 1), t_of(k1), 0, part1);
-                    if (rc) return rc;
-                    HIPCHK(hipEventRecord(g->ev_e2[k1 & 1], g->cstream));
-                }
-                // pass k+1's interior blocks read what part 2 of pass k wrote
-                HIPCHK(hipStreamWaitEvent(g->stream, g->ev_e2[k & 1], 0));
-                if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b + 1], g->stream));
-                if (b == batch - 1)  // the host reads the loop state after the last decide
-                    HIPCHK(hipStreamWaitEvent(g->stream, g->ev_dk[k & 1], 0));
-                continue;
-            }
-            if (first_x) {  // src's halo for the first pass
-                first_x = false;
-                int rc = exchange(g, pbuf(g, cur0), depth, g->cstream);
-                if (rc) return rc;
-                HIPCHK(hipEventRecord(g->ev_x, g->cstream));
-            }
-            // edge blocks: after the interior blocks of pass k-1, the edge blocks
-            // of k-1 (this stream) and the exchange of src's halo (which follows
-            // decide k-2 on cstream)
-            if (k >= 1) HIPCHK(hipStreamWaitEvent(g->estream, g->ev_i[(k - 1) & 1], 0));
-            HIPCHK(hipStreamWaitEvent(g->estream, g->ev_x, 0));
-            {
-                int rc_ = pass(g->estream, 2, src, dst, Tk, 0, part);
-                if (rc_) return rc_;
-            }
-            HIPCHK(hipEventRecord(g->ev_e, g->estream));
-            // cstream: dst's halo for pass k+1 (none after the last planned
-            // pass: the result's halo is left to its next reader, p_halo), then
-            // the residual of pass k
-            HIPCHK(hipStreamWaitEvent(g->cstream, g->ev_e, 0));
+            // Part 2 (the blocks whose cone reads the halo) on the comm stream,
+            // right behind what it waits for: pass k+1's part 2 is enqueued here,
+            // after pass k's exchange, loop test and part 1 (its source is pass
+            // k's result), so no cross-stream wait stands between the exchange
+            // and it.  (On a stream of its own, waiting for the exchange on the
+            // comm stream and the interior blocks on this one, the second pass's
+            // part 2 started ~0.5 ms late on the 8-GPU rank block:
+            // profiles/r05_decomposed_loop_trace*.)  The first pass of a batch
+            // enqueues its own part 2: the previous batch's last pass leaves it
+            // out, so nothing of a batch is still queued on the comm stream
+            // behind the decide the host reads -- a solve that stops there (or a
+            // near-threshold hand-off to exact_tail, whose state upload would
+            // re-arm the device flag) leaves no pending launch that could still
+            // write a pressure buffer.
             int rc = MISOR_OK;
-            if (k + 1 < max_passes) {
+            if (first_x) {  // the solve's first pass: src's halo, then its part 2
+                first_x = false;
+                rc = exchange(g, const_cast<double*>(src), depth, g->cstream);
+                if (rc) return rc;
+            }
+            if (b == 0) {
+                rc = pass(g->cstream, 2, src, dst, Tk, 0, part);
+                if (rc) return rc;
+                HIPCHK(hipEventRecord(g->ev_e2[k & 1], g->cstream));
+            }
+            if (k + 1 < max_passes) {  // dst's halo (part 2 of pass k, above, wrote its send region)
                 rc = exchange(g, dst, depth, g->cstream);
                 if (rc) return rc;
-                HIPCHK(hipEventRecord(g->ev_x, g->cstream));
             }
             HIPCHK(hipStreamWaitEvent(g->cstream, g->ev_i[k & 1], 0));
             // the pass's residual sums for the all-reduce: the two-level sum (many
             // workgroups, the last one writing st->sum) -- one workgroup summing
             // every block partial took 70-100 us, after the last pass on the
             // solve's critical path (profiles/r05_decomposed_loop_trace.csv)
-            if (g->finish_merge)
-                launch_finish2(g->cstream, part, nparts_of(Tk), Tk, g->st, cells,
-                               g->partials + 2 * (long long)g->partials_cap, g->tb_queue + 10,
-                               0);
-            else
-                launch_finish(g->cstream, part, nparts_of(Tk), Tk, g->st, cells, 0);
+            launch_finish2(g->cstream, part, nparts_of(Tk), Tk, g->st, cells,
+                           g->partials + 2 * (long long)g->partials_cap, g->tb_queue + 10, 0);
             rc = allreduce(g, g->st->sum, Tk, 0, g->cstream);
             if (rc) return rc;
             launch_decide(g->cstream, g->st, Tk, cells);
             HIPCHK(hipEventRecord(g->ev_dk[k & 1], g->cstream));
-            // pass k+1's interior blocks read what the edge blocks of pass k wrote
-            HIPCHK(hipStreamWaitEvent(g->stream, g->ev_e, 0));
+            if (k + 1 < max_passes && b + 1 < batch) {  // pass k+1's part 2: after both parts of pass k
+                const long long k1 = k + 1;
+                double* part1 = g->partials + (k1 & 1) * (long long)g->partials_cap;
+                rc = pass(g->cstream, 2, dst, pbuf(g, cur0 + k1 + 1), t_of(k1), 0, part1);
+                if (rc) return rc;
+                HIPCHK(hipEventRecord(g->ev_e2[k1 & 1], g->cstream));
+            }
+            // pass k+1's interior blocks read what part 2 of pass k wrote
+            HIPCHK(hipStreamWaitEvent(g->stream, g->ev_e2[k & 1], 0));
             if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b + 1], g->stream));
             if (b == batch - 1)  // the host reads the loop state after the last decide
                 HIPCHK(hipStreamWaitEvent(g->stream, g->ev_dk[k & 1], 0));
@@ -2223,10 +2148,9 @@ static int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* 
                 int rc = allreduce(g, g->st->sum, Tk, 0);
                 if (rc) return rc;
                 launch_decide(g->stream, g->st, Tk, cells);
-            } else if (g->finish2) {
+            } else if (g->finish2) {  // the loop test in the last workgroup (tb_queue[9])
                 launch_finish2(g->stream, g->partials, nparts_of(Tk), Tk, g->st, cells,
-                               g->partials + 2 * (long long)g->partials_cap,
-                               g->finish_merge ? g->tb_queue + 9 : nullptr, 1);
+                               g->partials + 2 * (long long)g->partials_cap, g->tb_queue + 9, 1);
             } else {
                 launch_finish(g->stream, g->partials, nparts_of(Tk), Tk, g->st, cells, 1);
             }
@@ -2374,6 +2298,40 @@ int misor_ns_setup(misor_grid* g, const misor_ns_desc* ns) {
         HIPCHK(hipSetDevice((g)->device));                                         \
     } while (0)
 
+// add the NS kernel groups' timed launches so far to the stats
+static int collect_ns_times(misor_grid* g) {
+    for (int k = 0; k < 3; ++k) {
+        for (size_t q = 0; q < g->nev_used[k]; ++q) {
+            float ms = 0.f;
+            HIPCHK(hipEventSynchronize(g->nev[k][2 * q + 1]));
+            HIPCHK(hipEventElapsedTime(&ms, g->nev[k][2 * q], g->nev[k][2 * q + 1]));
+            g->stats.ns_ms[k] += ms;
+        }
+        g->nev_used[k] = 0;
+    }
+    return MISOR_OK;
+}
+
+// a start/stop event pair around launches of NS kernel group k (0 computeFG,
+// 1 adaptUV, 2 normalizePressure) when timing is on; `call` counts a call
+// (normalizePressure records three pairs per call)
+static bool ns_pair(misor_grid* g, int k, bool call, hipEvent_t* e0, hipEvent_t* e1) {
+    if (!g->timing) return false;
+    if (g->nev_used[k] >= 512 && collect_ns_times(g) != MISOR_OK) return false;
+    std::vector<hipEvent_t>& v = g->nev[k];
+    size_t& u = g->nev_used[k];
+    while (v.size() < 2 * (u + 1)) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return false;
+        v.push_back(e);
+    }
+    *e0 = v[2 * u];
+    *e1 = v[2 * u + 1];
+    ++u;
+    if (call) g->stats.ns_calls[k]++;
+    return true;
+}
+
 int misor_max_uv(misor_grid* g, double* umax, double* vmax) {
     NEED_NS(g);
     // the partials adaptUV computed, when no u, v write came after it
@@ -2443,6 +2401,9 @@ int misor_compute_fg(misor_grid* g) {
     if (!rc) rc = exchange(g, g->fld[kV], 1);
     if (rc) return rc;
     ++g->fgr_ver;
+    hipEvent_t t0 = nullptr, t1 = nullptr;
+    const bool timed = ns_pair(g, 0, true, &t0, &t1);
+    if (timed) HIPCHK(hipEventRecord(t0, g->stream));
     if (g->ns_fuse) {  // computeRHS of the same f, g in the same pass (ns_kernels.hip)
         launch_compute_fg_rhs(g->nl, g->fld[kU], g->fld[kV], g->fld[kF], g->fld[kG],
                               g->fld[kRhs]);
@@ -2452,6 +2413,7 @@ int misor_compute_fg(misor_grid* g) {
     } else {
         launch_compute_fg(g->nl, g->fld[kU], g->fld[kV], g->fld[kF], g->fld[kG]);
     }
+    if (timed) HIPCHK(hipEventRecord(t1, g->stream));
     HIPCHK(hipGetLastError());
     return MISOR_OK;
 }
@@ -2490,8 +2452,12 @@ int misor_normalize_pressure(misor_grid* g) {
     NEED_NS(g);
     double* p = pbuf(g, g->cur);
     const int nb = reduce_blocks(g->loc.ni, g->loc.nj);
+    hipEvent_t t0 = nullptr, t1 = nullptr;
+    bool timed = ns_pair(g, 2, true, &t0, &t1);
+    if (timed) HIPCHK(hipEventRecord(t0, g->stream));
     launch_absmax2(g->nl, p, p, g->red_partials);
     launch_finish_reduce(g->stream, g->red_partials, nb, kReduceMax, 2, g->red_out);
+    if (timed) HIPCHK(hipEventRecord(t1, g->stream));
     HIPCHK(hipGetLastError());
     if (g->dist) {
         int rc = allreduce(g, g->red_out, 1, 1);
@@ -2506,7 +2472,10 @@ int misor_normalize_pressure(misor_grid* g) {
     const double mx = g->red_host[0];
     int E = 0;
     (void)frexp(mx, &E);
+    timed = ns_pair(g, 2, false, &t0, &t1);
+    if (timed) HIPCHK(hipEventRecord(t0, g->stream));
     launch_exact_sum(g->nl, p, E, g->red_partials, g->red_out);
+    if (timed) HIPCHK(hipEventRecord(t1, g->stream));
     HIPCHK(hipGetLastError());
     if (g->dist) {
         int rc = allreduce(g, g->red_out, 3, 0);  // integer limbs < 2^53: exact
@@ -2520,7 +2489,10 @@ int misor_normalize_pressure(misor_grid* g) {
     }
     const double cells = (double)(g->desc.imax + 2) * (double)(g->desc.jmax + 2);
     const double avg = exact_sum_value(g->red_host, E) / cells;  // solver.c:213
+    timed = ns_pair(g, 2, false, &t0, &t1);
+    if (timed) HIPCHK(hipEventRecord(t0, g->stream));
     launch_sub_mean(g->nl, p, avg);
+    if (timed) HIPCHK(hipEventRecord(t1, g->stream));
     HIPCHK(hipGetLastError());
     return MISOR_OK;
 }
@@ -2531,8 +2503,12 @@ int misor_adapt_uv(misor_grid* g) {
         int rc = p_halo(g);  // P(i+1,j), P(i,j+1) of the rank's last column / row
         if (rc) return rc;
     }
+    hipEvent_t t0 = nullptr, t1 = nullptr;
+    const bool timed = ns_pair(g, 1, true, &t0, &t1);
+    if (timed) HIPCHK(hipEventRecord(t0, g->stream));
     launch_adapt_absmax(g->nl, g->fld[kF], g->fld[kG], pbuf(g, g->cur), g->fld[kU], g->fld[kV],
                         g->max_partials);
+    if (timed) HIPCHK(hipEventRecord(t1, g->stream));
     g->max_ver = ++g->uv_ver;
     HIPCHK(hipGetLastError());
     return MISOR_OK;
@@ -2546,6 +2522,12 @@ int misor_enable_timing(misor_grid* g, int on) {
 
 int misor_get_stats(const misor_grid* g, misor_stats* out) {
     if (!g || !out) return fail(MISOR_EINVAL, "null argument");
+    {
+        misor_grid* gm = const_cast<misor_grid*>(g);  // (pending NS kernel timings)
+        HIPCHK(hipSetDevice(gm->device));
+        int rc = collect_ns_times(gm);
+        if (rc) return rc;
+    }
     *out = g->stats;
     return MISOR_OK;
 }
@@ -2562,12 +2544,13 @@ int misor_set_tuning(misor_grid* g, int key, int value) {
     case MISOR_TUNE_SMALL_SOLVE: g->small_solve = value != 0; return MISOR_OK;
     case MISOR_TUNE_OVERLAP: g->overlap = value != 0; return MISOR_OK;
     case MISOR_TUNE_TSTEPS: {
-        // a request equal to the default rule's T is no request (the short
-        // plan and the chained-block re-pick stay on); a rejected one changes
-        // nothing
+        // an explicit request binds: every pass runs T = value iterations (no
+        // short plan, no re-pick by MISOR_TUNE_TB_CHAIN); value <= 0 returns
+        // to the default rule.  A rejected request changes nothing.
         const bool prev = g->tsteps_set;
-        g->tsteps_set = value != default_tsteps(g, g->tp.variant);
-        const int rc = configure_tb(g, value, g->tp.variant, g->tb_rows_req);
+        g->tsteps_set = value > 0;
+        const int rc = configure_tb(g, value > 0 ? value : default_tsteps(g, g->tp.variant),
+                                    g->tp.variant, g->tb_rows_req);
         if (rc) g->tsteps_set = prev;
         return rc;
     }
@@ -2638,6 +2621,7 @@ int misor_chain_trace(misor_grid* g, unsigned long long* out, long long cap, lon
 
 int misor_reset_stats(misor_grid* g) {
     if (!g) return fail(MISOR_EINVAL, "null grid");
+    for (auto& u : g->nev_used) u = 0;  // (pending NS kernel timings dropped)
     g->stats = misor_stats{};
     return MISOR_OK;
 }

@@ -816,19 +816,16 @@ __global__ __launch_bounds__(NT, 1) void k3_resident1(G3 g, double* __restrict__
     }
 }
 
-// the resident solve's form (MISOR3_RESIDENT_MODE, bits documented at
-// rgrid_sync and the kernels) and its kernel and threads per box (bit 7:
-// 1024, bit 8: 512, else 256; bit 12: no register form).  Default 240: one
-// barrier per iteration, atomics, the two-level barrier, 1024 threads per box
-// -- 128^3: 12.7 us per iteration against 16.5 at 256 threads, same box
-// (profiles/r04_res3d_modes.txt)
-static int resident_mode() {
-    static const int mode = [] {
-        const char* e = getenv("MISOR3_RESIDENT_MODE");
-        return e ? atoi(e) : 240;
-    }();
-    return mode;
-}
+// the resident solve's form (mode bits documented at rgrid_sync and the
+// kernels) and its kernel and threads per box (bit 7: 1024, bit 8: 512, else
+// 256; bit 12: no register form).  240: one barrier per iteration, atomics,
+// the two-level barrier, 1024 threads per box -- 128^3: 12.7 us per iteration
+// against 16.5 at 256 threads, same box (profiles/r04_res3d_modes.txt).
+// Other forms: an experiment build, make ab XFLAGS=-DMISOR3_RESIDENT_MODE=<bits>
+#ifndef MISOR3_RESIDENT_MODE
+#define MISOR3_RESIDENT_MODE 240
+#endif
+static int resident_mode() { return MISOR3_RESIDENT_MODE; }
 
 // full: every box lies wholly inside the domain -- then the register form
 // (REG; mode bit 12 turns it off): 128^3 at 12.2-12.6 us per iteration against

@@ -264,13 +264,14 @@ __device__ __forceinline__ double g_val(const FgArgs& a, const Uv3& S, const Uv3
 // algorithmic 16 B/cell, profiles/r03_pmc_ns16384_base.json.)
 constexpr int kFgW = 256, kFgRows = 64;
 
-static bool ns_nt() {
-    static const bool on = [] {
-        const char* e = getenv("MISOR_NS_NT");
-        return !(e && atoi(e) == 0);
-    }();
-    return on;
-}
+// nontemporal stores of f, g, rhs, u, v (fg_rhs 1.93 vs 1.97 ms at 16384^2,
+// the NS step 22.26 vs 22.36 ms, profiles/r05_ns_nt_ab.txt); the plain-store
+// instantiation is kept for A/B builds (make ab XFLAGS=-DMISOR_NS_PLAIN_STORES)
+#ifdef MISOR_NS_PLAIN_STORES
+static constexpr bool kNsNt = false;
+#else
+static constexpr bool kNsNt = true;
+#endif
 
 template <bool NT>
 __global__ __launch_bounds__(kFgW) void fg_rhs_kernel(CLay u, CLay v, Lay f, Lay g, Lay rhs,
@@ -344,7 +345,7 @@ void launch_compute_fg_rhs(const NsLaunch& L, const double* u, const double* v, 
     const NsParams& P = L.prm;
     FgArgs a{P.dt, 1.0 / P.re, 1.0 / P.dx, 1.0 / P.dy, P.gamma, P.gx, P.gy,
              1.0 / P.dx, 1.0 / P.dy, 1.0 / P.dt};
-    hipLaunchKernelGGL(ns_nt() ? fg_rhs_kernel<true> : fg_rhs_kernel<false>, dim3(grid), dim3(kFgW), 0, L.s, CLay{u, L.pitch},
+    hipLaunchKernelGGL(fg_rhs_kernel<kNsNt>, dim3(grid), dim3(kFgW), 0, L.s, CLay{u, L.pitch},
                        CLay{v, L.pitch}, Lay{f, L.pitch}, Lay{g, L.pitch}, Lay{rhs, L.pitch},
                        L.ni, L.nj, a, L.wall_left, L.wall_right, L.wall_bottom, L.wall_top, nbx,
                        nblocks);
@@ -421,12 +422,7 @@ constexpr int kRedBlocks = 1024;
 constexpr int kRedThreads = 256;
 
 int reduce_blocks(int ni, int nj) {
-    // MISOR_RED_BLOCKS: tuning experiments (read once)
-    static const int cap = [] {
-        const char* e = getenv("MISOR_RED_BLOCKS");
-        const int v = e ? atoi(e) : 0;
-        return v > 0 && v <= 8192 ? v : kRedBlocks;
-    }();
+    const int cap = kRedBlocks;
     long long cells = (long long)(ni + 2) * (nj + 2);
     long long b = (cells + kRedThreads - 1) / kRedThreads;
     return (int)(b < cap ? (b < 1 ? 1 : b) : cap);
@@ -619,15 +615,8 @@ __global__ __launch_bounds__(kRedThreads) void adapt_absmax_kernel(CLay f, CLay 
 void launch_adapt_absmax(const NsLaunch& L, const double* f, const double* g, const double* p,
                          double* u, double* v, double* partials) {
     // rows per tile: 8 (16384^2: 2.06 ms against 2.12 for 4 and 2.14 for 2,
-    // profiles/r03_ns_adapt_rows.txt; MISOR_ADAPT_ROWS: tuning experiments)
-    static const int rows = [] {
-        const char* e = getenv("MISOR_ADAPT_ROWS");
-        return e && atoi(e) == 4 ? 4 : e && atoi(e) == 2 ? 2 : 8;
-    }();
-    auto k = ns_nt() ? adapt_absmax_kernel<8, true>
-             : rows == 8 ? adapt_absmax_kernel<8, false>
-             : rows == 2 ? adapt_absmax_kernel<2, false>
-                         : adapt_absmax_kernel<4, false>;
+    // profiles/r03_ns_adapt_rows.txt)
+    auto k = adapt_absmax_kernel<8, kNsNt>;
     hipLaunchKernelGGL(k, dim3(reduce_blocks(L.ni, L.nj)), dim3(kRedThreads), 0,
                        L.s, CLay{f, L.pitch}, CLay{g, L.pitch}, CLay{p, L.pitch},
                        Lay{u, L.pitch}, Lay{v, L.pitch}, L.ni, L.nj, L.prm.dt / L.prm.dx,

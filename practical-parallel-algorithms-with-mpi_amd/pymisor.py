@@ -62,7 +62,7 @@ class Stats(C.Structure):
                 ("iters_per_pass", C.c_int), ("tb_variant", C.c_int),
                 ("halo_ms", C.c_double), ("halos", C.c_longlong),
                 ("allreduce_ms", C.c_double), ("allreduces", C.c_longlong),
-                ("chained", C.c_int)]
+                ("chained", C.c_int), ("ns_ms", C.c_double * 3), ("ns_calls", C.c_longlong * 3)]
 
 
 class Desc3(C.Structure):
@@ -96,6 +96,7 @@ SIGNATURES = {
     "misor_gather": (C.c_int, [C.c_void_p, C.c_int, _dp]),
     "misor_exchange": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     "misor_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "misor_comm_ranks": (C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
     "misor_poisson_init": (C.c_int, [C.c_void_p, C.c_double, C.c_double, C.c_int]),
     "misor_solve_rb": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), _dp]),
     "misor_solve_rb_n": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_int), _dp]),
@@ -281,6 +282,13 @@ class Grid:
     def synchronize(self):
         _check(lib().misor_synchronize(self.h))
 
+    def comm_ranks(self):
+        """ranks of the grid's communicator as the transport counts them
+        (ncclCommCount for RCCL)"""
+        n = C.c_int(0)
+        _check(lib().misor_comm_ranks(self.h, C.byref(n)))
+        return n.value
+
     def set_stream(self, stream_ptr):
         _check(lib().misor_set_stream(self.h, C.c_void_p(stream_ptr)))
 
@@ -333,7 +341,7 @@ class Grid:
                 "iters_per_pass": s.iters_per_pass, "tb_variant": s.tb_variant,
                 "halo_ms": s.halo_ms, "halos": s.halos,
                 "allreduce_ms": s.allreduce_ms, "allreduces": s.allreduces,
-                "chained": s.chained}
+                "chained": s.chained, "ns_ms": list(s.ns_ms), "ns_calls": list(s.ns_calls)}
 
     def reset_stats(self):
         _check(lib().misor_reset_stats(self.h))

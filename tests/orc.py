@@ -221,6 +221,9 @@ def ref():
         R.refa4_solve_rb_arrays.argtypes = [C.c_int, C.c_int, C.c_double, C.c_double,
                                             C.c_double, C.c_double, C.c_int, _dp, _dp, _dp]
         R.refa4_solve_rb_arrays.restype = C.c_int
+        R.refns_timed.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, _dp, _dp,
+                                  C.POINTER(C.c_longlong)]
+        R.refns_timed.restype = C.c_int
         _ref = R
     return _ref
 
@@ -243,6 +246,16 @@ def ref_solve_rb_arrays(p, rhs, dx, dy, omega, eps, itermax):
     it = ref().refa4_solve_rb_arrays(imax, jmax, dx, dy, omega, eps, itermax, _ptr(p),
                                      _ptr(rhs), C.byref(sec))
     return it, sec.value
+
+
+def ref_ns_timed(par, imax, jmax, itermax, steps):
+    """`steps` time steps of the reference's NS loop (composed with solveRB) on
+    the .par's problem at imax x jmax, solve capped at itermax; returns
+    (steps, seconds in solveRB, seconds of the steps, iterations)"""
+    a, b, n = C.c_double(0.0), C.c_double(0.0), C.c_longlong(0)
+    k = ref().refns_timed(par.encode(), imax, jmax, itermax, steps, C.byref(a), C.byref(b),
+                          C.byref(n))
+    return k, a.value, b.value, n.value
 
 
 def ref_ns(par, te=-1.0, max_steps=-1, solver=1, cap=1 << 20):

@@ -103,16 +103,15 @@ def test_chain_converges_mid_pass(T):
     assert abs(r - res_ref) <= 1e-12 * res_ref
 
 
-def test_chain_rings_env(monkeypatch):
-    """block heights of 1, 2 and 9 ring lengths (MISOR_TB_CHAIN_RINGS)"""
+def test_chain_block_heights():
+    """chained blocks of 1, 2 and 9 ring lengths (an explicit MISOR_TUNE_TB_ROWS)"""
     ni, nj = 1500, 1111
     rng = np.random.default_rng(9)
     p = rng.standard_normal((nj + 2, ni + 2))
     rhs = rng.standard_normal((nj + 2, ni + 2))
     want = p.copy()
     orc.solve_rb(want, rhs, 1.0 / ni, 1.0 / nj, 1.7, 1e-300, 17)
-    for rings in ("1", "2", "9"):
-        monkeypatch.setenv("MISOR_TB_CHAIN_RINGS", rings)
-        it, _, got, h = run(p, rhs, 1.0 / ni, 1.0 / nj, 17, 8)
-        assert h == int(rings) * 18
+    for rings in (1, 2, 9):
+        it, _, got, h = run(p, rhs, 1.0 / ni, 1.0 / nj, 17, 8, rows=rings * 18)
+        assert h == rings * 18
         assert np.array_equal(got, want), rings

@@ -171,20 +171,20 @@ def test_zero_iterations():
         assert g.solve_rb() == (0, 1.0)
 
 
-@pytest.mark.parametrize("finish2", ["1", "0"])
+@pytest.mark.parametrize("finish2", [1, 0])
 @pytest.mark.parametrize("k", [2, 3])
-def test_large_grid_few_sweeps(k, finish2, monkeypatch):
+def test_large_grid_few_sweeps(k, finish2):
     """8192^2 (67M cells, 0.54 GB per field): bit-exact after 2 and 3 sweeps
     (default path: temporally blocked; a capped solve's passes run only the
     iterations left, so these are single passes of T' = 2 and 3), with the
-    single-rank loop test in two levels (MISOR_FINISH2=1, default) and in
-    one kernel (0): same p, same iteration count"""
-    monkeypatch.setenv("MISOR_FINISH2", finish2)
+    single-rank loop test in two levels (MISOR_TUNE_FINISH2 = 1, default) and
+    in one kernel (0): same p, same iteration count"""
     n = 8192
     p, rhs = orc.poisson_init(n, n)
     want = p.copy()
     it_ref, res_ref = orc.solve_rb(want, rhs, 1.0 / n, 1.0 / n, OMEGA, 1e-300, k)
     with make_grid(n, n, eps=1e-300, itermax=k) as g:
+        g.set_tuning(M.TUNE_FINISH2, finish2)
         g.poisson_init(1.0, 1.0, 2)
         it, res = g.solve_rb()
         got = g.download(M.P)
@@ -227,12 +227,12 @@ def test_tb_converges_mid_pass(T, variant):
 @pytest.mark.parametrize("variant", [-1, 2], ids=["v0", "v2"])
 @pytest.mark.parametrize("T", [2, 5, 8])
 @pytest.mark.parametrize("ni,nj", [(1024, 1024), (1000, 1537), (2050, 300)])
-def test_pow2_spacing_vs_oracle(ni, nj, T, variant, monkeypatch):
+def test_pow2_spacing_vs_oracle(ni, nj, T, variant):
     """dx == dy == 2^-10: the TB kernel computes r with one fma in place of
     two multiplies, an add and a subtract (sor_tb.h resid<true>); bit for bit
-    the reference's expression, on random fields of a wide dynamic range, and
-    identical to the general form (MISOR_NO_POW2=1); the default kernel and
-    the 2-strip workgroup variant"""
+    the reference's expression, on random fields of a wide dynamic range; the
+    default kernel and the 2-strip workgroup variant (the general form runs on
+    every other spacing of the suite)"""
     rng = np.random.default_rng(ni + 7 * nj + T)
     p = rng.standard_normal((nj + 2, ni + 2)) * np.exp(rng.uniform(-20, 20, (nj + 2, ni + 2)))
     rhs = rng.standard_normal((nj + 2, ni + 2)) * 1e6
@@ -240,17 +240,13 @@ def test_pow2_spacing_vs_oracle(ni, nj, T, variant, monkeypatch):
     k = 2 * T + 1
     want = p.copy()
     orc.solve_rb(want, rhs, h, h, 1.7, 1e-300, k)
-    got = {}
-    for no in ("0", "1"):
-        monkeypatch.setenv("MISOR_NO_POW2", no)
-        with M.Grid(ni, nj, h, h, 1.7, 1e-300, k) as g:
-            set_mode(g, "t%d" % T)
-            if variant >= 0:
-                g.set_tuning(M.TUNE_TB_VARIANT, variant)
-            g.upload(M.P, p)
-            g.upload(M.RHS, rhs)
-            it, _ = g.solve_rb()
-            got[no] = g.download(M.P)
-        assert it == k
-    assert np.array_equal(got["0"], want), np.argwhere(got["0"] != want)[:5]
-    assert np.array_equal(got["1"], want)
+    with M.Grid(ni, nj, h, h, 1.7, 1e-300, k) as g:
+        set_mode(g, "t%d" % T)
+        if variant >= 0:
+            g.set_tuning(M.TUNE_TB_VARIANT, variant)
+        g.upload(M.P, p)
+        g.upload(M.RHS, rhs)
+        it, _ = g.solve_rb()
+        got = g.download(M.P)
+    assert it == k
+    assert np.array_equal(got, want), np.argwhere(got != want)[:5]

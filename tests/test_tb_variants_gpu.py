@@ -136,9 +136,9 @@ def test_variant_converges_mid_pass(T, variant, mid_pass_case):
 @pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("T", [2, 5, 8, 10])
 @pytest.mark.parametrize("ni,nj", [(1024, 1024), (2050, 300)])
-def test_variant_pow2_spacing(ni, nj, T, variant, monkeypatch):
+def test_variant_pow2_spacing(ni, nj, T, variant):
     """dx == dy == 2^-10: the power-of-two form of r (sor_tb.h resid<true>)
-    on fields of a wide dynamic range, and the general form"""
+    on fields of a wide dynamic range"""
     rng = np.random.default_rng(ni + 7 * nj + T)
     p = rng.standard_normal((nj + 2, ni + 2)) * np.exp(rng.uniform(-20, 20, (nj + 2, ni + 2)))
     rhs = rng.standard_normal((nj + 2, ni + 2)) * 1e6
@@ -146,11 +146,9 @@ def test_variant_pow2_spacing(ni, nj, T, variant, monkeypatch):
     k = 2 * T + 1
     want = p.copy()
     orc.solve_rb(want, rhs, h, h, 1.7, 1e-300, k)
-    for no in ("0", "1"):
-        monkeypatch.setenv("MISOR_NO_POW2", no)
-        it, _, got, _ = solve(p, rhs, h, h, k, T, variant, rows=4 * ring(T, variant))
-        assert it == k
-        assert np.array_equal(got, want), (no, np.argwhere(got != want)[:5])
+    it, _, got, _ = solve(p, rhs, h, h, k, T, variant, rows=4 * ring(T, variant))
+    assert it == k
+    assert np.array_equal(got, want), np.argwhere(got != want)[:5]
 
 
 @pytest.mark.parametrize("variant,T", [(HRS, 8), (HRS, 10)])

@@ -1,11 +1,14 @@
 #!/usr/bin/env python3
-"""HBM bytes per launch of the NS config-5 streaming kernels from separate
-rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (tools/gpu/r5_v.sh), with the
-gfx950 correction of MI355X_MICROARCH.md (FETCH_SIZE KB x 1024 x 2 + WRITE_SIZE
-KB x 1024), against each kernel's algorithmic bytes (40 B per cell: fg_rhs
-reads u, v and writes f, g, rhs; adapt_absmax reads f, g, p and writes u, v).
+"""HBM bytes per launch of the NS config-5 kernels (bench.py --workload ns)
+from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (tools/gpu/run.sh
+ns), with the gfx950 correction of MI355X_MICROARCH.md (FETCH_SIZE KB x 1024 x
+2 + WRITE_SIZE KB x 1024), against each kernel's algorithmic bytes per cell:
+fg_rhs 40 (u, v in; f, g, rhs out), adapt_absmax 40 (f, g, p in; u, v out),
+the solve's pass 24 (p, rhs in; p out), and normalizePressure's three
+kernels -- absmax2 8 (p in), exact_sum 8 (p in), sub_mean 16 (p in and out) --
+also summed as "normalize_pressure" (32).
 
-    python tools/ns_pmc_summary.py gpurun_out/r5v profiles/r05_pmc_ns16384_nt.json --size 16384
+    python tools/ns_pmc_summary.py gpurun_out/TAG/ns_pmc profiles/r06_pmc_ns16384.json --size 16384
 """
 import argparse
 import collections
@@ -13,6 +16,12 @@ import csv
 import glob
 import json
 import os
+
+# kernel name fragment -> algorithmic bytes per cell
+KERNELS = {"fg_rhs_kernel": 40, "adapt_absmax_kernel": 40, "rb_tb_kernel": 24,
+           "rb_tbc_kernel": 24, "rb_tbhc_kernel": 24, "absmax2_kernel": 8,
+           "exact_sum_kernel": 8, "sub_mean_kernel": 16}
+NORMALIZE = ("absmax2_kernel", "exact_sum_kernel", "sub_mean_kernel")
 
 
 def per_kernel(d, prefix, counter):
@@ -22,8 +31,8 @@ def per_kernel(d, prefix, counter):
             if r["Counter_Name"] != counter:
                 continue
             name = r["Kernel_Name"]
-            for k in ("fg_rhs_kernel", "adapt_absmax_kernel"):
-                if k in name:
+            for k in KERNELS:
+                if "::%s<" % k in name or "::%s(" % k in name or name.startswith(k):
                     acc[k].append(float(r["Counter_Value"]))
     return acc
 
@@ -33,21 +42,35 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("out")
     ap.add_argument("--size", type=int, default=16384)
+    ap.add_argument("--nranks", type=int, default=1)
     a = ap.parse_args()
     fetch = per_kernel(a.dir, "fetch", "FETCH_SIZE")
     write = per_kernel(a.dir, "write", "WRITE_SIZE")
     cells = a.size * a.size
-    res = {"size": a.size, "algorithmic_bytes_per_launch": 40 * cells, "kernels": {}}
+    res = {"size": a.size, "nranks": a.nranks, "kernels": {}}
     for k in sorted(fetch):
+        if k not in write:
+            continue
         f = sum(fetch[k]) / len(fetch[k])
         w = sum(write[k]) / len(write[k])
         b = f * 1024 * 2 + w * 1024
+        alg = KERNELS[k] * cells
         res["kernels"][k] = {"launches": len(fetch[k]), "fetch_size_kb_raw": f,
                              "write_size_kb": w, "read_bytes_corrected": f * 2048,
                              "write_bytes": w * 1024, "bytes_per_launch": b,
-                             "ratio_to_algorithmic": b / (40 * cells)}
+                             "algorithmic_bytes_per_launch": alg,
+                             "ratio_to_algorithmic": b / alg}
+    if all(k in res["kernels"] for k in NORMALIZE):
+        b = sum(res["kernels"][k]["bytes_per_launch"] for k in NORMALIZE)
+        res["kernels"]["normalize_pressure"] = {
+            "bytes_per_launch": b, "algorithmic_bytes_per_launch": 32 * cells,
+            "ratio_to_algorithmic": b / (32 * cells), "parts": list(NORMALIZE)}
+    solve = [k for k in ("rb_tbhc_kernel", "rb_tbc_kernel", "rb_tb_kernel") if k in res["kernels"]]
+    if solve:
+        res["solve_kernel"] = solve[0]
     res["note"] = ("separate rocprofv3 --pmc passes of bench.py --workload ns; FETCH_SIZE x1024 x2 "
-                   "(gfx950: 128-B requests tallied at 64 B) + WRITE_SIZE x1024")
+                   "(gfx950: 128-B requests tallied at 64 B) + WRITE_SIZE x1024; the solve kernel's "
+                   "bytes are per pass (its launches run 7 or 8 iterations each)")
     json.dump(res, open(a.out, "w"), indent=1)
     print(json.dumps(res["kernels"], indent=1))
 

@@ -56,8 +56,14 @@ def main():
                          "self-exchanges through the one-rank communicator; timing only)")
     args = ap.parse_args()
     if args.sides is not None:
+        # the proxy exists only in the experiment build (csrc/misor_api.hip
+        # MISOR_PROXY): make -C practical-parallel-algorithms-with-mpi_amd ab
+        # B=build_proxy L=lib_proxy XFLAGS=-DMISOR_PROXY
         args.comm = True
         os.environ["MISOR_PROXY_SIDES"] = args.sides or "-"
+        if not args.lib:
+            args.lib = os.path.join(ROOT, "practical-parallel-algorithms-with-mpi_amd", "lib_proxy",
+                                    "libmisor.so")
     if args.lib:
         M.LIBPATH = os.path.abspath(args.lib)
     n = args.size

@@ -1,59 +1,15 @@
-// misor_api.hip -- the C ABI of include/misor.h: device state, transfers,
-// the solve loop (batched launches with a device-resident convergence flag),
-// the NS step entry points and the 2D decomposition over RCCL.
+// misor_api.hip -- the C ABI of include/misor.h, part 1: errors, the 2D
+// decomposition, grid lifecycle (create / destroy, streams), transfers
+// (upload / download / gather / exchange / fill / Poisson init), tuning and
+// statistics.  The solve loop is in misor_solve.hip, the NS step in
+// misor_ns.hip, communication in misor_comm.hip, launch plans in
+// misor_plan.hip; their shared state is struct misor_grid (misor_grid.h).
 
-#include <algorithm>
-#include <chrono>
-#include <cmath>
-#include <cstdarg>
-#include <cstdio>
-#include <cstdlib>
-#include <condition_variable>
-#include <cstring>
-#include <map>
-#include <memory>
-#include <mutex>
-#include <thread>
-#include <vector>
-
-#include "misor_internal.h"
-
-using namespace misor;
+#include "misor_grid.h"
 
 namespace {
 
 thread_local std::string g_err;
-
-int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
-int fail(int code, const char* fmt, ...) {
-    char buf[512];
-    va_list ap;
-    va_start(ap, fmt);
-    vsnprintf(buf, sizeof buf, fmt, ap);
-    va_end(ap);
-    g_err = buf;
-    return code;
-}
-
-#define HIPCHK(x)                                                                         \
-    do {                                                                                  \
-        hipError_t e_ = (x);                                                              \
-        if (e_ != hipSuccess)                                                             \
-            return fail(MISOR_EHIP, "%s: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, \
-                        __LINE__);                                                        \
-    } while (0)
-
-#define NCCLCHK(x)                                                                        \
-    do {                                                                                  \
-        ncclResult_t r_ = (x);                                                            \
-        if (r_ != ncclSuccess)                                                            \
-            return fail(MISOR_ECOMM, "%s: %s (%s:%d)", #x, ncclGetErrorString(r_),        \
-                        __FILE__, __LINE__);                                              \
-    } while (0)
-
-// kP2: third pressure buffer of decomposed runs (the pipelined pass loop of
-// misor_solve_rb_n writes pass k's result while pass k-1's source is kept)
-enum { kP0 = 0, kP1 = 1, kRhs = 2, kU = 3, kV = 4, kF = 5, kG = 6, kP2 = 7, kNumFields = 8 };
 
 // MPI_Dims_create(n, 2): the most balanced factorisation, larger factor first
 void dims_create(int n, int dims[2]) {
@@ -67,182 +23,23 @@ void dims_create(int n, int dims[2]) {
 // sizeOfRank (assignment-5/skeleton/src/solver.c:30-32)
 int size_of_rank(int rank, int size, int n) { return n / size + ((n % size > rank) ? 1 : 0); }
 
-// In-process transport: every rank of the group is a misor_grid owned by its
-// own host thread of ONE process (any devices, including all on one GPU).
-// Collectives are a host barrier plus device-to-device copies; the sum is
-// combined in rank order.  It exists so the decomposed kernels can be run and
-// checked on a single-GPU machine; across GPUs the RCCL path is used.
-struct LocalGroup {
-    int n = 0;
-    std::vector<misor_grid*> members;
-    std::vector<double> vals;  // n * kMaxT scratch for all-reduce
-    std::mutex m;
-    std::condition_variable cv;
-    int arrived = 0;
-    long long generation = 0;
-    int joined = 0, left = 0;
-
-    void barrier() {
-        std::unique_lock<std::mutex> lk(m);
-        const long long gen = generation;
-        if (++arrived == n) {
-            arrived = 0;
-            ++generation;
-            cv.notify_all();
-        } else {
-            cv.wait(lk, [&] { return generation != gen; });
-        }
-    }
-};
 std::mutex g_groups_mu;
 std::map<std::string, std::shared_ptr<LocalGroup>> g_groups;
 constexpr char kLocalPrefix[] = "LOCAL:";
 
 }  // namespace
 
-void misor::set_last_error(const char* msg) { g_err = msg; }
-
-struct misor_grid {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    bool own_stream = false;
-    misor_desc desc{};
-    misor_local loc{};
-    long long pitch = 0, rows = 0, elems = 0;
-    double* fld[kNumFields] = {};
-    int np = 2;   // pressure buffers: 2 (ping-pong), 3 on decomposed runs
-    int cur = 0;  // which one (0 .. np-1, see pbuf) holds the current pressure
-    int rhs_halo = 0;  // depth of rhs's exchanged halo still valid (0: rhs changed)
-    // the current pressure buffer's halo (cells of the neighbours) predates the
-    // last solve: a solve leaves it as the reference's solve loop does (its
-    // exchange opens each iteration, assignment-5/skeleton/src/solver.c:607);
-    // the next reader of it -- adaptUV, a download of p -- exchanges first
-    // (p_halo), the next solve exchanges at its start anyway
-    bool p_stale = false;
-    // u, v versions: every entry point that writes u or v bumps uv_ver;
-    // adaptUV leaves max |u|, |v| partials in max_partials (max_ver = uv_ver)
-    unsigned uv_ver = 1, max_ver = 0;
-    double* max_partials = nullptr;
-    // f, g, rhs versions: every write of f, g or rhs from outside bumps fgr_ver;
-    // the fused computeFG (ns_fuse) leaves rhs computed from its f, g with dt
-    // fused_dt (fused_ver = fgr_ver), so computeRHS only completes the cells
-    // next to a neighbour rank
-    bool ns_fuse = true;
-    unsigned fgr_ver = 1, fused_ver = 0;
-    double fused_dt = 0.0;
-
-    // sweep
-    SweepParams sp{};
-    int nbx = 0, nby = 0, nparts = 0, partials_cap = 0;
-    double* partials = nullptr;  // two slots of partials_cap doubles (by pass parity)
-    bool finish2 = true;  // single rank: two-level loop test (MISOR_TUNE_FINISH2 = 0: one kernel)
-    DevState* st = nullptr;
-    DevState* st_host = nullptr;  // pinned
-    int last_iters = 0;
-    // solveRB's loop test near its threshold (MISOR_TUNE_NEAR_BAND): relative
-    // band of eps^2 whose iterations are re-summed exactly (exact_tail); 0: off
-    double near_rel = 1e-10;
-    int near_exp = 10;
-    double* rsq = nullptr;  // exact_tail: r^2 per cell (allocated on first use)
-    bool small_solve = true;  // whole-solve LDS kernel when p fits (single rank)
-
-    // temporally blocked sweep (sor_tb.hip): T iterations per pass over HBM
-    int tsteps = kDefaultTsteps;  // requested T (1: single-iteration kernel)
-    bool tsteps_set = false;      // T requested by MISOR_TUNE_TSTEPS (else the default rule)
-    bool short_plan = false;      // capped solves may run as kShortT-iteration split-ring passes
-    bool short_all = false;       // ... every solve of more than kDefaultTsteps iterations
-    SweepParams tp{};             // its launch geometry (for T = tsteps)
-    int tb_nparts = 0;
-    int tb_rows_req = 0;          // MISOR_TUNE_TB_ROWS (0: automatic)
-    bool tb_persistent = true;    // MISOR_TUNE_TB_PERSISTENT: work-queue launches
-    int tb_reserve = kTbReserve;  // MISOR_TUNE_TB_RESERVE: slots a pipelined interior launch
-                                  // leaves to the communication / edge-block streams
-    int* tb_queue = nullptr;      // 8 per-XCD block counters of a persistent launch + its exit count
-    // chained passes (sor_tb.h rb_tbc_kernel; MISOR_TUNE_TB_CHAIN): the initial
-    // segment list of every pass length and part (0: whole pass, 1: interior
-    // blocks, 2: edge blocks of a pipelined decomposed pass), and two work
-    // areas (parts 0 / 1, part 2: they run concurrently on two streams)
-    int tb_chain = -1;  // 1 on, 0 off, -1 automatic: on for local blocks below kChainCells
-    // (each plan: the list of the main kernel and of the edge kernel --
-    // columns at a physical left / right side, launched beside it on xstream)
-    struct ChainList {
-        unsigned long long* tmpl = nullptr;
-        int nseg0 = 0, blocks = 0;
-        int run[9] = {};  // XCD runs of the list
-    };
-    struct ChainPlan {
-        ChainList main, edge;
-        int reserve = -1;  // part 1 of a pipelined pass: the slots it leaves to part 2
-        bool built = false;
-    } chain_plan[2][kMaxT + 1][3];  // [the default variant's / the split ring's][T][part]
-    int* tb_work[4] = {nullptr, nullptr, nullptr, nullptr};  // main / edge x parts 0-1 / 2
-    long long tb_work_bytes[4] = {0, 0, 0, 0};
-    hipStream_t xstream[2] = {nullptr, nullptr};  // edge kernels (parts 0-1 / 2)
-    hipEvent_t ev_fork[2] = {}, ev_join[2] = {};
-    // MISOR_CHAIN_TRACE=1: per-block timeline of the last chained pass (diagnostics)
-    unsigned long long* chain_trace = nullptr;
-    long long chain_trace_blocks = 0, chain_trace_last = 0;
-
-    // reductions
-    double* red_partials = nullptr;
-    double* red_out = nullptr;   // 4 doubles on device
-    double* red_host = nullptr;  // 4 doubles pinned
-
-    // NS
-    bool ns_ready = false;
-    NsLaunch nl{};
-
-    // multi-GPU
-    bool dist = false;
-    ncclComm_t comm = nullptr;
-    int nbr[kDirs] = {-1, -1, -1, -1, -1, -1, -1, -1};  // L R B T BL BR TL TR
-    HaloPlan plan[2 * kMaxT + 1] = {};                   // by halo depth 1 .. 2*kMaxT
-    int max_depth = 2;                                   // deepest plan built
-    std::shared_ptr<LocalGroup> local;                   // in-process transport
-    bool overlap = true;            // exchange on cstream while the interior sweeps
-    hipStream_t cstream = nullptr;  // communication stream
-    hipEvent_t ev_s = nullptr, ev_x = nullptr, ev_d = nullptr;
-    hipEvent_t ev_i[2] = {}, ev_dk[2] = {};  // interior blocks / decide of pass k, by k & 1
-    hipEvent_t ev_e2[2] = {};                // edge blocks of pass k on cstream, by k & 1
-#ifdef MISOR_PROXY
-    bool proxy = false;  // MISOR_PROXY_SIDES: a measurement proxy, fields meaningless
-#endif
-    double* sendbuf = nullptr;
-    double* recvbuf = nullptr;
-    double* gbuf = nullptr;  // misor_gather: this rank's owned block, packed
-    long long gbuf_cap = 0;
-    // in-process transport, event-driven: device work of different ranks is
-    // ordered by HIP events only (no host-device synchronisation); the host
-    // threads meet at barriers just to publish which event records to wait on
-    hipEvent_t lx_pk = nullptr, lx_cp = nullptr;  // exchange: my send buffer packed / copies done
-    hipEvent_t la_val[2] = {}, la_rd[2] = {}, la_cmb[2] = {};  // all-reduce, by parity
-    double* la_stage = nullptr;   // 2 x kMaxT: my value, by all-reduce parity
-    double* la_gather = nullptr;  // 2 x nranks x kMaxT: every rank's value, by parity
-    long long la_gen = 0;
-    bool comm_dead = false;       // the RCCL communicator was aborted (error / timeout)
-    // communication timing inside a timed solve: start/stop event pairs of the
-    // halo exchanges (0) and residual all-reduces (1) of the current batch
-    bool comm_timing = false;
-    std::vector<hipEvent_t> cev[2];
-    size_t cev_used[2] = {0, 0};
-
-    // stats
-    bool timing = false;
-    std::vector<hipEvent_t> ev;
-    misor_stats stats{};
-    // NS kernel timing (misor_stats.ns_ms): start/stop event pairs by kernel
-    // group, resolved by misor_get_stats (or when a pool is full)
-    std::vector<hipEvent_t> nev[3];
-    size_t nev_used[3] = {0, 0, 0};
-};
-
-// pressure buffer x (mod np)
-static double* pbuf(misor_grid* g, long long x) {
-    const int b = (int)(x % g->np);
-    return g->fld[b == 2 ? kP2 : kP0 + b];
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
 }
 
-extern "C" {
+void misor::set_last_error(const char* msg) { g_err = msg; }
 
 const char* misor_last_error(void) { return g_err.c_str(); }
 const char* misor_version(void) { return "misor 0.1 (gfx950, fp64 red-black SOR)"; }
@@ -353,715 +150,6 @@ void misor_destroy(misor_grid* g) {
     delete g;
 }
 
-// Regions of the 8-neighbour exchange at halo depth d.  A rank sends the
-// cells it owns (interior, plus ghost cells on its physical sides) next to each
-// neighbour; ranks in one process row share nj and their physical top/bottom,
-// ranks in one process column share ni, so send and receive extents match.
-static void build_plan(misor_grid* g, int d) {
-    const int ni = g->loc.ni, nj = g->loc.nj;
-    const int* nb = g->nbr;
-    const int cl = nb[0] >= 0 ? 1 : 0, ch = nb[1] >= 0 ? ni : ni + 1;
-    const int rl = nb[2] >= 0 ? 1 : 0, rh = nb[3] >= 0 ? nj : nj + 1;
-    HaloRegion S[kDirs] = {
-        {1, rl, d, rh - rl + 1, 0},      {ni - d + 1, rl, d, rh - rl + 1, 0},
-        {cl, 1, ch - cl + 1, d, 0},      {cl, nj - d + 1, ch - cl + 1, d, 0},
-        {1, 1, d, d, 0},                 {ni - d + 1, 1, d, d, 0},
-        {1, nj - d + 1, d, d, 0},        {ni - d + 1, nj - d + 1, d, d, 0}};
-    HaloRegion R[kDirs] = {
-        {1 - d, rl, d, rh - rl + 1, 0},  {ni + 1, rl, d, rh - rl + 1, 0},
-        {cl, 1 - d, ch - cl + 1, d, 0},  {cl, nj + 1, ch - cl + 1, d, 0},
-        {1 - d, 1 - d, d, d, 0},         {ni + 1, 1 - d, d, d, 0},
-        {1 - d, nj + 1, d, d, 0},        {ni + 1, nj + 1, d, d, 0}};
-    HaloPlan& P = g->plan[d];
-    long long so = 0, ro = 0;
-    for (int k = 0; k < kDirs; ++k) {
-        if (nb[k] < 0) S[k].w = S[k].h = R[k].w = R[k].h = 0;
-        S[k].off = so;
-        R[k].off = ro;
-        so += (long long)S[k].w * S[k].h;
-        ro += (long long)R[k].w * R[k].h;
-        P.send[k] = S[k];
-        P.recv[k] = R[k];
-    }
-    P.total = so > ro ? so : ro;
-}
-
-// a start/stop event pair for timing one communication step (kind 0: halo
-// exchange, 1: all-reduce) of the current batch; false when not timing
-static bool comm_pair(misor_grid* g, int kind, hipEvent_t* e0, hipEvent_t* e1) {
-    if (!g->comm_timing) return false;
-    std::vector<hipEvent_t>& v = g->cev[kind];
-    size_t& u = g->cev_used[kind];
-    while (v.size() < 2 * (u + 1)) {
-        hipEvent_t e;
-        if (hipEventCreate(&e) != hipSuccess) return false;
-        v.push_back(e);
-    }
-    *e0 = v[2 * u];
-    *e1 = v[2 * u + 1];
-    ++u;
-    return true;
-}
-
-// add the timed communication steps of the batch just synchronised to the stats
-static int collect_comm_times(misor_grid* g) {
-    for (int kind = 0; kind < 2; ++kind) {
-        for (size_t k = 0; k < g->cev_used[kind]; ++k) {
-            float ms = 0.f;
-            HIPCHK(hipEventElapsedTime(&ms, g->cev[kind][2 * k], g->cev[kind][2 * k + 1]));
-            if (kind == 0) {
-                g->stats.halo_ms += ms;
-                g->stats.halos++;
-            } else {
-                g->stats.allreduce_ms += ms;
-                g->stats.allreduces++;
-            }
-        }
-        g->cev_used[kind] = 0;
-    }
-    return MISOR_OK;
-}
-
-static double comm_timeout_s() {
-    const char* e = getenv("MISOR_COMM_TIMEOUT");
-    const double v = e && *e ? atof(e) : 0.0;
-    return v > 0 ? v : 600.0;
-}
-
-// Wait for stream s.  With an RCCL communicator, poll instead of blocking:
-// an asynchronous communicator error (a peer died, a link failed:
-// ncclCommGetAsyncError) or no progress for MISOR_COMM_TIMEOUT seconds
-// (default 600) aborts the communicator and returns MISOR_ECOMM on this rank,
-// where the reference's MPI default (MPI_ERRORS_ARE_FATAL) would end the job;
-// a blocked hipStreamSynchronize would hang instead.
-static int wait_stream(misor_grid* g, hipStream_t s) {
-    if (!g->comm) {
-        HIPCHK(hipStreamSynchronize(s));
-        return MISOR_OK;
-    }
-    const auto t0 = std::chrono::steady_clock::now();
-    const double limit = comm_timeout_s();
-    for (long spins = 0;; ++spins) {
-        const hipError_t e = hipStreamQuery(s);
-        if (e == hipSuccess) return MISOR_OK;
-        if (e != hipErrorNotReady)
-            return fail(MISOR_EHIP, "stream wait: %s", hipGetErrorString(e));
-        ncclResult_t ar = ncclSuccess;
-        const bool bad = ncclCommGetAsyncError(g->comm, &ar) == ncclSuccess &&
-                         ar != ncclSuccess && ar != ncclInProgress;
-        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        if (bad || el > limit) {
-            (void)ncclCommAbort(g->comm);
-            g->comm = nullptr;
-            g->comm_dead = true;
-            if (bad)
-                return fail(MISOR_ECOMM, "RCCL asynchronous error: %s", ncclGetErrorString(ar));
-            return fail(MISOR_ECOMM, "communication made no progress for %.0f s "
-                                     "(MISOR_COMM_TIMEOUT)", limit);
-        }
-        if (spins > 2000) std::this_thread::sleep_for(std::chrono::microseconds(20));
-    }
-}
-
-#define COMMCHK(g)                                                                        \
-    do {                                                                                  \
-        if ((g)->comm_dead)                                                               \
-            return fail(MISOR_ECOMM, "the communicator was aborted by an earlier error"); \
-    } while (0)
-
-// one 8-neighbour exchange of `field` at depth d on stream s (default: the
-// grid stream): pack kernel, transport, unpack kernel
-static int exchange(misor_grid* g, double* field, int d, hipStream_t s = nullptr) {
-    if (!g->dist) return MISOR_OK;
-    COMMCHK(g);
-    if (!s) s = g->stream;
-    const HaloPlan& P = g->plan[d];
-    hipEvent_t t0 = nullptr, t1 = nullptr;
-    const bool timed = comm_pair(g, 0, &t0, &t1);
-    if (timed) HIPCHK(hipEventRecord(t0, s));
-    if (g->local) {
-        // In-process transport.  Rank q's copies of my send buffer and my own
-        // unpack of the previous exchange must be done before I pack again;
-        // my copies of q's buffer wait for q's pack.  Barrier 1: every rank has
-        // recorded its pack event; barrier 2: every rank has recorded its copy
-        // event (so the next exchange waits on this exchange's records).
-        static const int opposite[kDirs] = {1, 0, 3, 2, 7, 6, 5, 4};
-        LocalGroup& G = *g->local;
-        HIPCHK(hipStreamWaitEvent(s, g->lx_cp, 0));
-        for (int k = 0; k < kDirs; ++k)
-            if (g->nbr[k] >= 0) HIPCHK(hipStreamWaitEvent(s, G.members[g->nbr[k]]->lx_cp, 0));
-        launch_pack(s, field, g->pitch, P, g->sendbuf);
-        HIPCHK(hipEventRecord(g->lx_pk, s));
-        G.barrier();
-        for (int k = 0; k < kDirs; ++k) {
-            if (g->nbr[k] < 0) continue;
-            const misor_grid* q = G.members[g->nbr[k]];
-            const HaloRegion& sr = q->plan[d].send[opposite[k]];
-            const HaloRegion& rr = P.recv[k];
-            HIPCHK(hipStreamWaitEvent(s, q->lx_pk, 0));
-            HIPCHK(hipMemcpyAsync(g->recvbuf + rr.off, q->sendbuf + sr.off,
-                                  sizeof(double) * (size_t)rr.w * rr.h,
-                                  hipMemcpyDeviceToDevice, s));
-        }
-        launch_unpack(s, field, g->pitch, P, g->recvbuf);
-        HIPCHK(hipEventRecord(g->lx_cp, s));
-        if (timed) HIPCHK(hipEventRecord(t1, s));
-        HIPCHK(hipGetLastError());
-        G.barrier();
-        return MISOR_OK;
-    }
-    launch_pack(s, field, g->pitch, P, g->sendbuf);
-    NCCLCHK(ncclGroupStart());
-    for (int k = 0; k < kDirs; ++k) {
-        if (g->nbr[k] < 0) continue;
-        const size_t ns = (size_t)P.send[k].w * P.send[k].h;
-        const size_t nr = (size_t)P.recv[k].w * P.recv[k].h;
-        NCCLCHK(ncclSend(g->sendbuf + P.send[k].off, ns, ncclDouble, g->nbr[k], g->comm, s));
-        NCCLCHK(ncclRecv(g->recvbuf + P.recv[k].off, nr, ncclDouble, g->nbr[k], g->comm, s));
-    }
-    NCCLCHK(ncclGroupEnd());
-    launch_unpack(s, field, g->pitch, P, g->recvbuf);
-    if (timed) HIPCHK(hipEventRecord(t1, s));
-    HIPCHK(hipGetLastError());
-    return MISOR_OK;
-}
-
-// the current pressure buffer's halo, exchanged 2 deep if a solve left it stale
-static int p_halo(misor_grid* g) {
-    if (!g->dist || !g->p_stale) return MISOR_OK;
-    int rc = exchange(g, pbuf(g, g->cur), 2);
-    if (rc == MISOR_OK) g->p_stale = false;
-    return rc;
-}
-
-// all-reduce of n <= kMaxT device doubles (sum or max) across the ranks, on
-// stream s (default: the grid stream)
-static int allreduce(misor_grid* g, double* dev, int n, int is_max, hipStream_t s = nullptr) {
-    if (!g->dist) return MISOR_OK;
-    COMMCHK(g);
-    if (!s) s = g->stream;
-    hipEvent_t t0 = nullptr, t1 = nullptr;
-    const bool timed = comm_pair(g, 1, &t0, &t1);
-    if (timed) HIPCHK(hipEventRecord(t0, s));
-    if (g->local) {
-        // In-process transport: every rank stages its values (slot by parity,
-        // reused two all-reduces later once every rank has read it), gathers
-        // every rank's staged values after barrier 1 and combines them in rank
-        // order on its device; barrier 2 publishes the read events.
-        LocalGroup& G = *g->local;
-        const int par = (int)(g->la_gen++ & 1);
-        double* stage = g->la_stage + par * kMaxT;
-        double* gather = g->la_gather + (size_t)par * G.n * kMaxT;
-        HIPCHK(hipStreamWaitEvent(s, g->la_cmb[par], 0));
-        for (int q = 0; q < G.n; ++q) HIPCHK(hipStreamWaitEvent(s, G.members[q]->la_rd[par], 0));
-        HIPCHK(hipMemcpyAsync(stage, dev, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
-        HIPCHK(hipEventRecord(g->la_val[par], s));
-        G.barrier();
-        for (int q = 0; q < G.n; ++q) {
-            const misor_grid* o = G.members[q];
-            HIPCHK(hipStreamWaitEvent(s, o->la_val[par], 0));
-            HIPCHK(hipMemcpyAsync(gather + (size_t)q * kMaxT, o->la_stage + par * kMaxT,
-                                  sizeof(double) * n, hipMemcpyDeviceToDevice, s));
-        }
-        HIPCHK(hipEventRecord(g->la_rd[par], s));
-        launch_local_combine(s, gather, G.n, n, is_max, dev);
-        HIPCHK(hipEventRecord(g->la_cmb[par], s));
-        if (timed) HIPCHK(hipEventRecord(t1, s));
-        HIPCHK(hipGetLastError());
-        G.barrier();
-        return MISOR_OK;
-    }
-    NCCLCHK(ncclAllReduce(dev, dev, n, ncclDouble, is_max ? ncclMax : ncclSum, g->comm, s));
-    if (timed) HIPCHK(hipEventRecord(t1, s));
-    return MISOR_OK;
-}
-
-static int pick_rows_per_block(int ni, int nj, int waves) {
-    // enough workgroups to fill 256 CUs several times, but long enough row
-    // marches that the two redundant halo rows per block stay cheap
-    const int strips = (ni + kStripCells - 1) / kStripCells;
-    const int nbx = (strips + waves - 1) / waves;
-    const int target_blocks = 2048;
-    int want_nby = (target_blocks + nbx - 1) / nbx;
-    int h = (nj + want_nby - 1) / want_nby;
-    if (h < 4) h = 4;
-    if (h > 16) h = 16;  // measured optimum at 32768^2 (profiles/r01_tune_rows.txt)
-    return h;
-}
-
-static int ensure_partials(misor_grid* g, int n) {
-    if (n <= g->partials_cap) return MISOR_OK;
-    if (g->partials) (void)hipFree(g->partials);
-    g->partials = nullptr;
-    g->partials_cap = 0;
-    // two slots of n (by pass parity) + the two-level finish's chunk sums
-    if (hipMalloc(&g->partials, sizeof(double) * (2 * (size_t)n + kMaxT * kFinishChunks)) !=
-        hipSuccess)
-        return fail(MISOR_ENOMEM, "partials allocation failed");
-    g->partials_cap = n;
-    return MISOR_OK;
-}
-
-// (re)derive the sweep launch geometry; partials are sized for the largest
-static int configure_sweep(misor_grid* g, int variant, int rows, int remap) {
-    if (variant < 0 || variant >= kNumSweepVariants) return fail(MISOR_EINVAL, "bad variant");
-    SweepParams& sp = g->sp;
-    const int waves = sweep_waves(variant);
-    sp.variant = variant;
-    sp.rows_per_block = rows > 0 ? rows : pick_rows_per_block(g->loc.ni, g->loc.nj, waves);
-    if (sp.rows_per_block < 1) sp.rows_per_block = 1;
-    sp.xcd_remap = remap;
-    int nby = 0;
-    g->nparts = sweep_partials(g->loc.ni, g->loc.nj, sp.rows_per_block, waves, &g->nbx, &nby);
-    g->nby = nby;
-    sp.nbx = g->nbx;
-    sp.nblocks = g->nparts;
-    g->tp.xcd_remap = remap;
-    return ensure_partials(g, g->nparts);
-}
-
-// T that a multi-block solve uses: the requested one, limited so that the
-// 2T-deep halo of a decomposed run fits inside the smallest neighbour block
-static int effective_tsteps(const misor_grid* g) {
-    int T = g->tsteps;
-    if (T < 1) T = 1;
-    if (T > kMaxT) T = kMaxT;
-    if (g->dist) {
-        const int mi = g->desc.imax / g->loc.dims[0], mj = g->desc.jmax / g->loc.dims[1];
-        while (T > 1 && (2 * T > mi || 2 * T > mj || 2 * T > g->max_depth)) --T;
-    }
-    return T;
-}
-
-// Block height H of a pass of T iterations.  A block streams H + 4T rows for
-// its H, so tall blocks waste less; short ones give a launch more workgroups.
-// With one workgroup per block, round-1 measurements put the optimum near 192
-// rows (profiles/r01_shape_sweep*.txt); with the persistent work-queue passes
-// (the 64 workgroups of an XCD stream neighbouring blocks of one block row,
-// and the pass ends on a band of short blocks) taller blocks pay off: 384 rows
-// 0.796 vs 0.821 ms per iteration at 32768^2, 576-768 within noise of 384,
-// 1536 slower (profiles/r02_tb_rows_persistent.txt).  H is a multiple of the
-// static ring's S slots (sor_tb.hip: interior blocks march in chunks of S
-// steps); smaller grids halve it until the launch has ~1024 workgroups.  The last block row takes the rest
-// (at most H rows) and marches in pairs.
-static int pick_tb_rows(int ni, int nj, int T, int variant) {
-    const long long nbx = tb_nbx(ni, T, variant);
-    const int S = tb_ring_slots(T, variant);
-    auto on_ring = [&](int h) { return S * std::max(1, (h + S / 2) / S); };
-    // the tallest of the ladder that still gives the launch ~6 blocks per
-    // resident workgroup (3000 blocks)
-    int h = kTbRowLadder[0];
-    for (int k = 0; k < kTbRowLadderLen; ++k) {
-        h = kTbRowLadder[k];
-        if (nbx * ((nj + on_ring(h) - 1) / on_ring(h)) >= 3000) break;
-    }
-    return on_ring(h);
-}
-
-// geometry of the temporally blocked pass with T iterations into `tp`: block
-// columns and block rows.  Automatic geometry (no MISOR_TUNE_TB_ROWS request):
-// blocks of pick_tb_rows' height H, then about two resident rounds of short
-// ones (~32 rows) -- the work order takes them last, so the pass ends on
-// blocks a sixth as long (the makespan of a persistent pass runs ~half a
-// block past its average), at the cost of their extra halo rows -- and a last
-// block row of one to two short-block heights (the rest; round 1 left up to H
-// rows there, a long row-tested block at the very end of the order).
-// (tools/scale_proxy.py, profiles/r02_small_rows.txt: the short band took one
-// rank's 8192 x 16384 at 8 GPUs from 0.149 to 0.118 ms per iteration.)  A
-// three-level form -- the bulk in 576-row blocks, one round of H, then the
-// short band -- ran up to 1.7x slower on the small grids (the tall blocks
-// hold their slots for a whole pass; profiles/r02_tb_levels.txt) and was
-// dropped.  An explicit request gives uniform blocks of that height, the last
-// row taking the rest.
-static bool chain_on(const misor_grid* g, int variant) {
-    if (!g->tb_persistent) return false;
-    // the split-ring passes are always chained runs (the warm-up rows they
-    // save are VALU work of a VALU-bound pass, sor_tbh.h rb_tbhc_kernel; an
-    // unchained form measured 2-15% slower, profiles/r05_hrsweep*.txt)
-    if (variant == kHrTbVariant) return true;
-    const bool want = g->tb_chain > 0 ||
-                      (g->tb_chain < 0 && (long long)g->loc.ni * g->loc.nj < kChainCells);
-    return want && variant == kDefaultTbVariant;
-}
-
-// T when none was requested: 8 on large local blocks; on small ones 8 with
-// chained passes (the default there), 7 without (misor_internal.h)
-static int default_tsteps(const misor_grid* g, int variant) {
-    const long long cells = (long long)g->loc.ni * g->loc.nj;
-    return cells >= kTsteps8Cells || chain_on(g, variant) ? kDefaultTsteps : kSmallBlockTsteps;
-}
-
-// residual partials per stage of a pass: one per block, or one per block and
-// wave for a chained pass (sor_tb.h chain_block_end)
-static int tb_parts(const SweepParams& tp) {
-    return tp.chain ? tp.nblocks * tb_waves(tp.variant) : tp.nblocks;
-}
-
-static void tb_geometry(const misor_grid* g, int T, SweepParams& tp) {
-    const int nj = g->loc.nj, req = g->tb_rows_req;
-    tp.nbx = tb_nbx(g->loc.ni, T, tp.variant);
-    const int S = tb_ring_slots(T, tp.variant);
-    tp.chain = chain_on(g, tp.variant);
-    if (tp.chain) {
-        // chained passes: short blocks (the unit of residual partials and of
-        // work stealing), long runs; every block row but the last a multiple
-        // of the ring
-        const int rings = tp.variant == kHrTbVariant
-                              ? (g->dist ? kHrChainRingsDist : kHrChainRingsPerBlock)
-                              : kChainRingsPerBlock;
-        int h = req > 0 ? S * std::max(1, (req + S / 2) / S) : rings * S;
-        if (h > nj) h = nj;
-        tp.rows_per_block = h;
-        tp.nby = (nj + h - 1) / h;
-        tp.nby_big = tp.nby - 1;
-        tp.h_small = h;
-        tp.nblocks = tp.nbx * tp.nby;
-        return;
-    }
-    int h = req > 0 ? req : pick_tb_rows(g->loc.ni, nj, T, tp.variant);
-    if (h > nj) h = nj;
-    const int small_rows = kTbSmallRows;
-    const double band_rounds = kTbSmallRounds;
-    const int hs = S * std::max(1, (small_rows + S / 2) / S);
-    int nbig = 0, ns = 0;
-    if (req > 0 || hs >= h || nj < 4 * hs) {  // uniform blocks, the last takes the rest
-        nbig = nj / h;
-        if (nbig * h == nj && nbig > 0) --nbig;
-    } else {
-        const int band = std::min(
-            (int)((band_rounds * tb_resident(T, tp.variant) + tp.nbx - 1) / tp.nbx), nj / 4 / hs);
-        nbig = std::max(0, (nj - band * hs - hs) / h);
-        ns = std::max(0, (nj - nbig * h) / hs - 1);  // the last row: [hs, 2 hs)
-    }
-    tp.rows_per_block = h;
-    tp.nby_big = nbig;
-    tp.h_small = hs;
-    tp.nby = nbig + ns + 1;
-    tp.nblocks = tp.nbx * tp.nby;
-}
-
-// The initial segment list of a chained pass (sor_tb.h rb_tbc_kernel) of Tp
-// iterations, part `part`, built on first use.  Blocks in a part: all (0),
-// those whose cone stays clear of the halo (1, sor_tb.h tb_block's test), the
-// rest (2).  Along a column, blocks of steady-able rows (chain_rows_ok) form
-// runs, each split into segments of about B / G blocks (B: blocks of the
-// part, G: workgroups resident at once), so that the initial list gives every
-// resident workgroup about one segment; every other block (cone at a
-// physical bottom / top side, a last block off the ring) is a segment of its
-// own.  The list is column-interleaved (segment s of every column, then s + 1
-// ...): the XCD queues deal contiguous runs of it, so neighbouring columns --
-// whose strips share 4T columns -- march side by side on one XCD.
-static void drop_chain_plans(misor_grid* g) {
-    for (auto& v : g->chain_plan)
-        for (auto& row : v)
-            for (auto& pl : row) {
-                (void)hipFree(pl.main.tmpl);
-                (void)hipFree(pl.edge.tmpl);
-                pl = misor_grid::ChainPlan{};
-            }
-}
-
-// (variant: the configured one or the split ring of the short plan; the plan
-// follows that variant's geometry: strip width, ring, block height)
-static int chain_plan(misor_grid* g, int variant, int Tp, int part,
-                      const misor_grid::ChainPlan** out) {
-    auto& pl = g->chain_plan[variant == kHrTbVariant ? 1 : 0][Tp][part];
-    *out = &pl;
-    if (pl.built) return MISOR_OK;
-    SweepParams tp = g->tp;
-    tp.variant = variant;
-    tb_geometry(g, Tp, tp);
-    const int W = tb_waves(tp.variant), OW = tb_out_width(Tp, tp.variant);
-    const int S = tb_ring_slots(Tp, tp.variant);
-    const int nbx = tp.nbx, nby = tp.nby;
-    auto rows = [&](int by, int& j0, int& j1) {
-        j0 = 1 + by * tp.rows_per_block;
-        j1 = by == nby - 1 ? tp.nj + 1 : j0 + tp.rows_per_block;
-    };
-    auto interior = [&](int bx, int by) {
-        int j0, j1;
-        rows(by, j0, j1);
-        const int lo = 1 + bx * W * OW - 2 * Tp;
-        const int hi = 1 + (bx * W + W - 1) * OW - 2 * Tp + kStripCells - 1;
-        return lo >= tp.int_lo_i && hi <= tp.int_hi_i && j0 - 2 * Tp >= tp.int_lo_j &&
-               j1 - 1 + 2 * Tp <= tp.int_hi_j;
-    };
-    auto steady = [&](int by) {  // sor_tb.h chain_rows_ok
-        int j0, j1;
-        rows(by, j0, j1);
-        return j0 - 2 * Tp >= tp.upd_lo_j && j1 - 1 + 2 * Tp <= tp.upd_hi_j &&
-               (j1 - j0) % S == 0 && j1 > j0;
-    };
-    auto in_part = [&](int bx, int by) { return part == 0 || interior(bx, by) == (part == 1); };
-    // a column with a strip at a physical left / right side marches the
-    // general, lane-masked way (sor_tb.h chain_run's cols_in)
-    auto edge_col = [&](int bx) {
-        for (int w = 0; w < W; ++w) {
-            const int c_out = 1 + (bx * W + w) * OW;
-            if (c_out > tp.ni) break;
-            const int c_ld = c_out - 2 * Tp;
-            if (!(c_ld >= tp.upd_lo_i && c_ld + kStripCells - 1 <= tp.upd_hi_i &&
-                  (c_out + OW - 1 <= tp.ni || (tp.ni & 1) == 0)))
-                return true;
-        }
-        return false;
-    };
-    // Cost model, in steady-block units: a block of an edge column costs
-    // kChainEdgeCost (kSteadyEdge chunks), a block of a row that is not
-    // steady-able (a segment of its own) that much plus its 4T warm-up rows.
-    // The segments are cut so that each costs about (total / resident
-    // workgroups): every workgroup starts one at once and they end together.
-    const double E = variant == kHrTbVariant ? (g->dist ? kHrChainEdgeCostDist : kHrChainEdgeCost)
-                                             : kChainEdgeCost;
-    const int H = tp.rows_per_block;
-    // The split ring's plan (round 5): main and edge lists, segments of cost /
-    // resident workgroups, and the pipelined pass's part-2 slots sized to its
-    // cost share (below): the 8-GPU rank block's pipelined loop 0.130-0.135
-    // against 0.145-0.147 ms per iteration with physical left and bottom
-    // sides, 0.130-0.131 against 0.136-0.138 with the bottom one only
-    // (profiles/r05_reserve_ab.txt).  One list for both kinds of column with
-    // exactly one item per workgroup measured 1-3% slower at 32768^2 and on
-    // the 8-GPU rank block (profiles/r05_hr_plan_ab.txt: edge-column blocks ran
-    // 1.4x longer among the main list's) and was removed.
-    const bool sized = variant == kHrTbVariant && part != 0;
-    std::vector<unsigned long long> singles;
-    double cost = 0;
-    long long Bm = 0, Be = 0;
-    for (int bx = 0; bx < nbx; ++bx) {
-        const bool ecol = edge_col(bx);
-        for (int by = 0; by < nby; ++by) {
-            if (!in_part(bx, by)) continue;
-            if (!steady(by)) {
-                singles.push_back(chain_word(bx, by, by + 1));
-                cost += E * (H + 4.0 * Tp) / H;
-                ++Bm;
-            } else {
-                cost += ecol ? E : 1.0;
-                ++(ecol ? Be : Bm);
-            }
-        }
-    }
-    const int G = std::max(8, tb_resident(Tp, tp.variant));
-    // a pipelined pass's parts (1: interior blocks, 2: the blocks whose cone
-    // reads the halo, launched once the exchange is in): part 2 runs beside
-    // part 1 on the slots part 1 leaves free, so those are sized to its share
-    // of the pass's cost (at least MISOR_TUNE_TB_RESERVE, which also serves the
-    // exchange's kernels) and each part's items to its slots -- part 2's
-    // blocks then run as chained runs of the border columns instead of one
-    // warmed-up block per slot at the end of the pass
-    int Gp = G;
-    if (sized) {
-        double c12[3] = {0, 0, 0};
-        for (int bx = 0; bx < nbx; ++bx) {
-            const bool ecol = edge_col(bx);
-            for (int by = 0; by < nby; ++by)
-                c12[interior(bx, by) ? 1 : 2] +=
-                    !steady(by) ? E * (H + 4.0 * Tp) / H : ecol ? E : 1.0;
-        }
-        const int R = std::min(G / 2, std::max(g->tb_reserve,
-                                               (int)llround(G * c12[2] / (c12[1] + c12[2]))));
-        pl.reserve = R;
-        Gp = std::max(8, part == 1 ? G - R : R);
-    }
-    double per = std::max(1.0, cost / Gp);  // cost of one segment
-    // segments of one steady run of n blocks of cost c1 each
-    auto pieces = [&](int n, double c1) {
-        return std::min(n, std::max(1, (int)llround(n * c1 / per)));
-    };
-    auto each_run = [&](auto&& fn) {  // fn(bx, by, n, edge column)
-        for (int bx = 0; bx < nbx; ++bx) {
-            const bool ecol = edge_col(bx);
-            for (int by = 0; by < nby;) {
-                if (!in_part(bx, by) || !steady(by)) {
-                    ++by;
-                    continue;
-                }
-                int e = by;
-                while (e < nby && in_part(bx, e) && steady(e)) ++e;
-                fn(bx, by, e - by, ecol);
-                by = e;
-            }
-        }
-    };
-    std::vector<unsigned long long> edge, inner;  // inner: column-interleaved
-    std::vector<std::vector<unsigned long long>> col(nbx);
-    each_run([&](int bx, int by, int n, bool ecol) {
-        const int k = pieces(n, ecol ? E : 1.0);
-        for (int q = 0; q < k; ++q) {
-            const unsigned long long w = chain_word(
-                bx, by + (int)((long long)n * q / k), by + (int)((long long)n * (q + 1) / k));
-            if (ecol) edge.push_back(w);
-            else col[bx].push_back(w);
-        }
-    });
-    for (size_t q = 0;; ++q) {
-        bool any = false;
-        for (int bx = 0; bx < nbx; ++bx)
-            if (q < col[bx].size()) {
-                inner.push_back(col[bx][q]);
-                any = true;
-            }
-        if (!any) break;
-    }
-    // XCD runs: the main list -- singles dealt round-robin first, then the
-    // inner list in 8 contiguous parts; the edge list round-robin
-    auto upload = [&](misor_grid::ChainList& L, const std::vector<unsigned long long>* xl,
-                      long long blocks) -> int {
-        std::vector<unsigned long long> list;
-        for (int x = 0; x < 8; ++x) {
-            L.run[x] = (int)list.size();
-            list.insert(list.end(), xl[x].begin(), xl[x].end());
-        }
-        L.run[8] = (int)list.size();
-        L.nseg0 = (int)list.size();
-        L.blocks = (int)blocks;
-        if (list.empty()) return MISOR_OK;
-        if (hipMalloc(&L.tmpl, list.size() * sizeof(unsigned long long)) != hipSuccess ||
-            hipMemcpy(L.tmpl, list.data(), list.size() * sizeof(unsigned long long),
-                      hipMemcpyHostToDevice) != hipSuccess)
-            return fail(MISOR_ENOMEM, "chain plan allocation failed");
-        return MISOR_OK;
-    };
-    std::vector<unsigned long long> xm[8], xe[8];
-    for (size_t k = 0; k < singles.size(); ++k) xm[k % 8].push_back(singles[k]);
-    for (int x = 0; x < 8; ++x)
-        for (size_t k = inner.size() * x / 8; k < inner.size() * (x + 1) / 8; ++k)
-            xm[x].push_back(inner[k]);
-    for (size_t k = 0; k < edge.size(); ++k) xe[k % 8].push_back(edge[k]);
-    int rc = upload(pl.main, xm, Bm);
-    if (rc) return rc;
-    rc = upload(pl.edge, xe, Be);
-    if (rc) return rc;
-    pl.built = true;
-    return MISOR_OK;
-}
-
-static int configure_tb(misor_grid* g, int T, int variant, int rows) {
-    if (T < 1 || T > kMaxT) return fail(MISOR_EINVAL, "iterations per pass must be 1..%d", kMaxT);
-    if (variant < 0 || variant >= kNumTbVariants) return fail(MISOR_EINVAL, "bad tb variant");
-    if (tb_max_t(variant) == 0)  // measured slower, then not built
-        return fail(MISOR_EINVAL, "TB variant %d is retired (measured slower; not built)",
-                    variant);
-    if (variant == kHrTbVariant && !g->tb_persistent)
-        return fail(MISOR_EINVAL, "TB variant %d runs persistent chained passes only", variant);
-    if (T > tb_max_t(variant))
-        return fail(MISOR_EINVAL, "TB variant %d runs at most %d iterations per pass", variant,
-                    tb_max_t(variant));
-    g->tsteps = T;
-    g->tb_rows_req = rows;
-    SweepParams& tp = g->tp;
-    tp.variant = variant;
-    tp.xcd_remap = g->sp.xcd_remap;
-    const int Te = effective_tsteps(g);
-    // every pass length a solve may launch (T, the last pass of a capped
-    // solve, a pass recomputed after convergence) has its own geometry; the
-    // partials hold the largest
-    long long need = 1;
-    for (int Tp = 1; Tp <= std::max(1, Te); ++Tp) {
-        SweepParams q = tp;
-        tb_geometry(g, Tp, q);
-        // the steady march addresses a block's rows with 32-bit buffer offsets
-        // and marks lanes that do not store with offset 2^30
-        // (every block row is at most rows_per_block tall)
-        if ((q.rows_per_block + 4LL * kMaxT + 8) * tp.pitch * 8 >= (1LL << 30))
-            return fail(MISOR_EINVAL, "tb rows %d: a block of rows exceeds 1 GiB",
-                        q.rows_per_block);
-        need = std::max(need, (long long)Tp * tb_parts(q));
-    }
-    tb_geometry(g, std::max(2, Te), tp);
-    g->tb_nparts = tb_parts(tp);
-    // The short plan (solve_rb_from): a single-rank solve capped at few
-    // iterations runs them in fewer, longer passes of the split-ring kernel
-    // when that saves a pass; its geometries share the partials
-    // Where (round 5, the chained split ring; profiles/r05_plan_ab*.txt, wall
-    // ms per iteration of 20- and 100-iteration solves against the T = 8 plan):
-    //  - blocks of [2^26, 2^28) cells, where the T = 8 passes are chained
-    //    (the 8-GPU rank block 8192 x 16384: 0.106 vs 0.123, in the pipelined
-    //    loop 0.122 vs 0.142): every solve of more than 8 iterations;
-    //  - a single rank of >= 2^29 cells (the 32768^2 bench grid: 0.676 vs 0.682
-    //    at 100 iterations, 20 iterations in 2 passes instead of 3): the same;
-    //  - a single rank of 2^28 cells, and decomposed blocks of >= 2^28 (the
-    //    two- and four-GPU splits of the bench grid): only where it saves
-    //    passes, the rule in solve_rb_from (at 100 iterations the two plans are
-    //    within 1-3%; the 4-GPU rank block through the pipelined loop of round
-    //    5, 20 iterations: 0.2247-0.2250 vs 0.2317-0.2327 ms per iteration,
-    //    profiles/r05_plan_ab_ranks.txt -- round 4's loop measured the opposite).
-    const long long cells = (long long)g->loc.ni * g->loc.nj;
-    const bool small_chain = cells >= kHrAllCells && cells < kTsteps8Cells &&
-                             chain_on(g, variant);
-    g->short_all = small_chain || (!g->dist && cells >= 2 * kTsteps8Cells);
-    g->short_plan = variant == kDefaultTbVariant && !g->tsteps_set &&
-                    g->tb_persistent &&
-                    (g->short_all ||
-                     (!chain_on(g, variant) &&
-                      cells >= (g->dist ? kShortDistCells : kTsteps8Cells)));
-    if (g->short_plan) {
-        for (int Tp = 1; Tp <= kShortT; ++Tp) {
-            SweepParams q = tp;
-            q.variant = kShortTbVariant;
-            tb_geometry(g, Tp, q);
-            if ((q.rows_per_block + 4LL * kMaxT + 8) * tp.pitch * 8 >= (1LL << 30)) {
-                g->short_plan = false;
-                break;
-            }
-            need = std::max(need, (long long)Tp * tb_parts(q));
-        }
-    }
-    drop_chain_plans(g);  // geometry changed: rebuilt on first use
-    const bool short_chain = g->short_plan && chain_on(g, kShortTbVariant);
-    if (chain_on(g, variant) || short_chain) {
-        for (int k = 0; k < 2; ++k) {  // the edge kernels' streams
-            if (g->xstream[k]) continue;
-            int lo = 0, hi = 0;
-            (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-            if (hipStreamCreateWithPriority(&g->xstream[k], hipStreamNonBlocking, hi) !=
-                    hipSuccess ||
-                hipEventCreateWithFlags(&g->ev_fork[k], hipEventDisableTiming) != hipSuccess ||
-                hipEventCreateWithFlags(&g->ev_join[k], hipEventDisableTiming) != hipSuccess)
-                return fail(MISOR_EHIP, "edge stream creation failed");
-        }
-        // work areas (parts 0 / 1, part 2): head, an initial list of at most
-        // one segment per block, the dynamic slots; sized once for every pass
-        // length (a launch may still be using them when a plan is built)
-        long long most = 1;
-        for (int Tp = 1; Tp <= std::max(2, Te); ++Tp) {
-            SweepParams q = tp;
-            tb_geometry(g, Tp, q);
-            most = std::max(most, (long long)q.nblocks);
-        }
-        for (int Tp = 1; short_chain && Tp <= kShortT; ++Tp) {
-            SweepParams q = tp;
-            q.variant = kShortTbVariant;
-            tb_geometry(g, Tp, q);
-            most = std::max(most, (long long)q.nblocks);
-        }
-        const long long bytes = kChainHead * (long long)sizeof(int) +
-                                (most + kChainSegCap) * (long long)sizeof(unsigned long long);
-        const char* et = getenv("MISOR_CHAIN_TRACE");
-        if (et && et[0] == '1' && most > g->chain_trace_blocks) {
-            (void)hipDeviceSynchronize();
-            (void)hipFree(g->chain_trace);
-            g->chain_trace = nullptr;
-            g->chain_trace_blocks = 0;
-            if (hipMalloc(&g->chain_trace, 3 * most * sizeof(unsigned long long)) != hipSuccess)
-                return fail(MISOR_ENOMEM, "chain trace allocation failed");
-            g->chain_trace_blocks = most;
-        }
-        for (int k = 0; k < 4; ++k) {
-            if (bytes <= g->tb_work_bytes[k]) continue;
-            if (g->tb_work[k]) {
-                (void)hipDeviceSynchronize();
-                (void)hipFree(g->tb_work[k]);
-            }
-            g->tb_work[k] = nullptr;
-            g->tb_work_bytes[k] = 0;
-            if (hipMalloc(&g->tb_work[k], bytes) != hipSuccess)
-                return fail(MISOR_ENOMEM, "chain work area allocation failed");
-            g->tb_work_bytes[k] = bytes;
-        }
-    }
-    return ensure_partials(g, (int)need);
-}
 
 int misor_create(misor_grid** out, const misor_desc* d) {
     if (!out || !d) return fail(MISOR_EINVAL, "null argument");
@@ -1604,915 +692,6 @@ int misor_poisson_init(misor_grid* g, double xlength, double ylength, int proble
     return MISOR_OK;
 }
 
-// ---------------------------------------------------------------------------
-// solve loop
-// ---------------------------------------------------------------------------
-
-static int ensure_events(misor_grid* g, size_t n) {
-    while (g->ev.size() < n) {
-        hipEvent_t e;
-        HIPCHK(hipEventCreate(&e));
-        g->ev.push_back(e);
-    }
-    return MISOR_OK;
-}
-
-static int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* iters,
-                         double* res, bool* hand_off);
-static int exact_tail(misor_grid* g, int itermax, int it0, double res0, int* iters, double* res,
-                      bool* hand_off);
-
-// The batched passes and the exact tail (below) hand the solve to each other
-// (*hand_off) with the iterations done and the last residual; this loop runs
-// them in turn, so the hand-overs of a long solve need no stack.
-int misor_solve_rb_n(misor_grid* g, int itermax, int* iters, double* res) {
-    if (!g) return fail(MISOR_EINVAL, "null grid");
-    HIPCHK(hipSetDevice(g->device));
-    int it = 0;
-    double r = 1.0;  // solver.c:196
-    for (bool tail = false;; tail = !tail) {
-        bool hand_off = false;
-        const int rc = tail ? exact_tail(g, itermax, it, r, &it, &r, &hand_off)
-                            : solve_rb_from(g, itermax, it, r, &it, &r, &hand_off);
-        if (rc) return rc;
-        if (!hand_off) break;
-    }
-    if (iters) *iters = it;
-    if (res) *res = r;
-    return MISOR_OK;
-}
-
-// ---------------------------------------------------------------------------
-// The loop test near its threshold (partition independence).
-// The residual of a pass is a sum of per-workgroup (and, decomposed, per-rank)
-// partials, so its last bits depend on the partition -- as the reference's own
-// MPI_Allreduce of per-rank sums (assignment-5/skeleton/src/solver.c:651) does.
-// An iteration count can only depend on that when res lies within a few ulps
-// of eps^2.  The loop-test kernels therefore stop the solve BEFORE any
-// iteration whose res lies within near_rel * eps^2 of eps^2 (DevState::near;
-// far outside the rounding spread, so every partition stops at the same
-// iteration), the pass is recomputed up to there from its untouched source,
-// and exact_tail takes over: one sweep per iteration that stores r^2 of every
-// cell, whose sum is formed exactly (fixed-point 128-bit limbs per cell --
-// each truncation a function of the cell alone -- added in any order and
-// all-reduced exactly, ns_kernels.hip exact_sum), so res and the loop test are
-// bit for bit the same on every partition.  Once 2T consecutive iterations
-// are outside the band again the batched passes resume.  Only solves that come
-// near the threshold pay for it.
-// ---------------------------------------------------------------------------
-static int exact_residual(misor_grid* g, double cells, double* out) {
-    NsLaunch L{};  // the reduction region: interior + physical ghost cells (zero in rsq)
-    L.s = g->stream;
-    L.pitch = g->pitch;
-    L.ni = g->loc.ni;
-    L.nj = g->loc.nj;
-    L.wall_left = g->loc.neighbours[0] < 0;
-    L.wall_right = g->loc.neighbours[1] < 0;
-    L.wall_bottom = g->loc.neighbours[2] < 0;
-    L.wall_top = g->loc.neighbours[3] < 0;
-    const int nb = reduce_blocks(L.ni, L.nj);
-    launch_absmax2(L, g->rsq, g->rsq, g->red_partials);
-    launch_finish_reduce(g->stream, g->red_partials, nb, kReduceMax, 2, g->red_out);
-    HIPCHK(hipGetLastError());
-    if (g->dist) {
-        int rc = allreduce(g, g->red_out, 1, 1);
-        if (rc) return rc;
-    }
-    HIPCHK(hipMemcpyAsync(g->red_host, g->red_out, sizeof(double), hipMemcpyDeviceToHost,
-                          g->stream));
-    {
-        int rc_ = wait_stream(g, g->stream);
-        if (rc_) return rc_;
-    }
-    int E = 0;
-    (void)frexp(g->red_host[0], &E);
-    launch_exact_sum(L, g->rsq, E, g->red_partials, g->red_out);
-    HIPCHK(hipGetLastError());
-    if (g->dist) {
-        int rc = allreduce(g, g->red_out, 3, 0);  // integer limbs < 2^53: exact
-        if (rc) return rc;
-    }
-    HIPCHK(hipMemcpyAsync(g->red_host, g->red_out, 3 * sizeof(double), hipMemcpyDeviceToHost,
-                          g->stream));
-    {
-        int rc_ = wait_stream(g, g->stream);
-        if (rc_) return rc_;
-    }
-    *out = exact_sum_value(g->red_host, E) / cells;  // solver.c:229
-    return MISOR_OK;
-}
-
-// iterations it0 + 1 .. of solveRB from the current field, one sweep each with
-// the exact residual and the loop test on the host (solver.c:197)
-static int exact_tail(misor_grid* g, int itermax, int it0, double res0, int* iters, double* res,
-                      bool* hand_off) {
-    const double epssq = g->desc.eps * g->desc.eps;
-    const double cells = (double)g->desc.imax * (double)g->desc.jmax;
-    if (!g->rsq) {
-        if (hipMalloc(&g->rsq, (size_t)g->elems * sizeof(double)) != hipSuccess) {
-            g->rsq = nullptr;
-            return fail(MISOR_ENOMEM, "exact residual buffer allocation failed");
-        }
-        HIPCHK(hipMemsetAsync(g->rsq, 0, (size_t)g->elems * sizeof(double), g->stream));
-    }
-    // the sweep kernel runs while the device state says not done
-    DevState s{};
-    s.it = it0;
-    s.res = res0;
-    s.epssq = epssq;
-    s.itermax = itermax;
-    s.nband = -1.0;
-    *g->st_host = s;
-    HIPCHK(hipMemcpyAsync(g->st, g->st_host, sizeof(DevState), hipMemcpyHostToDevice, g->stream));
-    SweepParams sp = g->sp;  // the default sweep variant's geometry
-    if (sp.variant != kDefaultSweepVariant) {
-        sp.variant = kDefaultSweepVariant;
-        sp.rows_per_block = pick_rows_per_block(g->loc.ni, g->loc.nj, sweep_waves(sp.variant));
-        int nby = 0, nbx = 0;
-        sp.nblocks = sweep_partials(g->loc.ni, g->loc.nj, sp.rows_per_block,
-                                    sweep_waves(sp.variant), &nbx, &nby);
-        sp.nbx = nbx;
-        if (sp.nblocks > g->partials_cap) {
-            int rc = ensure_partials(g, sp.nblocks);
-            if (rc) return rc;
-        }
-    }
-    sp.part = 0;
-    int it = it0, far = 0;
-    double r = res0;
-    const int T = effective_tsteps(g);
-    while ((r >= epssq) && (it < itermax)) {
-        double* src = pbuf(g, g->cur);
-        double* dst = pbuf(g, g->cur + 1);
-        if (g->dist) {
-            int rc = exchange(g, src, 2);  // the sweep reads the 2-deep halo
-            if (rc) return rc;
-        }
-        launch_sweep_rsq(g->stream, sp, src, dst, g->fld[kRhs], g->partials, g->st, g->rsq);
-        HIPCHK(hipGetLastError());
-        g->cur = (g->cur + 1) % g->np;
-        int rc = exact_residual(g, cells, &r);
-        if (rc) return rc;
-        ++it;
-        g->stats.launches += 1;
-        // back to the batched passes after 2T iterations outside the band
-        far = fabs(r - epssq) > g->near_rel * epssq ? far + 1 : 0;
-        if (far >= 2 * T && (r >= epssq) && (it < itermax)) {
-            *hand_off = true;  // back to solve_rb_from (misor_solve_rb_n)
-            break;
-        }
-    }
-    g->p_stale = g->dist;  // (p_halo)
-    {
-        int rc_ = wait_stream(g, g->stream);
-        if (rc_) return rc_;
-    }
-    g->stats.sweeps += it - it0;
-    g->last_iters = it;
-    *iters = it;
-    *res = r;
-    return MISOR_OK;
-}
-
-static int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* iters,
-                         double* res, bool* hand_off) {
-    const double epssq = g->desc.eps * g->desc.eps;
-    DevState s0{};
-    s0.it = it0;
-    s0.res = res0;
-    s0.epssq = epssq;
-    s0.itermax = itermax;
-    // (eps^2 = 0 -- e.g. eps = 1e-300 -- has no threshold to come near: res >= 0
-    // always continues the loop)
-    s0.nband = g->near_rel > 0.0 && epssq > 0.0 ? g->near_rel * epssq : -1.0;
-    s0.done = !((res0 >= epssq) && (it0 < itermax));  // loop test of solver.c:197
-    if (s0.done) {
-        *iters = it0;
-        *res = res0;
-        return MISOR_OK;
-    }
-    *g->st_host = s0;
-    HIPCHK(hipMemcpyAsync(g->st, g->st_host, sizeof(DevState), hipMemcpyHostToDevice,
-                          g->stream));
-    const double cells = (double)g->desc.imax * (double)g->desc.jmax;
-    if (!g->dist && g->small_solve && small_solve_fits(g->loc.ni, g->loc.nj)) {
-        double* p = pbuf(g, g->cur);
-        if (g->timing) {
-            int rc = ensure_events(g, 2);
-            if (rc) return rc;
-            HIPCHK(hipEventRecord(g->ev[0], g->stream));
-        }
-        launch_solve_small(g->stream, p, g->fld[kRhs], g->loc.ni, g->loc.nj, g->pitch,
-                           g->sp.idx2, g->sp.idy2, g->sp.coef, cells, g->st);
-        HIPCHK(hipGetLastError());
-        if (g->timing) HIPCHK(hipEventRecord(g->ev[1], g->stream));
-        HIPCHK(hipMemcpyAsync(g->st_host, g->st, sizeof(DevState), hipMemcpyDeviceToHost,
-                              g->stream));
-        {
-            int rc_ = wait_stream(g, g->stream);
-            if (rc_) return rc_;
-        }
-        const int it = g->st_host->it;
-        if (g->timing) {
-            float ms = 0.f;
-            HIPCHK(hipEventElapsedTime(&ms, g->ev[0], g->ev[1]));
-            g->stats.sweep_ms += ms;
-            g->stats.timed_sweeps += it - it0;
-        }
-        g->stats.launches += 1;
-        if (g->st_host->near) {
-            // the kernel left p untouched: run it again up to the iteration
-            // before the near one, then the exact tail
-            const double rn = g->st_host->res;
-            DevState s1 = s0;
-            s1.itermax = it;
-            s1.nband = -1.0;
-            *g->st_host = s1;
-            HIPCHK(hipMemcpyAsync(g->st, g->st_host, sizeof(DevState), hipMemcpyHostToDevice,
-                                  g->stream));
-            launch_solve_small(g->stream, p, g->fld[kRhs], g->loc.ni, g->loc.nj, g->pitch,
-                               g->sp.idx2, g->sp.idy2, g->sp.coef, cells, g->st);
-            HIPCHK(hipGetLastError());
-            g->stats.sweeps += it - it0;
-            *hand_off = true;  // the exact tail from iteration it (misor_solve_rb_n)
-            *iters = it;
-            *res = rn;
-            return MISOR_OK;
-        }
-        g->stats.sweeps += it - it0;
-        g->last_iters = it;
-        *iters = it;
-        *res = g->st_host->res;
-        return MISOR_OK;
-    }
-    // multi-block path: passes of T iterations (T = 1: single-iteration sweep
-    // kernel; T >= 2: temporally blocked kernel, sor_tb.hip)
-    //
-    // The short plan: a pass costs about the same for any T <= 8 (it streams
-    // its fields; profiles/r04_tcurve.txt), so a solve capped at few iterations
-    // is cheapest in as few passes as possible.  The split-ring kernel runs
-    // kShortT = 10 iterations a pass at ~1.4 x the time of a T = 8 pass
-    // (profiles/r04_ab_splitring.txt): where its passes times 1.4 undercut the
-    // default's pass count -- 9-10 and 17-20 iterations (the driver's
-    // 20-iteration solve: 2 passes instead of 7 + 7 + 6) -- the solve takes it.
-    // With the chained split ring (round 5) a T = 10 pass costs about a T = 8
-    // one on the blocks where configure_tb sets short_all, so there every solve
-    // of more than 8 iterations takes it.
-    const int todo0 = itermax - it0;
-    const bool shortp = g->short_plan && effective_tsteps(g) == kDefaultTsteps &&
-                        (g->short_all ? todo0 > kDefaultTsteps
-                                      : 7LL * ((todo0 + kShortT - 1) / kShortT) <
-                                            5LL * ((todo0 + kDefaultTsteps - 1) / kDefaultTsteps));
-    const int T = shortp ? kShortT : effective_tsteps(g);
-    SweepParams tpl = g->tp;  // the plan's geometry
-    if (shortp) {
-        tpl.variant = kShortTbVariant;
-        tb_geometry(g, T, tpl);
-    }
-    // time the communication steps of the loop (collected after each batch)
-    g->comm_timing = g->timing && g->dist;
-    g->cev_used[0] = g->cev_used[1] = 0;
-    const int depth = 2 * T;  // halo of src each pass needs
-    const int nparts = T == 1 ? g->nparts : tb_parts(tpl);
-    double* const rhs = g->fld[kRhs];
-    auto pass = [&](hipStream_t s, int part, const double* src, double* dst, int Tp, int force,
-                    double* partials) -> int {
-        if (T == 1) {
-            SweepParams sp = g->sp;
-            sp.part = part;
-            launch_sweep(s, sp, src, dst, rhs, partials, g->st);
-        } else {
-            SweepParams tp = tpl;
-            tp.part = part;
-            // the interior blocks of an overlapped pass leave workgroup slots to the
-            // halo exchange, the residual all-reduce + loop test and the edge blocks
-            // on the other streams: a persistent launch holds every slot it gets
-            // until the pass is over, so without them the exchange would only start
-            // at the end of the interior blocks
-            tp.reserve = part == 1 ? g->tb_reserve : 0;
-            if (Tp != T) tb_geometry(g, Tp, tp);  // narrower cone: wider strips
-            if (tp.chain) {  // chained runs, work stealing (parts 0 / 1 and 2 concurrently)
-                const misor_grid::ChainPlan* pl = nullptr;
-                int rc = chain_plan(g, tp.variant, Tp, part, &pl);
-                if (rc) return rc;
-                const int k = part == 2 ? 1 : 0;
-                tp.seg_cap = kChainSegCap;
-                tp.trace = part == 2 ? nullptr : g->chain_trace;
-                if (tp.trace) g->chain_trace_last = tp.nblocks;
-                auto use = [&](SweepParams& q, const misor_grid::ChainList& L) {
-                    q.seg_tmpl = L.tmpl;
-                    q.nseg0 = L.nseg0;
-                    q.chain_blocks = L.blocks;
-                    for (int x = 0; x < 9; ++x) q.seg_run[x] = L.run[x];
-                };
-                const int eg = pl->edge.nseg0;  // edge workgroups: one per initial segment
-                // Where the two kernels run: the main kernel forked to xstream,
-                // the edge kernel on s.  The other way round (the edge kernel on
-                // xstream, launched first or after the main one) its 16-odd
-                // workgroups did not start until the main kernel's workgroups
-                // retired, in every pass of a multi-pass solve but the first,
-                // though its slots were free (profiles/r03_chain_xmode.txt: 8.5-8.9
-                // ms per 32768^2 pass against 6.0).
-                SweepParams te = tp;
-                use(te, pl->edge);
-                te.chain_edge = 1;
-                te.reserve = std::max(0, tb_resident(Tp, tp.variant) - eg);
-                SweepParams tm = tp;
-                use(tm, pl->main);
-                tm.chain_edge = 0;
-                if (part == 1 && pl->reserve >= 0) tm.reserve = pl->reserve;
-                tm.reserve += pl->edge.blocks > 0 ? eg : 0;
-                const bool has_e = pl->edge.blocks > 0, has_m = pl->main.blocks > 0;
-                // (no edge list: the main kernel alone, on s)
-                const bool fork = has_e && has_m;
-                hipStream_t ms = fork ? g->xstream[k] : s;
-                if (fork) {
-                    HIPCHK(hipEventRecord(g->ev_fork[k], s));
-                    HIPCHK(hipStreamWaitEvent(g->xstream[k], g->ev_fork[k], 0));
-                }
-                if (has_e)
-                    launch_tb(s, Tp, te, src, dst, rhs, partials, g->st, force, g->tb_work[2 + k]);
-                if (has_m)
-                    launch_tb(ms, Tp, tm, src, dst, rhs, partials, g->st, force, g->tb_work[k]);
-                if (fork) {
-                    HIPCHK(hipEventRecord(g->ev_join[k], g->xstream[k]));
-                    HIPCHK(hipStreamWaitEvent(s, g->ev_join[k], 0));
-                }
-                return MISOR_OK;
-            }
-            // persistent work-queue launch on the grid stream (whole passes and
-            // interior blocks); the boundary blocks of a split pass are few
-            int* q = (g->tb_persistent && part != 2 && s == g->stream) ? g->tb_queue : nullptr;
-            launch_tb(s, Tp, tp, src, dst, rhs, partials, g->st, force, q);
-        }
-        return MISOR_OK;
-    };
-    const int cur0 = g->cur;
-    long long launched = 0;  // passes enqueued
-    const int rhs_depth = T == 1 ? 1 : depth;
-    if (g->dist && g->rhs_halo < rhs_depth) {  // the halo-ring updates read rhs outside the block
-        int rc = exchange(g, rhs, rhs_depth);
-        if (rc) return rc;
-        g->rhs_halo = rhs_depth;
-    }
-    // Pipelined decomposed passes (T >= 2, overlap on; three pressure buffers):
-    // pass k reads src_k = pbuf(k), writes pbuf(k+1), which is the source of
-    // pass k-2 -- so pass k waits for the loop test of pass k-2 only (a pass that
-    // overshoots convergence is recomputed from its source), and the all-reduce
-    // + loop test of pass k-1 run while pass k sweeps.  Within a pass the
-    // interior blocks (part 1, main stream) and the edge blocks (part 2, on
-    // cstream: those whose cone reads src's halo; they alone write dst's send
-    // region) run concurrently; the exchange of dst's halo for pass k+1 follows
-    // the edge blocks on cstream, and so overlaps the interior blocks.
-    const bool pipelined = g->dist && g->overlap && T > 1;
-    // (the exchange of the first source follows the first pass's interior
-    // launch on the host: RCCL's host side of a grouped send / receive takes
-    // ~0.1 ms, which the interior blocks need not wait for --
-    // profiles/r05_decomposed_loop_trace.csv)
-    bool first_x = pipelined;
-    if (pipelined) {
-        HIPCHK(hipEventRecord(g->ev_s, g->stream));  // state upload, rhs halo, prior work
-        HIPCHK(hipStreamWaitEvent(g->cstream, g->ev_s, 0));
-    }
-    // passes plan the iterations still to do (it0 of them are done: a solve
-    // resumed after an exact tail)
-    const int todo = itermax - it0;
-    const long long max_passes = (todo + T - 1) / T;
-    // iterations pass k performs.  The cap takes max_passes passes of at most T
-    // iterations (no pass overshoots it); they are made as even as possible --
-    // `extra` passes of base + 1, the rest of base -- because a pass costs
-    // nearly as much with fewer iterations (a T' = 4 pass at 32768^2 is
-    // HBM-bound at 5.06 ms against 5.41 for T = 8), so 20 iterations run as
-    // 7 + 7 + 6 rather than 8 + 8 + 4.  A solve that converges earlier stops
-    // at the same iteration either way.
-    const long long base = todo / max_passes;
-    const long long extra = todo % max_passes;
-    auto t_of = [&](long long k) -> int { return (int)(base + (k < extra ? 1 : 0)); };
-    auto nparts_of = [&](int Tk) -> int {
-        if (T == 1 || Tk == T) return nparts;
-        SweepParams tp = tpl;
-        tb_geometry(g, Tk, tp);
-        return tb_parts(tp);
-    };
-    // iterations covered by the first p passes, and the passes that cover `it`
-    auto covered = [&](long long p) -> long long { return p * base + std::min(p, extra); };
-    auto passes_for = [&](long long it) -> long long {
-        const long long head = extra * (base + 1);  // iterations of the longer passes
-        if (it <= head) return (it + base) / (base + 1);
-        return std::min(extra + (it - head + base - 1) / base, max_passes);
-    };
-    // passes enqueued before the host reads the loop state: as many as the last
-    // solve took (rounded up: a solve capped at itermax = 100 with T = 8 --
-    // NS config 5 -- enqueues its 13 passes at once), at least 8
-    const int last_passes = (g->last_iters + T - 1) / T;
-    int batch = last_passes > 8 ? last_passes : 8;
-    for (;;) {
-        if (batch > max_passes - launched) batch = (int)(max_passes - launched);
-        if (batch < 1) batch = 1;
-        if (g->timing) {
-            int rc = ensure_events(g, 2 * (size_t)batch);
-            if (rc) return rc;
-        }
-        for (int b = 0; b < batch && pipelined; ++b) {
-            const long long k = launched + b;
-            const int Tk = t_of(k);
-            const double* src = pbuf(g, cur0 + k);
-            double* dst = pbuf(g, cur0 + k + 1);
-            double* part = g->partials + (k & 1) * (long long)g->partials_cap;
-            // interior blocks: after pass k-1 (this stream, plus the edge blocks:
-            // waited on at the end of the previous iteration) and decide k-2
-            if (k >= 2) HIPCHK(hipStreamWaitEvent(g->stream, g->ev_dk[k & 1], 0));
-            if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b], g->stream));
-            {
-                int rc_ = pass(g->stream, 1, src, dst, Tk, 0, part);
-                if (rc_) return rc_;
-            }
-            HIPCHK(hipEventRecord(g->ev_i[k & 1], g->stream));
-            // Part 2 (the blocks whose cone reads the halo) on the comm stream,
-            // right behind what it waits for: pass k+1's part 2 is enqueued here,
-            // after pass k's exchange, loop test and part 1 (its source is pass
-            // k's result), so no cross-stream wait stands between the exchange
-            // and it.  (On a stream of its own, waiting for the exchange on the
-            // comm stream and the interior blocks on this one, the second pass's
-            // part 2 started ~0.5 ms late on the 8-GPU rank block:
-            // profiles/r05_decomposed_loop_trace*.)  The first pass of a batch
-            // enqueues its own part 2: the previous batch's last pass leaves it
-            // out, so nothing of a batch is still queued on the comm stream
-            // behind the decide the host reads -- a solve that stops there (or a
-            // near-threshold hand-off to exact_tail, whose state upload would
-            // re-arm the device flag) leaves no pending launch that could still
-            // write a pressure buffer.
-            int rc = MISOR_OK;
-            if (first_x) {  // the solve's first pass: src's halo, then its part 2
-                first_x = false;
-                rc = exchange(g, const_cast<double*>(src), depth, g->cstream);
-                if (rc) return rc;
-            }
-            if (b == 0) {
-                rc = pass(g->cstream, 2, src, dst, Tk, 0, part);
-                if (rc) return rc;
-                HIPCHK(hipEventRecord(g->ev_e2[k & 1], g->cstream));
-            }
-            if (k + 1 < max_passes) {  // dst's halo (part 2 of pass k, above, wrote its send region)
-                rc = exchange(g, dst, depth, g->cstream);
-                if (rc) return rc;
-            }
-            HIPCHK(hipStreamWaitEvent(g->cstream, g->ev_i[k & 1], 0));
-            // the pass's residual sums for the all-reduce: the two-level sum (many
-            // workgroups, the last one writing st->sum) -- one workgroup summing
-            // every block partial took 70-100 us, after the last pass on the
-            // solve's critical path (profiles/r05_decomposed_loop_trace.csv)
-            launch_finish2(g->cstream, part, nparts_of(Tk), Tk, g->st, cells,
-                           g->partials + 2 * (long long)g->partials_cap, g->tb_queue + 10, 0);
-            rc = allreduce(g, g->st->sum, Tk, 0, g->cstream);
-            if (rc) return rc;
-            launch_decide(g->cstream, g->st, Tk, cells);
-            HIPCHK(hipEventRecord(g->ev_dk[k & 1], g->cstream));
-            if (k + 1 < max_passes && b + 1 < batch) {  // pass k+1's part 2: after both parts of pass k
-                const long long k1 = k + 1;
-                double* part1 = g->partials + (k1 & 1) * (long long)g->partials_cap;
-                rc = pass(g->cstream, 2, dst, pbuf(g, cur0 + k1 + 1), t_of(k1), 0, part1);
-                if (rc) return rc;
-                HIPCHK(hipEventRecord(g->ev_e2[k1 & 1], g->cstream));
-            }
-            // pass k+1's interior blocks read what part 2 of pass k wrote
-            HIPCHK(hipStreamWaitEvent(g->stream, g->ev_e2[k & 1], 0));
-            if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b + 1], g->stream));
-            if (b == batch - 1)  // the host reads the loop state after the last decide
-                HIPCHK(hipStreamWaitEvent(g->stream, g->ev_dk[k & 1], 0));
-        }
-        for (int b = 0; b < batch && g->dist && g->overlap && !pipelined; ++b) {
-            // Overlapped pass k.  comm stream: [wait pass k-1] all-reduce and
-            // decide of k-1, exchange of src_k.  compute stream: interior blocks
-            // of pass k (no halo reads) meanwhile, then [wait exchange] boundary
-            // blocks, partial sums.  (T = 1 only: T >= 2 takes the pipelined
-            // loop above.)  An interior pass launched after convergence (decide
-            // k-1 still in flight) only writes a buffer that is not the result.
-            const long long k = launched + b;
-            const int Tk = t_of(k);
-            const double* src = pbuf(g, cur0 + k);
-            double* dst = pbuf(g, cur0 + k + 1);
-            HIPCHK(hipEventRecord(g->ev_s, g->stream));
-            HIPCHK(hipStreamWaitEvent(g->cstream, g->ev_s, 0));
-            if (b > 0) {  // pass k-1 of this batch (the previous batch closed its own)
-                int rc = allreduce(g, g->st->sum, t_of(k - 1), 0, g->cstream);
-                if (rc) return rc;
-                launch_decide(g->cstream, g->st, t_of(k - 1), cells);
-                if (T > 1) {
-                    HIPCHK(hipEventRecord(g->ev_d, g->cstream));
-                    HIPCHK(hipStreamWaitEvent(g->stream, g->ev_d, 0));
-                }
-            }
-            int rc = exchange(g, const_cast<double*>(src), depth, g->cstream);
-            if (rc) return rc;
-            HIPCHK(hipEventRecord(g->ev_x, g->cstream));
-            if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b], g->stream));
-            {
-                int rc_ = pass(g->stream, 1, src, dst, Tk, 0, g->partials);
-                if (rc_) return rc_;
-            }
-            HIPCHK(hipStreamWaitEvent(g->stream, g->ev_x, 0));
-            {
-                int rc_ = pass(g->stream, 2, src, dst, Tk, 0, g->partials);
-                if (rc_) return rc_;
-            }
-            if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b + 1], g->stream));
-            launch_finish(g->stream, g->partials, nparts_of(Tk), Tk, g->st, cells, 0);
-            if (b == batch - 1) {  // close the batch: all-reduce + decide of the last one
-                HIPCHK(hipEventRecord(g->ev_s, g->stream));
-                HIPCHK(hipStreamWaitEvent(g->cstream, g->ev_s, 0));
-                rc = allreduce(g, g->st->sum, Tk, 0, g->cstream);
-                if (rc) return rc;
-                launch_decide(g->cstream, g->st, Tk, cells);
-                HIPCHK(hipEventRecord(g->ev_x, g->cstream));
-                HIPCHK(hipStreamWaitEvent(g->stream, g->ev_x, 0));
-            }
-        }
-        for (int b = 0; b < batch && !(g->dist && g->overlap); ++b) {
-            const long long k = launched + b;
-            const int Tk = t_of(k);
-            const double* src = pbuf(g, cur0 + k);
-            double* dst = pbuf(g, cur0 + k + 1);
-            if (g->dist) {  // 2T-deep halo of src: one exchange per pass
-                int rc = exchange(g, const_cast<double*>(src), depth);
-                if (rc) return rc;
-            }
-            if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b], g->stream));
-            {
-                int rc_ = pass(g->stream, 0, src, dst, Tk, 0, g->partials);
-                if (rc_) return rc_;
-            }
-            if (g->timing) HIPCHK(hipEventRecord(g->ev[2 * b + 1], g->stream));
-            if (g->dist) {
-                launch_finish(g->stream, g->partials, nparts_of(Tk), Tk, g->st, cells, 0);
-                int rc = allreduce(g, g->st->sum, Tk, 0);
-                if (rc) return rc;
-                launch_decide(g->stream, g->st, Tk, cells);
-            } else if (g->finish2) {  // the loop test in the last workgroup (tb_queue[9])
-                launch_finish2(g->stream, g->partials, nparts_of(Tk), Tk, g->st, cells,
-                               g->partials + 2 * (long long)g->partials_cap, g->tb_queue + 9, 1);
-            } else {
-                launch_finish(g->stream, g->partials, nparts_of(Tk), Tk, g->st, cells, 1);
-            }
-        }
-        HIPCHK(hipGetLastError());
-        launched += batch;
-        g->stats.launches += batch;
-        HIPCHK(hipMemcpyAsync(g->st_host, g->st, sizeof(DevState), hipMemcpyDeviceToHost,
-                              g->stream));
-        {
-            int rc_ = wait_stream(g, g->stream);
-            if (rc_) return rc_;
-        }
-        if (g->comm_timing) {
-            int rc = collect_comm_times(g);
-            if (rc) return rc;
-        }
-        if (g->timing) {
-            // passes after convergence exit at once; count only the real ones
-            const long long real_before = launched - batch;
-            const long long real_end = passes_for(g->st_host->it - it0);
-            for (int b = 0; b < batch; ++b) {
-                if (real_before + b >= real_end) break;
-                float ms = 0.f;
-                HIPCHK(hipEventElapsedTime(&ms, g->ev[2 * b], g->ev[2 * b + 1]));
-                g->stats.sweep_ms += ms;
-                g->stats.timed_sweeps += t_of(real_before + b);
-                g->stats.timed_passes++;
-            }
-        }
-        if (g->st_host->done) break;
-        if (launched >= max_passes) break;  // cannot happen: done covers it
-        batch = batch < 512 ? 2 * batch : 1024;
-    }
-    const int it = g->st_host->it;
-    const long long passes = passes_for(it - it0);
-    const int over = (int)(covered(passes) - (it - it0));
-    g->cur = (int)((cur0 + passes) % g->np);
-    if (over > 0) {
-        // the last pass ran past the iteration that ended the loop: redo it
-        // with T - over iterations from its source (untouched since)
-        const double* src = pbuf(g, cur0 + passes - 1);
-        {
-            int rc_ = pass(g->stream, 0, src, pbuf(g, g->cur), t_of(passes - 1) - over, 1, g->partials);
-            if (rc_) return rc_;
-        }
-        HIPCHK(hipGetLastError());
-    }
-    g->comm_timing = false;
-    g->p_stale = g->dist;  // the final field's halo: exchanged by its next reader (p_halo)
-    {
-        int rc_ = wait_stream(g, g->stream);
-        if (rc_) return rc_;
-    }
-    g->last_iters = it;
-    g->stats.sweeps += it - it0;
-    g->stats.iters_per_pass = T;
-    g->stats.tb_variant = T == 1 ? -1 : tpl.variant;
-    g->stats.chained = T > 1 && tpl.chain ? 1 : 0;
-    // stopped before an iteration near the threshold: the exact tail goes on
-    // from it (misor_solve_rb_n)
-    if (g->st_host->near) *hand_off = true;
-    *iters = it;
-    *res = g->st_host->res;
-    return MISOR_OK;
-}
-
-int misor_solve_lex(misor_grid* g, int xorder, int* iters, double* res) {
-    if (!g) return fail(MISOR_EINVAL, "null grid");
-    if (g->desc.nranks != 1)
-        return fail(MISOR_ESTATE, "lexicographic SOR has no decomposed form (use red-black)");
-    if (g->desc.variant != MISOR_SOLVE_RB)
-        return fail(MISOR_ESTATE, "lexicographic SOR uses the solveRB factor (variant RB)");
-    HIPCHK(hipSetDevice(g->device));
-    const double epssq = g->desc.eps * g->desc.eps;
-    DevState s0{};
-    s0.res = 1.0;
-    s0.epssq = epssq;
-    s0.itermax = g->desc.itermax;
-    *g->st_host = s0;
-    HIPCHK(hipMemcpyAsync(g->st, g->st_host, sizeof(DevState), hipMemcpyHostToDevice,
-                          g->stream));
-    const double cells = (double)g->desc.imax * (double)g->desc.jmax;
-    launch_solve_lex(g->stream, pbuf(g, g->cur), g->fld[kRhs], g->loc.ni, g->loc.nj, g->pitch,
-                     g->sp.idx2, g->sp.idy2, g->sp.coef, cells, xorder != 0, g->st);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(g->st_host, g->st, sizeof(DevState), hipMemcpyDeviceToHost,
-                          g->stream));
-    HIPCHK(hipStreamSynchronize(g->stream));
-    const int it = g->st_host->it;
-    g->last_iters = it;
-    g->stats.sweeps += it;
-    if (iters) *iters = it;
-    if (res) *res = g->st_host->res;
-    return MISOR_OK;
-}
-
-int misor_solve_rb(misor_grid* g, int* iters, double* res) {
-    if (!g) return fail(MISOR_EINVAL, "null grid");
-    return misor_solve_rb_n(g, g->desc.itermax, iters, res);
-}
-
-// ---------------------------------------------------------------------------
-// NS step
-// ---------------------------------------------------------------------------
-
-int misor_ns_setup(misor_grid* g, const misor_ns_desc* ns) {
-    if (!g || !ns) return fail(MISOR_EINVAL, "null argument");
-    NsLaunch& L = g->nl;
-    L.s = g->stream;
-    L.pitch = g->pitch;
-    L.ni = g->loc.ni;
-    L.nj = g->loc.nj;
-    L.prm.dx = g->desc.dx;
-    L.prm.dy = g->desc.dy;
-    L.prm.dt = 0.0;
-    L.prm.xlength = ns->xlength;
-    L.prm.ylength = ns->ylength;
-    L.prm.re = ns->re;
-    L.prm.gx = ns->gx;
-    L.prm.gy = ns->gy;
-    L.prm.gamma = ns->gamma;
-    L.prm.bc_left = ns->bcLeft;
-    L.prm.bc_right = ns->bcRight;
-    L.prm.bc_bottom = ns->bcBottom;
-    L.prm.bc_top = ns->bcTop;
-    L.prm.problem = ns->problem;
-    L.wall_left = g->loc.neighbours[0] < 0;
-    L.wall_right = g->loc.neighbours[1] < 0;
-    L.wall_bottom = g->loc.neighbours[2] < 0;
-    L.wall_top = g->loc.neighbours[3] < 0;
-    L.ioff = g->loc.ioff;
-    L.joff = g->loc.joff;
-    L.imax_g = g->desc.imax;
-    L.jmax_g = g->desc.jmax;
-    ++g->uv_ver;
-    g->ns_ready = true;
-    return MISOR_OK;
-}
-
-#define NEED_NS(g)                                                                 \
-    do {                                                                           \
-        if (!(g)) return fail(MISOR_EINVAL, "null grid");                          \
-        if (!(g)->ns_ready) return fail(MISOR_ESTATE, "misor_ns_setup not called"); \
-        HIPCHK(hipSetDevice((g)->device));                                         \
-    } while (0)
-
-// add the NS kernel groups' timed launches so far to the stats
-static int collect_ns_times(misor_grid* g) {
-    for (int k = 0; k < 3; ++k) {
-        for (size_t q = 0; q < g->nev_used[k]; ++q) {
-            float ms = 0.f;
-            HIPCHK(hipEventSynchronize(g->nev[k][2 * q + 1]));
-            HIPCHK(hipEventElapsedTime(&ms, g->nev[k][2 * q], g->nev[k][2 * q + 1]));
-            g->stats.ns_ms[k] += ms;
-        }
-        g->nev_used[k] = 0;
-    }
-    return MISOR_OK;
-}
-
-// a start/stop event pair around launches of NS kernel group k (0 computeFG,
-// 1 adaptUV, 2 normalizePressure) when timing is on; `call` counts a call
-// (normalizePressure records three pairs per call)
-static bool ns_pair(misor_grid* g, int k, bool call, hipEvent_t* e0, hipEvent_t* e1) {
-    if (!g->timing) return false;
-    if (g->nev_used[k] >= 512 && collect_ns_times(g) != MISOR_OK) return false;
-    std::vector<hipEvent_t>& v = g->nev[k];
-    size_t& u = g->nev_used[k];
-    while (v.size() < 2 * (u + 1)) {
-        hipEvent_t e;
-        if (hipEventCreate(&e) != hipSuccess) return false;
-        v.push_back(e);
-    }
-    *e0 = v[2 * u];
-    *e1 = v[2 * u + 1];
-    ++u;
-    if (call) g->stats.ns_calls[k]++;
-    return true;
-}
-
-int misor_max_uv(misor_grid* g, double* umax, double* vmax) {
-    NEED_NS(g);
-    // the partials adaptUV computed, when no u, v write came after it
-    const double* part = g->max_partials;
-    if (g->max_ver != g->uv_ver) {
-        launch_absmax2(g->nl, g->fld[kU], g->fld[kV], g->red_partials);
-        part = g->red_partials;
-    }
-    launch_finish_reduce(g->stream, part, reduce_blocks(g->loc.ni, g->loc.nj),
-                         kReduceMax, 2, g->red_out);
-    HIPCHK(hipGetLastError());
-    if (g->dist)
-    {
-        int rc = allreduce(g, g->red_out, 2, 1);
-        if (rc) return rc;
-    }
-    HIPCHK(hipMemcpyAsync(g->red_host, g->red_out, 2 * sizeof(double), hipMemcpyDeviceToHost,
-                          g->stream));
-    {
-        int rc_ = wait_stream(g, g->stream);
-        if (rc_) return rc_;
-    }
-    if (umax) *umax = g->red_host[0];
-    if (vmax) *vmax = g->red_host[1];
-    return MISOR_OK;
-}
-
-int misor_compute_timestep(misor_grid* g, double dt_bound, double tau, double* dt_out) {
-    double umax = 0, vmax = 0;
-    int rc = misor_max_uv(g, &umax, &vmax);
-    if (rc) return rc;
-    // computeTimestep, assignment-5/sequential/src/solver.c:219-234
-    double dt = dt_bound;
-    const double dx = g->desc.dx, dy = g->desc.dy;
-    if (umax > 0) dt = (dt > dx / umax) ? dx / umax : dt;
-    if (vmax > 0) dt = (dt > dy / vmax) ? dy / vmax : dt;
-    g->nl.prm.dt = dt * tau;
-    if (dt_out) *dt_out = g->nl.prm.dt;
-    return MISOR_OK;
-}
-
-int misor_set_dt(misor_grid* g, double dt) {
-    if (!g) return fail(MISOR_EINVAL, "null grid");
-    g->nl.prm.dt = dt;
-    return MISOR_OK;
-}
-
-int misor_set_boundary_conditions(misor_grid* g) {
-    NEED_NS(g);
-    ++g->uv_ver;
-    launch_set_bc(g->nl, g->fld[kU], g->fld[kV]);
-    HIPCHK(hipGetLastError());
-    return MISOR_OK;
-}
-
-int misor_set_special_boundary_condition(misor_grid* g) {
-    NEED_NS(g);
-    ++g->uv_ver;
-    launch_special_bc(g->nl, g->fld[kU]);
-    HIPCHK(hipGetLastError());
-    return MISOR_OK;
-}
-
-int misor_compute_fg(misor_grid* g) {
-    NEED_NS(g);
-    int rc = exchange(g, g->fld[kU], 1);  // 9-point stencil incl. diagonals: corners too
-    if (!rc) rc = exchange(g, g->fld[kV], 1);
-    if (rc) return rc;
-    ++g->fgr_ver;
-    hipEvent_t t0 = nullptr, t1 = nullptr;
-    const bool timed = ns_pair(g, 0, true, &t0, &t1);
-    if (timed) HIPCHK(hipEventRecord(t0, g->stream));
-    if (g->ns_fuse) {  // computeRHS of the same f, g in the same pass (ns_kernels.hip)
-        launch_compute_fg_rhs(g->nl, g->fld[kU], g->fld[kV], g->fld[kF], g->fld[kG],
-                              g->fld[kRhs]);
-        g->rhs_halo = 0;
-        g->fused_ver = g->fgr_ver;
-        g->fused_dt = g->nl.prm.dt;
-    } else {
-        launch_compute_fg(g->nl, g->fld[kU], g->fld[kV], g->fld[kF], g->fld[kG]);
-    }
-    if (timed) HIPCHK(hipEventRecord(t1, g->stream));
-    HIPCHK(hipGetLastError());
-    return MISOR_OK;
-}
-
-int misor_compute_rhs(misor_grid* g) {
-    NEED_NS(g);
-    // the fused computeFG already wrote rhs from these f, g and this dt: only
-    // the cells that read a neighbour's F(0, j) / G(i, 0) are left
-    // (decomposed: the exchange is collective, so every rank takes part, also
-    // one with walls on its left and bottom whose rhs is complete already)
-    const bool fused = g->fused_ver == g->fgr_ver && g->fused_dt == g->nl.prm.dt;
-    ++g->fgr_ver;
-    g->rhs_halo = 0;
-    if (fused && !g->dist) return MISOR_OK;
-    int rc = exchange(g, g->fld[kF], 1);  // F(i-1,j), G(i,j-1): the skeleton's shift()
-    if (!rc) rc = exchange(g, g->fld[kG], 1);
-    if (rc) return rc;
-    if (fused) {
-        if (!(g->nl.wall_left && g->nl.wall_bottom))
-            launch_rhs_edges(g->nl, g->fld[kF], g->fld[kG], g->fld[kRhs]);
-    } else {
-        launch_compute_rhs(g->nl, g->fld[kF], g->fld[kG], g->fld[kRhs]);
-    }
-    HIPCHK(hipGetLastError());
-    return MISOR_OK;
-}
-
-// normalizePressure (assignment-5/sequential/src/solver.c:204-217) with the
-// sum exact (ns_kernels.hip launch_exact_sum): the mean, and so p, is the same
-// for every decomposition -- the reference's MPI build all-reduces per-rank
-// partial sums (assignment-5/skeleton/src/solver.c:697), whose rounding depends
-// on the partition.  Two passes over p: the global max |p| (order-free) fixes
-// the fixed-point scale, then the exact sum; one host round trip per call
-// (every 100 time steps in the reference's main loop).
-int misor_normalize_pressure(misor_grid* g) {
-    NEED_NS(g);
-    double* p = pbuf(g, g->cur);
-    const int nb = reduce_blocks(g->loc.ni, g->loc.nj);
-    hipEvent_t t0 = nullptr, t1 = nullptr;
-    bool timed = ns_pair(g, 2, true, &t0, &t1);
-    if (timed) HIPCHK(hipEventRecord(t0, g->stream));
-    launch_absmax2(g->nl, p, p, g->red_partials);
-    launch_finish_reduce(g->stream, g->red_partials, nb, kReduceMax, 2, g->red_out);
-    if (timed) HIPCHK(hipEventRecord(t1, g->stream));
-    HIPCHK(hipGetLastError());
-    if (g->dist) {
-        int rc = allreduce(g, g->red_out, 1, 1);
-        if (rc) return rc;
-    }
-    HIPCHK(hipMemcpyAsync(g->red_host, g->red_out, sizeof(double), hipMemcpyDeviceToHost,
-                          g->stream));
-    {
-        int rc_ = wait_stream(g, g->stream);
-        if (rc_) return rc_;
-    }
-    const double mx = g->red_host[0];
-    int E = 0;
-    (void)frexp(mx, &E);
-    timed = ns_pair(g, 2, false, &t0, &t1);
-    if (timed) HIPCHK(hipEventRecord(t0, g->stream));
-    launch_exact_sum(g->nl, p, E, g->red_partials, g->red_out);
-    if (timed) HIPCHK(hipEventRecord(t1, g->stream));
-    HIPCHK(hipGetLastError());
-    if (g->dist) {
-        int rc = allreduce(g, g->red_out, 3, 0);  // integer limbs < 2^53: exact
-        if (rc) return rc;
-    }
-    HIPCHK(hipMemcpyAsync(g->red_host, g->red_out, 3 * sizeof(double), hipMemcpyDeviceToHost,
-                          g->stream));
-    {
-        int rc_ = wait_stream(g, g->stream);
-        if (rc_) return rc_;
-    }
-    const double cells = (double)(g->desc.imax + 2) * (double)(g->desc.jmax + 2);
-    const double avg = exact_sum_value(g->red_host, E) / cells;  // solver.c:213
-    timed = ns_pair(g, 2, false, &t0, &t1);
-    if (timed) HIPCHK(hipEventRecord(t0, g->stream));
-    launch_sub_mean(g->nl, p, avg);
-    if (timed) HIPCHK(hipEventRecord(t1, g->stream));
-    HIPCHK(hipGetLastError());
-    return MISOR_OK;
-}
-
-int misor_adapt_uv(misor_grid* g) {
-    NEED_NS(g);
-    {
-        int rc = p_halo(g);  // P(i+1,j), P(i,j+1) of the rank's last column / row
-        if (rc) return rc;
-    }
-    hipEvent_t t0 = nullptr, t1 = nullptr;
-    const bool timed = ns_pair(g, 1, true, &t0, &t1);
-    if (timed) HIPCHK(hipEventRecord(t0, g->stream));
-    launch_adapt_absmax(g->nl, g->fld[kF], g->fld[kG], pbuf(g, g->cur), g->fld[kU], g->fld[kV],
-                        g->max_partials);
-    if (timed) HIPCHK(hipEventRecord(t1, g->stream));
-    g->max_ver = ++g->uv_ver;
-    HIPCHK(hipGetLastError());
-    return MISOR_OK;
-}
 
 int misor_enable_timing(misor_grid* g, int on) {
     if (!g) return fail(MISOR_EINVAL, "null grid");
@@ -2625,5 +804,3 @@ int misor_reset_stats(misor_grid* g) {
     g->stats = misor_stats{};
     return MISOR_OK;
 }
-
-}  // extern "C"

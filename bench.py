@@ -799,6 +799,9 @@ def main():
                     help="iterations per kernel launch (0: library default)")
     ap.add_argument("--tb-variant", type=int, default=-1,
                     help="temporally blocked kernel variant (-1: library default)")
+    ap.add_argument("--res-lite", type=int, choices=(0, 1), default=1,
+                    help="residual lower bounds of the 10-iteration passes (MISOR_TUNE_RES_LITE; "
+                         "0: every iteration's residual counted in full, for A/B)")
     ap.add_argument("--workload", choices=("poisson", "ns", "ns3d"), default="poisson",
                     help="poisson: the headline metric (config 4); ns: config 5, "
                          "dcavity NS weak scaling (--size cells^2 per GPU); ns3d: "
@@ -887,6 +890,7 @@ def main():
         g.set_tuning(M.TUNE_TB_VARIANT, args.tb_variant)
     if args.tsteps > 0:
         g.set_tuning(M.TUNE_TSTEPS, args.tsteps)
+    g.set_tuning(M.TUNE_RES_LITE, args.res_lite)
     g.poisson_init(float(pdims[0]), float(pdims[1]), 2)
     local_cells = g.loc.ni * g.loc.nj
     rccl_ranks = g.comm_ranks() if world > 1 else None
@@ -992,7 +996,11 @@ def main():
                                    imax, jmax, args.steps, split_txt),
                    "iters_per_pass": T, "pass_split": split, "tb_variant": tbv,
                    "imax": imax, "jmax": jmax, "omega": 1.9, "problem": 2,
-                   "decomposition": dims, "baseline_config": 4},
+                   "decomposition": dims, "baseline_config": 4,
+                   # the 10-iteration passes' residual lower bounds (MISOR_TUNE_RES_LITE):
+                   # same p / iterations / res bits; misses = solves that fell back
+                   "residual_lower_bounds": {"on": bool(g.get_tuning(M.TUNE_RES_LITE)),
+                                             "misses": st.get("lite_misses", 0)}},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / PEAK_GBS, 4),
                      "traffic": traffic,

@@ -126,6 +126,9 @@ typedef struct {
      * subtract: absmax2 + finish_reduce, exact_sum, sub_mean kernels) */
     double ns_ms[3];
     long long ns_calls[3];
+    /* solves whose residual lower bounds (MISOR_TUNE_RES_LITE) missed once: the
+     * pass redone counting every cell, the rest of the solve so */
+    long long lite_misses;
 } misor_stats;
 
 const char* misor_last_error(void);
@@ -258,7 +261,16 @@ enum {
                                     * recomputed one sweep at a time with an exact
                                     * (order-independent) sum of r^2, so the iteration count
                                     * and res do not depend on the partition.  Default 10;
-                                    * >= 300: off (set by tests to force the path: -30) */
+                                    * >= 300: off (set by tests to force the path: -30) */,
+    MISOR_TUNE_RES_LITE = 15       /* single rank, 10-iteration split-ring passes: 1
+                                    * (default) = the steady chunks count the residual of
+                                    * a pass's iterations but its last on one row in S, a
+                                    * lower bound that the loop test accepts only where it
+                                    * proves the loop goes on (not converged, not near the
+                                    * threshold); otherwise the pass is redone counting
+                                    * every cell and the solve continues so.  The iteration
+                                    * count, res and p are the same bits either way.
+                                    * 0 = every iteration counted in full */
 };
 int misor_set_tuning(misor_grid* g, int key, int value);
 int misor_get_tuning(const misor_grid* g, int key, int* value);

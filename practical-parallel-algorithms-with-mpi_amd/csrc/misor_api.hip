@@ -759,6 +759,10 @@ int misor_set_tuning(misor_grid* g, int key, int value) {
         g->near_exp = value;
         g->near_rel = value >= 300 ? 0.0 : pow(10.0, -(double)value);
         return MISOR_OK;
+    case MISOR_TUNE_RES_LITE:
+        if (value != 0 && value != 1) return fail(MISOR_EINVAL, "RES_LITE is 0 or 1");
+        g->res_lite = value != 0;
+        return MISOR_OK;
     default: return fail(MISOR_EINVAL, "unknown tuning key %d", key);
     }
 }
@@ -777,6 +781,7 @@ int misor_get_tuning(const misor_grid* g, int key, int* value) {
     case MISOR_TUNE_TB_PERSISTENT: *value = g->tb_persistent; return MISOR_OK;
     case MISOR_TUNE_TB_CHAIN: *value = chain_on(g, g->tp.variant); return MISOR_OK;
     case MISOR_TUNE_NEAR_BAND: *value = g->near_exp; return MISOR_OK;
+    case MISOR_TUNE_RES_LITE: *value = g->res_lite; return MISOR_OK;
     case MISOR_TUNE_NS_FUSE: *value = g->ns_fuse; return MISOR_OK;
     case MISOR_TUNE_FINISH2: *value = g->finish2; return MISOR_OK;
     case MISOR_TUNE_TB_RESERVE: *value = g->tb_reserve; return MISOR_OK;

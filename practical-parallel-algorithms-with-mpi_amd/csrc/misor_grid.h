@@ -121,6 +121,10 @@ struct misor_grid {
     int near_exp = 10;
     double* rsq = nullptr;  // exact_tail: r^2 per cell (allocated on first use)
     bool small_solve = true;  // whole-solve LDS kernel when p fits (single rank)
+    // MISOR_TUNE_RES_LITE: single-rank 10-iteration split-ring passes count the
+    // residual of their inner iterations on one row in S (misor_solve.hip)
+    bool res_lite = true;
+    bool lite_block = false;  // the rest of this solve counts in full (a lower bound missed)
 
     // temporally blocked sweep (sor_tb.hip): T iterations per pass over HBM
     int tsteps = kDefaultTsteps;  // requested T (1: single-iteration kernel)

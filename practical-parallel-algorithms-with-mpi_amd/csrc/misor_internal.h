@@ -137,6 +137,8 @@ struct DevState {
     int itermax;   // cap of the current solve call
     int near;      // 1: stopped before iteration it+1, whose res fell within nband of
                    // eps^2 (misor_api.hip exact_tail recomputes from there)
+    int lite_miss; // 1: stopped before iteration it+1, whose residual lower bound (a
+                   // lite pass, SweepParams::lite) did not prove the loop goes on
     double res;    // residual of the last iteration
     double epssq;
     double nband = -1.0;  // |res - eps^2| <= nband: near the threshold (< 0: off, the
@@ -174,6 +176,9 @@ struct SweepParams {
     int seg_cap;              // dynamic segment slots (created by steals)
     int chain_blocks;         // blocks in the launch (its part)
     int chain_edge;           // the edge list (strips at a physical left / right side)
+    int lite;                 // the split ring's steady chunks count the residual of the
+                              // stages before the last one on one row in S (a lower
+                              // bound; misor_solve.hip kLite)
     int chain_grid;           // edge list: its workgroups (the first of the launch)
     int seg_run[9];           // XCD x takes the initial segments [seg_run[x], seg_run[x+1])
     unsigned long long* trace;  // diagnostics (MISOR_CHAIN_TRACE): per block L, 3 words --
@@ -249,7 +254,7 @@ constexpr int kFinishChunks = 32;
 // runs the loop test itself (one launch); nullptr: a second, finish launch.
 // decide 0: only the sums into st->sum (decomposed: all-reduce, then decide)
 void launch_finish2(hipStream_t s, const double* partials, int nparts, int T, DevState* st,
-                    double cells, double* scratch, int* count, int decide);
+                    double cells, double* scratch, int* count, int decide, int lite = 0);
 // queue: 8 device ints (zeroed by the launch) for a persistent launch whose
 // workgroups take blocks from per-XCD queues; nullptr: one workgroup per block
 void launch_tb(hipStream_t s, int T, const SweepParams& prm, const double* src, double* dst,

@@ -274,6 +274,20 @@ int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* iters,
     g->comm_timing = g->timing && g->dist;
     g->cev_used[0] = g->cev_used[1] = 0;
     const int depth = 2 * T;  // halo of src each pass needs
+    // Residual lower bounds (MISOR_TUNE_RES_LITE): on one rank, a
+    // kShortT-iteration split-ring pass counts r^2 of its iterations but the
+    // last on one row in S of its steady chunks (sor_tbh.h hrs_step LITE), one
+    // FP64 FMA per update fewer on a VALU-bound pass.  Each such sum is a lower
+    // bound of the iteration's residual; the loop test (rb_partsum_kernel) takes
+    // it only where it proves the loop goes on -- >= eps^2, outside the near
+    // band, before itermax -- and otherwise stops the pass before that
+    // iteration (DevState::lite_miss): the pass is redone from its source up to
+    // there and the rest of the solve counts every cell.  The pass's last
+    // iteration is always counted in full, so res after every pass is exact.
+    const bool lite_on = g->res_lite && !g->lite_block && !g->dist && g->finish2 && T > 1;
+    auto lite_pass = [&](int Tp, int force) {
+        return lite_on && force == 0 && Tp == kShortT && tpl.variant == kHrTbVariant;
+    };
     const int nparts = T == 1 ? g->nparts : tb_parts(tpl);
     double* const rhs = g->fld[kRhs];
     auto pass = [&](hipStream_t s, int part, const double* src, double* dst, int Tp, int force,
@@ -292,6 +306,7 @@ int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* iters,
             // at the end of the interior blocks
             tp.reserve = part == 1 ? g->tb_reserve : 0;
             if (Tp != T) tb_geometry(g, Tp, tp);  // narrower cone: wider strips
+            tp.lite = part == 0 && lite_pass(Tp, force) ? 1 : 0;
             if (tp.chain) {  // chained runs, work stealing (parts 0 / 1 and 2 concurrently)
                 const misor_grid::ChainPlan* pl = nullptr;
                 int rc = chain_plan(g, tp.variant, Tp, part, &pl);
@@ -551,7 +566,8 @@ int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* iters,
                 launch_decide(g->stream, g->st, Tk, cells);
             } else if (g->finish2) {  // the loop test in the last workgroup (tb_queue[9])
                 launch_finish2(g->stream, g->partials, nparts_of(Tk), Tk, g->st, cells,
-                               g->partials + 2 * (long long)g->partials_cap, g->tb_queue + 9, 1);
+                               g->partials + 2 * (long long)g->partials_cap, g->tb_queue + 9, 1,
+                               lite_pass(Tk, 0) ? (1 << (Tk - 1)) - 1 : 0);
             } else {
                 launch_finish(g->stream, g->partials, nparts_of(Tk), Tk, g->st, cells, 1);
             }
@@ -611,6 +627,15 @@ int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* iters,
     g->stats.iters_per_pass = T;
     g->stats.tb_variant = T == 1 ? -1 : tpl.variant;
     g->stats.chained = T > 1 && tpl.chain ? 1 : 0;
+    if (g->st_host->lite_miss) {
+        // a residual lower bound proved nothing: the field is the state after
+        // `it` iterations (the pass redone above), the rest counts every cell
+        g->stats.lite_misses++;
+        g->lite_block = true;
+        const int rc = solve_rb_from(g, itermax, it, g->st_host->res, iters, res, hand_off);
+        g->lite_block = false;
+        return rc;
+    }
     // stopped before an iteration near the threshold: the exact tail goes on
     // from it (misor_solve_rb_n)
     if (g->st_host->near) *hand_off = true;

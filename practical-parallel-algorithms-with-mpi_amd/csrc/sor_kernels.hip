@@ -329,7 +329,7 @@ template <bool SC1>
 __device__ __forceinline__ void finish_body(const double* __restrict__ partials, int n, int T,
                                             DevState* st, double cells, int decide,
                                             double (&sh)[kMaxT][kFinishThreads],
-                                            double (&tot)[kMaxT]) {
+                                            double (&tot)[kMaxT], int lite = 0) {
     constexpr int NT = kFinishThreads;
     const int t = threadIdx.x;
     auto ld = [&](const double* q) {
@@ -389,6 +389,23 @@ __device__ __forceinline__ void finish_body(const double* __restrict__ partials,
                 st->sum[g] = tot[g];  // decomposed: all-reduce, then decide
             } else if (!st->done) {
                 const double res = tot[g] / cells;
+                if ((lite >> g) & 1) {
+                    // a lower bound of the iteration's residual (the pass's steady
+                    // chunks counted one row in S of this stage): it decides only
+                    // where it proves the loop goes on -- not converged and not
+                    // near the threshold, whatever the cells left out add
+                    const int it = st->it + 1;
+                    const bool on = st->nband >= 0.0 ? res > st->epssq + st->nband
+                                                     : res >= st->epssq;
+                    if (on && it < st->itermax) {
+                        st->it = it;
+                        st->res = res;  // (the pass's last stage is counted in full)
+                    } else {
+                        st->lite_miss = 1;  // the host redoes the pass counting every cell
+                        st->done = 1;
+                    }
+                    continue;
+                }
                 if (fabs(res - st->epssq) <= st->nband) {  // near: stop before it
                     st->near = 1;
                     st->done = 1;
@@ -421,7 +438,8 @@ __global__ __launch_bounds__(kFinishThreads) void rb_finish_kernel(
 __global__ __launch_bounds__(256) void rb_partsum_kernel(const double* __restrict__ partials,
                                                          int n, const DevState* __restrict__ st,
                                                          double* __restrict__ out, int* count,
-                                                         int T, double cells, int decide) {
+                                                         int T, double cells, int decide,
+                                                         int lite) {
     __shared__ double sh[256];
     __shared__ int is_last;
     // (st->done is the same for the whole launch: only its last workgroup
@@ -472,15 +490,17 @@ __global__ __launch_bounds__(256) void rb_partsum_kernel(const double* __restric
         __shared__ double fsh[kMaxT][kFinishThreads];
         __shared__ double tot[kMaxT];
         finish_body<true>(out, kFinishChunks, T, const_cast<DevState*>(st), cells, decide, fsh,
-                          tot);
+                          tot, lite);
         if (t == 0) __hip_atomic_store(count, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
 void launch_finish2(hipStream_t s, const double* partials, int nparts, int T, DevState* st,
-                    double cells, double* scratch, int* count, int decide) {
+                    double cells, double* scratch, int* count, int decide, int lite) {
+    // (lite: the stages whose sums are lower bounds -- only with the loop test
+    // in the last workgroup, count != nullptr)
     hipLaunchKernelGGL(rb_partsum_kernel, dim3(kFinishChunks, T), dim3(256), 0, s, partials,
-                       nparts, st, scratch, count, T, cells, decide);
+                       nparts, st, scratch, count, T, cells, decide, count ? lite : 0);
     if (!count)
         hipLaunchKernelGGL(rb_finish_kernel, dim3(1), dim3(kFinishThreads), 0, s, scratch,
                            kFinishChunks, T, st, cells, decide);

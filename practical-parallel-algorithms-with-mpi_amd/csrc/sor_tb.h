@@ -549,7 +549,8 @@ template <int QA, int QB, bool P2, bool EM = false>
 __device__ __forceinline__ void stage_pair(const Lane& c, d2& InA, d2& A_a, d2& M1_a, d2& M2_a,
                                            d2 Ra_a, d2 Rb_a, TallyAcc& acc_a, d2& InB, d2& A_b,
                                            d2& M1_b, d2& M2_b, d2 Ra_b, d2 Rb_b,
-                                           TallyAcc& acc_b) {
+                                           TallyAcc& acc_b, bool tally_a = true,
+                                           bool tally_b = true) {
     auto fl = [](double v) { return from_left(v); };
     auto fr = [](double v) { return from_right(v); };
     double na, nb, ra, rb;
@@ -559,16 +560,16 @@ __device__ __forceinline__ void stage_pair(const Lane& c, d2& InA, d2& A_a, d2& 
     d2 Mr_a = A_a, Mr_b = A_b;
     put_new<QA, EM>(c, Mr_a, na);
     put_new<QB, EM>(c, Mr_b, nb);
-    tally_q<QA, EM>(c, acc_a, ra);
-    tally_q<QB, EM>(c, acc_b, rb);
+    if (tally_a) tally_q<QA, EM>(c, acc_a, ra);
+    if (tally_b) tally_q<QB, EM>(c, acc_b, rb);
     // black: row rin-2 (M1), reading the new red row above
     upd2<P2>(c, upd_ops<QA, false>(M1_a, Mr_a, M2_a, Rb_a, fl, fr),
              upd_ops<QB, false>(M1_b, Mr_b, M2_b, Rb_b, fl, fr), na, nb, ra, rb);
     d2 F_a = M1_a, F_b = M1_b;
     put_new<QA, EM>(c, F_a, na);
     put_new<QB, EM>(c, F_b, nb);
-    tally_q<QA, EM>(c, acc_a, ra);
-    tally_q<QB, EM>(c, acc_b, rb);
+    if (tally_a) tally_q<QA, EM>(c, acc_a, ra);
+    if (tally_b) tally_q<QB, EM>(c, acc_b, rb);
     ghost_cols<EM>(c, F_a);
     ghost_cols<EM>(c, F_b);
     M2_a = F_a; M1_a = Mr_a; A_a = InA; InA = F_a;

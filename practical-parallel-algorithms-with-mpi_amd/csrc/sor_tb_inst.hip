@@ -71,6 +71,13 @@ void MISOR_CAT(launch_tb_t, MISOR_TB_T)(hipStream_t s, const SweepParams& prm,
             // (one kernel for the main and the edge list: a strip at a physical
             // side marches block by block, the workgroup's other strips chain)
             const int res = residenthc<kT, 4, 2, false, SK_>();
+            if constexpr (kT == kShortT) {  // (the residual lower bound: the short plan's T)
+                if (prm.lite) {
+                    if (prm.pow2) gc(rb_tbhc_kernel<kT, 4, 2, true, SK_, 0, true>, res);
+                    else          gc(rb_tbhc_kernel<kT, 4, 2, false, SK_, 0, true>, res);
+                    return;
+                }
+            }
             if (prm.pow2) gc(rb_tbhc_kernel<kT, 4, 2, true, SK_, 0>, res);
             else          gc(rb_tbhc_kernel<kT, 4, 2, false, SK_, 0>, res);
             return;

@@ -170,7 +170,7 @@ __device__ __forceinline__ void hr_step(HrMarch<T, D>& m, d2* R, const Lane& c, 
 // residual windows sit one row higher (stage<..., SKH>).  Register ring: rows
 // n - 2K + 2 .. n + 1 + D; the row the leading register stages read last (n -
 // 2K + 2) moves to the LDS ring, which holds rows down to n - 2T + 1.
-template <int T, int D, int MODE, int Q, int PH, bool P2>
+template <int T, int D, int MODE, int Q, int PH, bool P2, bool LITE = false>
 __device__ __forceinline__ void hrs_step(HrMarch<T, D>& m, d2* R, const Lane& c, const HrIo& io,
                                          int r0, unsigned off_n, unsigned st_base) {
     using G = Hr<T, D, 1>;
@@ -202,12 +202,18 @@ __device__ __forceinline__ void hrs_step(HrMarch<T, D>& m, d2* R, const Lane& c,
     d2 prevM2 = m.M2[T - 1];
     if constexpr (MODE == kSteady || MODE == kSteadyEdge) {
         constexpr bool EM = MODE == kSteadyEdge;
+        // LITE: the residual of the stages before the last one only on the
+        // chunk's first step (a lower bound of each iteration's sum: the loop
+        // test, rb_partsum_kernel, takes it as a certificate or redoes the
+        // pass with every cell counted)
+        constexpr bool kAll = !LITE || PH == 0;
 #pragma unroll
         for (int k = 0; k < SKH; ++k) {
             const int ta = SKH + k, tb = k;
             stage_pair<Q, 1 - Q, P2, EM>(c, u, m.A[ta], m.M1[ta], m.M2[ta], rr(ta, true),
                                          rr(ta, false), m.acc[ta], v, m.A[tb], m.M1[tb],
-                                         m.M2[tb], rr(tb, true), rr(tb, false), m.acc[tb]);
+                                         m.M2[tb], rr(tb, true), rr(tb, false), m.acc[tb],
+                                         kAll || ta == T - 1, kAll || tb == T - 1);
         }
         if (T - SKH > SKH)
             u = stage<T, Q, MODE, false, P2, SKH>(c, T - 1, true, u, r0 - 2 * (T - 1),
@@ -283,13 +289,14 @@ __device__ __forceinline__ void hrs_step(HrMarch<T, D>& m, d2* R, const Lane& c,
 }
 
 // steps NN of a chunk whose first step has ring phase P0 and colour Q0
-template <int T, int D, int SK, int MODE, int Q0, bool P2, int P0 = 0, int... NN>
+template <int T, int D, int SK, int MODE, int Q0, bool P2, int P0 = 0, bool LITE = false,
+          int... NN>
 __device__ __forceinline__ void hr_chunk(HrMarch<T, D>& m, d2* R, const Lane& c, const HrIo& io,
                                          int r0, unsigned off_n, unsigned st_base,
                                          std::integer_sequence<int, NN...>) {
     constexpr int S = Hr<T, D, SK>::S;
     if constexpr (SK)
-        (hrs_step<T, D, MODE, Q0 ^ (NN & 1), (P0 + NN) % S, P2>(
+        (hrs_step<T, D, MODE, Q0 ^ (NN & 1), (P0 + NN) % S, P2, LITE>(
              m, R, c, io, r0 + NN, off_n + (unsigned)NN * io.row_bytes, st_base),
          ...);
     else
@@ -300,7 +307,7 @@ __device__ __forceinline__ void hr_chunk(HrMarch<T, D>& m, d2* R, const Lane& c,
 
 // chunks [k0, k1) of a march of colour Q0 (colour of step 0), the first
 // starting at step n0 (ring phase n0 mod S = P0)
-template <int T, int D, int SK, int MODE, int Q0, bool P2, int P0 = 0>
+template <int T, int D, int SK, int MODE, int Q0, bool P2, int P0 = 0, bool LITE = false>
 __device__ __forceinline__ void hr_run(HrMarch<T, D>& m, d2* R, const Lane& c, const HrIo& io,
                                        int rs0, int k0, int k1, unsigned st_base, int n0 = 0) {
     constexpr int S = Hr<T, D, SK>::S;
@@ -309,7 +316,7 @@ __device__ __forceinline__ void hr_run(HrMarch<T, D>& m, d2* R, const Lane& c, c
         // from taking it for a per-lane value where the march runs inside the
         // chained loop, hr_chain_steady -- a waterfall loop per buffer access)
         const int n = __builtin_amdgcn_readfirstlane(n0 + (k - k0) * S);
-        hr_chunk<T, D, SK, MODE, Q0 ^ (P0 & 1), P2, P0>(
+        hr_chunk<T, D, SK, MODE, Q0 ^ (P0 & 1), P2, P0, LITE>(
             m, R, c, io, rs0 + n, __builtin_amdgcn_readfirstlane((unsigned)n * io.row_bytes),
             st_base, std::make_integer_sequence<int, S>{});
     }
@@ -493,7 +500,7 @@ __host__ __device__ inline bool hr_chain_rows_ok(const SweepParams& prm, int j0,
 // colour Q of the run's first streamed row (the same at every block start: the
 // heights are multiples of the even S).  EM: a strip at a physical left /
 // right side -- kSteadyEdge chunks after a kEdge warm-up
-template <int T, int WAVES, int D, bool P2, int SK, int Q, bool EM>
+template <int T, int WAVES, int D, bool P2, int SK, int Q, bool EM, bool LITE = false>
 __device__ __forceinline__ void hr_chain_steady(const SweepParams& prm,
                                                 const double* __restrict__ src,
                                                 double* __restrict__ dst,
@@ -557,7 +564,8 @@ __device__ __forceinline__ void hr_chain_steady(const SweepParams& prm,
                                          std::make_integer_sequence<int, WR>{});
     for (;;) {
         // the block's H / S steady chunks from ring phase WR (step WU stores row j0)
-        hr_run<T, D, SK, SM, Q, P2, WR>(m, R, c, io, rs0, 0, (j1 - j0) / S, sb, WU);
+        hr_run<T, D, SK, SM, Q, P2, WR, LITE && !EM>(m, R, c, io, rs0, 0, (j1 - j0) / S, sb,
+                                                     WU);
         if (!EM && !c.own_a) {  // lanes that do not own their columns tallied garbage
 #pragma unroll
             for (int t = 0; t < T; ++t) m.acc[t] = 0.0;
@@ -585,7 +593,7 @@ __device__ __forceinline__ void hr_chain_steady(const SweepParams& prm,
 // waves; sor_tb.h chain_run): runs of steady blocks chained (hr_chain_steady),
 // every other block alone (hr_strip); EDGE = 1 (an A/B form): every block
 // alone.  Every wave calls chain_block_end at every block end of the run.
-template <int T, int WAVES, int D, bool P2, int SK, int EDGE>
+template <int T, int WAVES, int D, bool P2, int SK, int EDGE, bool LITE = false>
 __device__ __forceinline__ void hr_chain_run(const SweepParams& prm,
                                              const double* __restrict__ src,
                                              double* __restrict__ dst,
@@ -607,20 +615,20 @@ __device__ __forceinline__ void hr_chain_run(const SweepParams& prm,
         const bool q1 = ((prm.parity + j0 - 2 * T - SK) & 1) != 0;
         if (hr_cols_in<T>(prm, c_out)) {
             if (q1)
-                hr_chain_steady<T, WAVES, D, P2, SK, 1, false>(prm, src, dst, rhs, partials, sh,
+                hr_chain_steady<T, WAVES, D, P2, SK, 1, false, LITE>(prm, src, dst, rhs, partials, sh,
                                                                seg, c_out, bx, by, slot, own_end,
                                                                lane, lx);
             else
-                hr_chain_steady<T, WAVES, D, P2, SK, 0, false>(prm, src, dst, rhs, partials, sh,
+                hr_chain_steady<T, WAVES, D, P2, SK, 0, false, LITE>(prm, src, dst, rhs, partials, sh,
                                                                seg, c_out, bx, by, slot, own_end,
                                                                lane, lx);
         } else {
             if (q1)
-                hr_chain_steady<T, WAVES, D, P2, SK, 1, true>(prm, src, dst, rhs, partials, sh,
+                hr_chain_steady<T, WAVES, D, P2, SK, 1, true, false>(prm, src, dst, rhs, partials, sh,
                                                               seg, c_out, bx, by, slot, own_end,
                                                               lane, lx);
             else
-                hr_chain_steady<T, WAVES, D, P2, SK, 0, true>(prm, src, dst, rhs, partials, sh,
+                hr_chain_steady<T, WAVES, D, P2, SK, 0, true, false>(prm, src, dst, rhs, partials, sh,
                                                               seg, c_out, bx, by, slot, own_end,
                                                               lane, lx);
         }
@@ -645,7 +653,7 @@ __device__ __forceinline__ void hr_chain_run(const SweepParams& prm,
 // the chained split-ring pass (sor_tb.h rb_tbc_kernel's work area and
 // segment lists; EDGE: the kernel of the columns at a physical left / right
 // side, launched beside the main one)
-template <int T, int WAVES, int D, bool P2, int SK, int EDGE>
+template <int T, int WAVES, int D, bool P2, int SK, int EDGE, bool LITE = false>
 __global__ __launch_bounds__(kLanes* WAVES, 2) void rb_tbhc_kernel(
     SweepParams prm, const double* __restrict__ src, double* __restrict__ dst,
     const double* __restrict__ rhs, double* __restrict__ partials,
@@ -673,8 +681,8 @@ __global__ __launch_bounds__(kLanes* WAVES, 2) void rb_tbhc_kernel(
         const int own_end = __builtin_amdgcn_readfirstlane(sh[3]);
         __syncthreads();  // sh is rewritten by the run's block ends
         if (bx < 0) break;
-        hr_chain_run<T, WAVES, D, P2, SK, EDGE>(prm, src, dst, rhs, partials, sh, seg, bx, by,
-                                                slot, own_end, lx);
+        hr_chain_run<T, WAVES, D, P2, SK, EDGE, LITE>(prm, src, dst, rhs, partials, sh, seg, bx,
+                                                      by, slot, own_end, lx);
     }
 }
 

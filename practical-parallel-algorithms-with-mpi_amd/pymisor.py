@@ -26,7 +26,7 @@ SOLVE_RB, SOLVE_RBA = 0, 1
 LEX_A4, LEX_SEQ = 0, 1
 (TUNE_SWEEP_VARIANT, TUNE_ROWS_PER_BLOCK, TUNE_XCD_REMAP, TUNE_SMALL_SOLVE, TUNE_OVERLAP,
  TUNE_TSTEPS, TUNE_TB_VARIANT, TUNE_TB_ROWS, TUNE_TB_PERSISTENT, TUNE_NS_FUSE,
- TUNE_FINISH2, TUNE_TB_RESERVE, TUNE_TB_CHAIN, TUNE_NEAR_BAND) = range(1, 15)
+ TUNE_FINISH2, TUNE_TB_RESERVE, TUNE_TB_CHAIN, TUNE_NEAR_BAND, TUNE_RES_LITE) = range(1, 16)
 COMM_ID_BYTES = 128
 # 3D field ids (misor3_*)
 P3, RHS3, U3, V3, W3, F3, G3, H3 = range(8)
@@ -62,7 +62,8 @@ class Stats(C.Structure):
                 ("iters_per_pass", C.c_int), ("tb_variant", C.c_int),
                 ("halo_ms", C.c_double), ("halos", C.c_longlong),
                 ("allreduce_ms", C.c_double), ("allreduces", C.c_longlong),
-                ("chained", C.c_int), ("ns_ms", C.c_double * 3), ("ns_calls", C.c_longlong * 3)]
+                ("chained", C.c_int), ("ns_ms", C.c_double * 3), ("ns_calls", C.c_longlong * 3),
+                ("lite_misses", C.c_longlong)]
 
 
 class Desc3(C.Structure):
@@ -341,7 +342,8 @@ class Grid:
                 "iters_per_pass": s.iters_per_pass, "tb_variant": s.tb_variant,
                 "halo_ms": s.halo_ms, "halos": s.halos,
                 "allreduce_ms": s.allreduce_ms, "allreduces": s.allreduces,
-                "chained": s.chained, "ns_ms": list(s.ns_ms), "ns_calls": list(s.ns_calls)}
+                "chained": s.chained, "ns_ms": list(s.ns_ms), "ns_calls": list(s.ns_calls),
+                "lite_misses": s.lite_misses}
 
     def reset_stats(self):
         _check(lib().misor_reset_stats(self.h))

@@ -244,6 +244,9 @@ def run_ns(args, world, rank, local_rank, dist, torch):
                nranks=world, rank=rank, comm_id=comm_id)
     if args.tsteps > 0:
         g.set_tuning(M.TUNE_TSTEPS, args.tsteps)
+    if args.tb_variant >= 0:
+        g.set_tuning(M.TUNE_TB_VARIANT, args.tb_variant)
+    g.set_tuning(M.TUNE_RES_LITE, args.res_lite)
     g.ns_setup(prm)
     for f, v in ((M.U, prm["u_init"]), (M.V, prm["v_init"]), (M.P, prm["p_init"])):
         g.fill(f, v)
@@ -346,7 +349,15 @@ def run_ns(args, world, rank, local_rank, dist, torch):
                 "traffic": tr, "traffic_ratio": round(tr / nbytes, 4) if tr else None,
                 "kernel_ms": round(ms, 4), "bytes_per_launch": nbytes}
 
-    solve_kernel = pm.get("solve_kernel") or "rb_tb_kernel"
+    # the solve's passes: the register-ring kernel (T <= 8) or the split ring
+    # (variant 13); the PMC summary's traffic applies only to its own kernel
+    tbv_ns = st.get("tb_variant", 0)
+    solve_kernel = "rb_tbhc_kernel" if tbv_ns == 13 else "rb_tb_kernel"
+    if pm.get("solve_kernel") and pm.get("solve_kernel") != solve_kernel:
+        kp = {k: v for k, v in kp.items() if k != pm.get("solve_kernel")}
+    out["config"]["tb_variant"] = tbv_ns
+    out["config"]["residual_lower_bounds"] = {"on": bool(g.get_tuning(M.TUNE_RES_LITE)),
+                                              "misses": st.get("lite_misses", 0)}
     out["roofline"] = dict(roof(24.0 * lc, pass_ms, solve_kernel),
                            kernel="pressure solve pass (%s, %d iterations per pass, %d passes in "
                                   "the timed steps)" % (solve_kernel, T_ns, passes_ns))

@@ -246,7 +246,7 @@ void launch_sweep_rsq(hipStream_t s, const SweepParams& prm, const double* src, 
 // T iterations per pass: partials[t * nparts + block]
 void launch_finish(hipStream_t s, const double* partials, int nparts, int T, DevState* st,
                    double cells, int decide);
-void launch_decide(hipStream_t s, DevState* st, int T, double cells);
+void launch_decide(hipStream_t s, DevState* st, int T, double cells, int lite = 0);
 // single-rank loop test in two levels (chunk sums, then the finish kernel over
 // kFinishChunks values per stage); scratch holds kMaxT * kFinishChunks doubles
 constexpr int kFinishChunks = 32;

@@ -284,10 +284,16 @@ int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* iters,
     // iteration (DevState::lite_miss): the pass is redone from its source up to
     // there and the rest of the solve counts every cell.  The pass's last
     // iteration is always counted in full, so res after every pass is exact.
-    const bool lite_on = g->res_lite && !g->lite_block && !g->dist && g->finish2 && T > 1;
+    // One rank only: the loop test in the last workgroup of the partial sums.
+    // (The decide kernel after the all-reduce takes the same masks -- the sum
+    // of the ranks' lower bounds is one -- but the inner stages' sums of a
+    // decomposed split-ring pass with a y-split miscount a few cells,
+    // DESIGN.md section 7, so decomposed passes count every iteration.)
+    const bool lite_on = g->res_lite && !g->lite_block && T > 1 && !g->dist && g->finish2;
     auto lite_pass = [&](int Tp, int force) {
         return lite_on && force == 0 && Tp == kShortT && tpl.variant == kHrTbVariant;
     };
+    auto lite_mask = [&](int Tp) { return lite_pass(Tp, 0) ? (1 << (Tp - 1)) - 1 : 0; };
     const int nparts = T == 1 ? g->nparts : tb_parts(tpl);
     double* const rhs = g->fld[kRhs];
     auto pass = [&](hipStream_t s, int part, const double* src, double* dst, int Tp, int force,
@@ -306,7 +312,7 @@ int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* iters,
             // at the end of the interior blocks
             tp.reserve = part == 1 ? g->tb_reserve : 0;
             if (Tp != T) tb_geometry(g, Tp, tp);  // narrower cone: wider strips
-            tp.lite = part == 0 && lite_pass(Tp, force) ? 1 : 0;
+            tp.lite = lite_pass(Tp, force) ? 1 : 0;
             if (tp.chain) {  // chained runs, work stealing (parts 0 / 1 and 2 concurrently)
                 const misor_grid::ChainPlan* pl = nullptr;
                 int rc = chain_plan(g, tp.variant, Tp, part, &pl);
@@ -482,7 +488,7 @@ int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* iters,
                            g->partials + 2 * (long long)g->partials_cap, g->tb_queue + 10, 0);
             rc = allreduce(g, g->st->sum, Tk, 0, g->cstream);
             if (rc) return rc;
-            launch_decide(g->cstream, g->st, Tk, cells);
+            launch_decide(g->cstream, g->st, Tk, cells, lite_mask(Tk));
             HIPCHK(hipEventRecord(g->ev_dk[k & 1], g->cstream));
             if (k + 1 < max_passes && b + 1 < batch) {  // pass k+1's part 2: after both parts of pass k
                 const long long k1 = k + 1;
@@ -563,11 +569,11 @@ int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* iters,
                 launch_finish(g->stream, g->partials, nparts_of(Tk), Tk, g->st, cells, 0);
                 int rc = allreduce(g, g->st->sum, Tk, 0);
                 if (rc) return rc;
-                launch_decide(g->stream, g->st, Tk, cells);
+                launch_decide(g->stream, g->st, Tk, cells, lite_mask(Tk));
             } else if (g->finish2) {  // the loop test in the last workgroup (tb_queue[9])
                 launch_finish2(g->stream, g->partials, nparts_of(Tk), Tk, g->st, cells,
                                g->partials + 2 * (long long)g->partials_cap, g->tb_queue + 9, 1,
-                               lite_pass(Tk, 0) ? (1 << (Tk - 1)) - 1 : 0);
+                               lite_mask(Tk));
             } else {
                 launch_finish(g->stream, g->partials, nparts_of(Tk), Tk, g->st, cells, 1);
             }

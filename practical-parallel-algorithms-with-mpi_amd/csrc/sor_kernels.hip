@@ -559,17 +559,28 @@ void launch_finish(hipStream_t s, const double* partials, int nparts, int T, Dev
 // decomposed runs: st->sum[0..T-1] hold the all-reduced sums r^2 of every rank
 // one thread; the state is read once and written once (it runs on the comm
 // stream beside a full sweep, where every dependent memory round trip is slow)
-__global__ void rb_decide_kernel(DevState* st, int T, double cells) {
+// lite: the stages whose sums are lower bounds (finish_body)
+__global__ void rb_decide_kernel(DevState* st, int T, double cells, int lite) {
     if (st->done) return;
     double sum[kMaxT];
 #pragma unroll
     for (int g = 0; g < kMaxT; ++g) sum[g] = g < T ? st->sum[g] : 0.0;
     const double epssq = st->epssq, nband = st->nband;
     const int itermax = st->itermax;
-    int it = st->it, done = 0, near = 0;
+    int it = st->it, done = 0, near = 0, miss = 0;
     double res = st->res;
     for (int g = 0; g < T && !done; ++g) {
         const double r = sum[g] / cells;
+        if ((lite >> g) & 1) {  // a lower bound: proof that the loop goes on, or a miss
+            const bool on = nband >= 0.0 ? r > epssq + nband : r >= epssq;
+            if (on && it + 1 < itermax) {
+                res = r;
+                ++it;
+                continue;
+            }
+            miss = done = 1;
+            break;
+        }
         if (fabs(r - epssq) <= nband) {  // near the threshold: stop before this iteration
             near = done = 1;
             break;
@@ -582,10 +593,11 @@ __global__ void rb_decide_kernel(DevState* st, int T, double cells) {
     st->it = it;
     st->done = done;
     st->near = near;
+    if (miss) st->lite_miss = 1;
 }
 
-void launch_decide(hipStream_t s, DevState* st, int T, double cells) {
-    hipLaunchKernelGGL(rb_decide_kernel, dim3(1), dim3(1), 0, s, st, T, cells);
+void launch_decide(hipStream_t s, DevState* st, int T, double cells, int lite) {
+    hipLaunchKernelGGL(rb_decide_kernel, dim3(1), dim3(1), 0, s, st, T, cells, lite);
 }
 
 // ---------------------------------------------------------------------------

@@ -13,6 +13,8 @@ bounds off bit for bit, res included: when the bounds decide every iteration,
 when one misses near convergence, and when one misses at once (a near band
 that takes in every residual).
 """
+import threading
+
 import numpy as np
 import pytest
 
@@ -117,6 +119,84 @@ def test_bound_misses_at_once(converging):
     assert it == want_it and abs(res - want_res) <= 1e-12 * want_res
     assert np.array_equal(got, want)
     assert st["lite_misses"] == 1
+
+
+def ranks(world, p0, rhs, dx, dy, eps, itermax, lite, band=None, T=10, variant=13):
+    """`world` in-process ranks (LOCAL transport, the pipelined decomposed loop
+    with its 2T-deep exchanges); the owned blocks assembled into one field"""
+    cid = ("LOCAL:lite%d_%d_%s_%g_%d_%d_%d" % (world, lite, band, eps, itermax, T,
+                                               variant)).encode()
+    outs, errs = [None] * world, []
+
+    def body(r):
+        try:
+            with M.Grid(NI, NJ, dx, dy, 1.9, eps, itermax, device=0, nranks=world, rank=r,
+                        comm_id=cid) as g:
+                g.set_tuning(M.TUNE_TB_VARIANT, variant)
+                g.set_tuning(M.TUNE_TSTEPS, T)
+                g.set_tuning(M.TUNE_RES_LITE, lite)
+                if band is not None:
+                    g.set_tuning(M.TUNE_NEAR_BAND, band)
+                loc = g.loc
+                g.upload(M.P, np.ascontiguousarray(
+                    p0[loc.joff:loc.joff + loc.nj + 2, loc.ioff:loc.ioff + loc.ni + 2]))
+                g.upload(M.RHS, np.ascontiguousarray(
+                    rhs[loc.joff:loc.joff + loc.nj + 2, loc.ioff:loc.ioff + loc.ni + 2]))
+                it, res = g.solve_rb()
+                outs[r] = (loc, g.download(M.P), it, res, g.stats()["lite_misses"])
+        except BaseException as e:
+            errs.append((r, repr(e)))
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(300)
+        assert not t.is_alive(), "rank thread hung"
+    assert not errs, errs
+    got = np.full(p0.shape, np.nan)
+    for loc, blk, it, res, _ in outs:
+        nb = list(loc.neighbours)
+        i0, j0 = (0 if nb[0] < 0 else 1), (0 if nb[2] < 0 else 1)
+        i1 = loc.ni + 1 if nb[1] < 0 else loc.ni
+        j1 = loc.nj + 1 if nb[3] < 0 else loc.nj
+        got[loc.joff + j0:loc.joff + j1 + 1, loc.ioff + i0:loc.ioff + i1 + 1] = \
+            blk[j0:j1 + 1, i0:i1 + 1]
+    assert len({o[2] for o in outs}) == 1 and len({o[3] for o in outs}) == 1  # ranks agree
+    assert len({o[4] for o in outs}) == 1
+    return got, outs[0][2], outs[0][3], outs[0][4]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_decomposed_counts_in_full(world):
+    """decomposed ranks count every iteration (the bounds are one-rank only):
+    no miss, and the same bits as the bounds switched off"""
+    dx, dy = 1.0 / NI, 0.8 / NJ
+    p, rhs = fields(5)
+    want = p.copy()
+    it_w, res_w = orc.solve_rb(want, rhs, dx, dy, 1.9, 1e-300, 30)
+    runs = {}
+    for lite in (1, 0):
+        got, it, res, misses = ranks(world, p, rhs, dx, dy, 1e-300, 30, lite)
+        assert (it, misses) == (it_w, 0)
+        assert abs(res - res_w) <= 1e-12 * res_w
+        assert np.array_equal(got, want)
+        runs[lite] = res
+    assert runs[1] == runs[0]
+
+
+@pytest.mark.xfail(strict=True, reason="known gap (DESIGN.md section 7): on a 2 x 2 split the "
+                   "skewed split ring's leading stages (t < T/2) miscount a few cells of the "
+                   "residual, ~1e-5 relative")
+def test_decomposed_inner_stage_residual(converging):
+    """a converging solve that stops at a leading stage of a 10-iteration pass
+    on 4 ranks: res of that iteration to 1e-12 of the restatement's"""
+    p0, rhs0, dx0, dy0, eps, ks = converging
+    want0 = p0.copy()
+    it_r, res_r = orc.solve_rb(want0, rhs0, dx0, dy0, 1.9, eps, 100000)
+    got, it, res, misses = ranks(4, p0, rhs0, dx0, dy0, eps, 100000, 0)
+    assert it == it_r == ks and np.array_equal(got, want0)
+    assert abs(res - res_r) <= 1e-12 * res_r
 
 
 def test_bad_setting_refused():

@@ -305,9 +305,10 @@ int misor_create(misor_grid** out, const misor_desc* d) {
                                    nb[1] >= 0 && nb[3] >= 0 ? 0 : -1};
             for (int k = 0; k < kDirs; ++k) g->nbr[k] = pn[k];
         }
-        // halo plans up to depth 2*kMaxT, as deep as the smallest block allows
+        // halo plans up to depth 2*kMaxT + 1 (the skewed split ring's), as deep
+        // as the smallest block allows
         const int minb = std::min(d->imax / L.dims[0], d->jmax / L.dims[1]);
-        g->max_depth = std::max(2, std::min(2 * kMaxT, minb));
+        g->max_depth = std::max(2, std::min(2 * kMaxT + 1, minb));
         for (int dd = 1; dd <= g->max_depth; ++dd) build_plan(g, dd);
         // communication and edge blocks at high priority: their workgroups are
         // dispatched ahead of queued interior blocks as slots free up

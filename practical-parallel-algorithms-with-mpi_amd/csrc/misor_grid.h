@@ -176,7 +176,7 @@ struct misor_grid {
     bool dist = false;
     ncclComm_t comm = nullptr;
     int nbr[kDirs] = {-1, -1, -1, -1, -1, -1, -1, -1};  // L R B T BL BR TL TR
-    HaloPlan plan[2 * kMaxT + 1] = {};                   // by halo depth 1 .. 2*kMaxT
+    HaloPlan plan[2 * kMaxT + 2] = {};                   // by halo depth 1 .. 2*kMaxT + 1
     int max_depth = 2;                                   // deepest plan built
     std::shared_ptr<LocalGroup> local;                   // in-process transport
     bool overlap = true;            // exchange on cstream while the interior sweeps

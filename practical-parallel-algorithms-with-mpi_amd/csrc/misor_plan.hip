@@ -207,13 +207,16 @@ int chain_plan(misor_grid* g, int variant, int Tp, int part,
         j0 = 1 + by * tp.rows_per_block;
         j1 = by == nby - 1 ? tp.nj + 1 : j0 + tp.rows_per_block;
     };
+    // (the skewed split ring streams one row more each way: its leading
+    // stages run a row ahead, and the residual they count reads it)
+    const int sk = variant == kHrTbVariant && Tp >= 2 ? 1 : 0;
     auto interior = [&](int bx, int by) {
         int j0, j1;
         rows(by, j0, j1);
         const int lo = 1 + bx * W * OW - 2 * Tp;
         const int hi = 1 + (bx * W + W - 1) * OW - 2 * Tp + kStripCells - 1;
-        return lo >= tp.int_lo_i && hi <= tp.int_hi_i && j0 - 2 * Tp >= tp.int_lo_j &&
-               j1 - 1 + 2 * Tp <= tp.int_hi_j;
+        return lo >= tp.int_lo_i && hi <= tp.int_hi_i && j0 - 2 * Tp - sk >= tp.int_lo_j &&
+               j1 - 1 + 2 * Tp + sk <= tp.int_hi_j;
     };
     auto steady = [&](int by) {  // sor_tb.h chain_rows_ok
         int j0, j1;

@@ -273,7 +273,10 @@ int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* iters,
     // time the communication steps of the loop (collected after each batch)
     g->comm_timing = g->timing && g->dist;
     g->cev_used[0] = g->cev_used[1] = 0;
-    const int depth = 2 * T;  // halo of src each pass needs
+    // halo of src each pass needs: 2T, one row more for the skewed split ring
+    // (its leading stages run one row ahead of the trailing ones; the top rows
+    // of their residual windows at a neighbour above read row nj + 2T + 1)
+    const int depth = 2 * T + (T >= 2 && tpl.variant == kHrTbVariant && 2 * T < g->max_depth);
     // Residual lower bounds (MISOR_TUNE_RES_LITE): on one rank, a
     // kShortT-iteration split-ring pass counts r^2 of its iterations but the
     // last on one row in S of its steady chunks (sor_tbh.h hrs_step LITE), one
@@ -284,12 +287,10 @@ int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* iters,
     // iteration (DevState::lite_miss): the pass is redone from its source up to
     // there and the rest of the solve counts every cell.  The pass's last
     // iteration is always counted in full, so res after every pass is exact.
-    // One rank only: the loop test in the last workgroup of the partial sums.
-    // (The decide kernel after the all-reduce takes the same masks -- the sum
-    // of the ranks' lower bounds is one -- but the inner stages' sums of a
-    // decomposed split-ring pass with a y-split miscount a few cells,
-    // DESIGN.md section 7, so decomposed passes count every iteration.)
-    const bool lite_on = g->res_lite && !g->lite_block && T > 1 && !g->dist && g->finish2;
+    // (one rank: the loop test in the last workgroup of the partial sums;
+    // decomposed: the decide kernel after the all-reduce -- the sum of the
+    // ranks' lower bounds is one)
+    const bool lite_on = g->res_lite && !g->lite_block && T > 1 && (g->dist || g->finish2);
     auto lite_pass = [&](int Tp, int force) {
         return lite_on && force == 0 && Tp == kShortT && tpl.variant == kHrTbVariant;
     };

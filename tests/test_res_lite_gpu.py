@@ -167,10 +167,12 @@ def ranks(world, p0, rhs, dx, dy, eps, itermax, lite, band=None, T=10, variant=1
     return got, outs[0][2], outs[0][3], outs[0][4]
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_decomposed_counts_in_full(world):
-    """decomposed ranks count every iteration (the bounds are one-rank only):
-    no miss, and the same bits as the bounds switched off"""
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_decomposed_bounds(world, converging):
+    """decomposed ranks: the all-reduced sum of the ranks' lower bounds decides
+    (sor_kernels.hip rb_decide_kernel); far from eps every bound holds and the
+    bits equal the bounds switched off; near convergence one misses and the
+    solve still ends at k* with p bit for bit"""
     dx, dy = 1.0 / NI, 0.8 / NJ
     p, rhs = fields(5)
     want = p.copy()
@@ -183,20 +185,49 @@ def test_decomposed_counts_in_full(world):
         assert np.array_equal(got, want)
         runs[lite] = res
     assert runs[1] == runs[0]
-
-
-@pytest.mark.xfail(strict=True, reason="known gap (DESIGN.md section 7): on a 2 x 2 split the "
-                   "skewed split ring's leading stages (t < T/2) miscount a few cells of the "
-                   "residual, ~1e-5 relative")
-def test_decomposed_inner_stage_residual(converging):
-    """a converging solve that stops at a leading stage of a 10-iteration pass
-    on 4 ranks: res of that iteration to 1e-12 of the restatement's"""
     p0, rhs0, dx0, dy0, eps, ks = converging
     want0 = p0.copy()
     it_r, res_r = orc.solve_rb(want0, rhs0, dx0, dy0, 1.9, eps, 100000)
-    got, it, res, misses = ranks(4, p0, rhs0, dx0, dy0, eps, 100000, 0)
+    got, it, res, misses = ranks(world, p0, rhs0, dx0, dy0, eps, 100000, 1)
+    assert (it, misses) == (ks, 1) and it_r == ks
+    assert abs(res - res_r) <= 1e-12 * res_r
+    assert np.array_equal(got, want0)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("band", [None, 400])
+def test_decomposed_inner_stage_residual(converging, world, band):
+    """a converging solve that stops at a leading stage (t < T/2, one row
+    ahead in the skewed march) of a 10-iteration pass: res of that iteration
+    to 1e-12 of the restatement's on every split, y-splits included (their
+    top blocks read one halo row more: the 2T + 1-deep exchange)"""
+    p0, rhs0, dx0, dy0, eps, ks = converging
+    want0 = p0.copy()
+    it_r, res_r = orc.solve_rb(want0, rhs0, dx0, dy0, 1.9, eps, 100000)
+    got, it, res, misses = ranks(world, p0, rhs0, dx0, dy0, eps, 100000, 0, band=band)
     assert it == it_r == ks and np.array_equal(got, want0)
     assert abs(res - res_r) <= 1e-12 * res_r
+
+
+def test_decomposed_leading_stage_near_eps():
+    """eps^2 within 5e-7 of a leading stage's residual on 4 ranks: the solve
+    stops exactly there (before the 2T + 1-deep exchange it ran one iteration
+    on: the top rows of the leading stages' residual read a stale halo row)"""
+    dx, dy = 1.0 / NI, 1.0 / NJ
+    rng = np.random.default_rng(7)
+    p0 = rng.standard_normal((NJ + 2, NI + 2)) * 2.0 ** -30
+    rhs = np.zeros_like(p0)
+    q, res = p0.copy(), {}
+    for k in range(1, 47):
+        res[k] = orc.solve_rb(q, rhs, dx, dy, 1.9, 1e-300, 1)[1]
+    for k in (41, 43, 45):  # stages 0, 2, 4 of the fifth pass
+        lo = min(res[j] for j in range(1, k))
+        if not res[k] * (1 + 5e-7) < lo:
+            continue
+        eps = (res[k] * (1 + 5e-7)) ** 0.5
+        got, it, r, _ = ranks(4, p0, rhs, dx, dy, eps, 100000, 0, band=400)
+        assert it == k, (k, it)
+        assert abs(r - res[k]) <= 1e-12 * res[k]
 
 
 def test_bad_setting_refused():

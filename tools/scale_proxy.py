@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--shapes", default="",
                     help="explicit local blocks NIxNJ[:N],... instead of the decomposition of --ranks")
     ap.add_argument("--variants", default="-1", help="TB variants to try (-1: default)")
+    ap.add_argument("--res-lite", type=int, choices=(0, 1), default=1,
+                    help="residual lower bounds of the 10-iteration passes (MISOR_TUNE_RES_LITE)")
     ap.add_argument("--remap", default="1", help="XCD-aware block remap settings to try")
     ap.add_argument("--persistent", default="1", help="work-queue launch settings to try")
     ap.add_argument("--chain", default="-1",
@@ -136,6 +138,7 @@ def main():
                     g.set_tuning(M.TUNE_TSTEPS, T)
                     g.set_tuning(M.TUNE_TB_VARIANT, v0 if v < 0 else v)
                 g.set_tuning(M.TUNE_TB_ROWS, r)
+                g.set_tuning(M.TUNE_RES_LITE, args.res_lite)
                 hrow[c] = g.get_tuning(M.TUNE_TB_ROWS)
                 g.solve_rb(itermax=args.sweeps)  # (plans of the new setting built)
                 g.reset_stats()

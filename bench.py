@@ -242,10 +242,10 @@ def run_ns(args, world, rank, local_rank, dist, torch):
         comm_id = obj[0]
     g = M.Grid(imax, jmax, dx, dy, prm["omg"], prm["eps"], prm["itermax"], device=local_rank,
                nranks=world, rank=rank, comm_id=comm_id)
+    if args.tb_variant >= 0:  # (the variant first: T = 10 needs the split ring)
+        g.set_tuning(M.TUNE_TB_VARIANT, args.tb_variant)
     if args.tsteps > 0:
         g.set_tuning(M.TUNE_TSTEPS, args.tsteps)
-    if args.tb_variant >= 0:
-        g.set_tuning(M.TUNE_TB_VARIANT, args.tb_variant)
     g.set_tuning(M.TUNE_RES_LITE, args.res_lite)
     g.ns_setup(prm)
     for f, v in ((M.U, prm["u_init"]), (M.V, prm["v_init"]), (M.P, prm["p_init"])):
@@ -361,6 +361,14 @@ def run_ns(args, world, rank, local_rank, dist, torch):
     out["roofline"] = dict(roof(24.0 * lc, pass_ms, solve_kernel),
                            kernel="pressure solve pass (%s, %d iterations per pass, %d passes in "
                                   "the timed steps)" % (solve_kernel, T_ns, passes_ns))
+    # the solve pass's VALU issue (SQ_ACTIVE_INST_VALU per wave x 2 waves per
+    # SIMD, the committed PMC summary): >= 0.85 -- VALU-bound (the 10-iteration
+    # split-ring passes, as the headline's)
+    vb = kp.get(solve_kernel, {}).get("valu_busy_per_wave")
+    if vb is not None:
+        out["roofline"]["valu_busy_per_simd"] = round(2 * vb, 3)
+        if 2 * vb >= 0.85:
+            out["roofline"]["bound"] = "valu"
     out["kernels"] = {
         "fg_rhs_kernel": dict(roof(40.0 * lc, fg_ms, "fg_rhs_kernel"),
                               what="computeFG + computeRHS fused (solver.c:360-436, 122-138)"),

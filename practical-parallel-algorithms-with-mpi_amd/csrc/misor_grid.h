@@ -131,6 +131,7 @@ struct misor_grid {
     bool tsteps_set = false;      // T requested by MISOR_TUNE_TSTEPS (else the default rule)
     bool short_plan = false;      // capped solves may run as kShortT-iteration split-ring passes
     bool short_all = false;       // ... every solve of more than kDefaultTsteps iterations
+    bool short_all_lite = false;  // ... the same while res_lite is on
     SweepParams tp{};             // its launch geometry (for T = tsteps)
     int tb_nparts = 0;
     int tb_rows_req = 0;          // MISOR_TUNE_TB_ROWS (0: automatic)

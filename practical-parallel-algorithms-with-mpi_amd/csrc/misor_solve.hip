@@ -260,8 +260,9 @@ int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* iters,
     // one on the blocks where configure_tb sets short_all, so there every solve
     // of more than 8 iterations takes it.
     const int todo0 = itermax - it0;
+    const bool all = g->short_all || (g->short_all_lite && g->res_lite);
     const bool shortp = g->short_plan && effective_tsteps(g) == kDefaultTsteps &&
-                        (g->short_all ? todo0 > kDefaultTsteps
+                        (all ? todo0 > kDefaultTsteps
                                       : 7LL * ((todo0 + kShortT - 1) / kShortT) <
                                             5LL * ((todo0 + kDefaultTsteps - 1) / kDefaultTsteps));
     const int T = shortp ? kShortT : effective_tsteps(g);

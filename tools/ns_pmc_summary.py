@@ -46,13 +46,18 @@ def main():
     a = ap.parse_args()
     fetch = per_kernel(a.dir, "fetch", "FETCH_SIZE")
     write = per_kernel(a.dir, "write", "WRITE_SIZE")
+    cyc = per_kernel(a.dir, "sq", "SQ_WAVE_CYCLES")
+    vbusy = per_kernel(a.dir, "sq", "SQ_ACTIVE_INST_VALU")
     cells = a.size * a.size
     res = {"size": a.size, "nranks": a.nranks, "kernels": {}}
     for k in sorted(fetch):
         if k not in write:
             continue
-        f = sum(fetch[k]) / len(fetch[k])
-        w = sum(write[k]) / len(write[k])
+        # the split ring runs a pass as two launches (main and edge lists):
+        # bytes per pass = the mean launch x 2
+        per = 2 if k == "rb_tbhc_kernel" else 1
+        f = sum(fetch[k]) / len(fetch[k]) * per
+        w = sum(write[k]) / len(write[k]) * per
         b = f * 1024 * 2 + w * 1024
         alg = KERNELS[k] * cells
         res["kernels"][k] = {"launches": len(fetch[k]), "fetch_size_kb_raw": f,
@@ -60,6 +65,8 @@ def main():
                              "write_bytes": w * 1024, "bytes_per_launch": b,
                              "algorithmic_bytes_per_launch": alg,
                              "ratio_to_algorithmic": b / alg}
+        if cyc.get(k) and vbusy.get(k):
+            res["kernels"][k]["valu_busy_per_wave"] = round(sum(vbusy[k]) / sum(cyc[k]), 3)
     if all(k in res["kernels"] for k in NORMALIZE):
         b = sum(res["kernels"][k]["bytes_per_launch"] for k in NORMALIZE)
         res["kernels"]["normalize_pressure"] = {
@@ -70,7 +77,8 @@ def main():
         res["solve_kernel"] = solve[0]
     res["note"] = ("separate rocprofv3 --pmc passes of bench.py --workload ns; FETCH_SIZE x1024 x2 "
                    "(gfx950: 128-B requests tallied at 64 B) + WRITE_SIZE x1024; the solve kernel's "
-                   "bytes are per pass (its launches run 7 or 8 iterations each)")
+                   "bytes are per pass (rb_tbhc_kernel: two launches per pass, main and edge "
+                   "lists); valu_busy_per_wave = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES")
     json.dump(res, open(a.out, "w"), indent=1)
     print(json.dumps(res["kernels"], indent=1))
 

@@ -422,12 +422,14 @@ int configure_tb(misor_grid* g, int T, int variant, int rows) {
     const bool small_chain = cells >= kHrAllCells && cells < kTsteps8Cells &&
                              chain_on(g, variant);
     g->short_all = small_chain || (!g->dist && cells >= 2 * kTsteps8Cells);
-    //  - round 6: a single rank of 2^28 cells too while the residual lower
-    //    bounds are on (MISOR_TUNE_RES_LITE: one FMA per update fewer on the
-    //    10-iteration passes) -- NS config 5, 16384^2 with 100 iterations per
-    //    solve: 20.63-20.66 ms per step against 21.85-22.57 for the 13 T = 8
-    //    passes (profiles/r06_ns_plan_ab.txt)
-    g->short_all_lite = !g->dist && cells >= kTsteps8Cells;
+    //  - round 6: blocks of >= 2^28 cells too, one rank or decomposed, while
+    //    the residual lower bounds are on (MISOR_TUNE_RES_LITE: one FMA per
+    //    update fewer on the 10-iteration passes) -- NS config 5, 16384^2 with
+    //    100 iterations per solve: 20.63-20.66 ms per step against 21.85-22.57
+    //    for the 13 T = 8 passes (profiles/r06_ns_plan_ab.txt); the 4-GPU rank
+    //    block (sides L, B) at 100 iterations: 0.2072-0.2081 against
+    //    0.2189-0.2224 ms per iteration (profiles/r06_plan_ab_rank100.txt)
+    g->short_all_lite = cells >= kTsteps8Cells;
     g->short_plan = variant == kDefaultTbVariant && !g->tsteps_set &&
                     g->tb_persistent &&
                     (g->short_all ||

@@ -564,8 +564,7 @@ __device__ __forceinline__ void hr_chain_steady(const SweepParams& prm,
                                          std::make_integer_sequence<int, WR>{});
     for (;;) {
         // the block's H / S steady chunks from ring phase WR (step WU stores row j0)
-        hr_run<T, D, SK, SM, Q, P2, WR, LITE && !EM>(m, R, c, io, rs0, 0, (j1 - j0) / S, sb,
-                                                     WU);
+        hr_run<T, D, SK, SM, Q, P2, WR, LITE>(m, R, c, io, rs0, 0, (j1 - j0) / S, sb, WU);
         if (!EM && !c.own_a) {  // lanes that do not own their columns tallied garbage
 #pragma unroll
             for (int t = 0; t < T; ++t) m.acc[t] = 0.0;
@@ -624,11 +623,11 @@ __device__ __forceinline__ void hr_chain_run(const SweepParams& prm,
                                                                lane, lx);
         } else {
             if (q1)
-                hr_chain_steady<T, WAVES, D, P2, SK, 1, true, false>(prm, src, dst, rhs, partials, sh,
+                hr_chain_steady<T, WAVES, D, P2, SK, 1, true, LITE>(prm, src, dst, rhs, partials, sh,
                                                               seg, c_out, bx, by, slot, own_end,
                                                               lane, lx);
             else
-                hr_chain_steady<T, WAVES, D, P2, SK, 0, true, false>(prm, src, dst, rhs, partials, sh,
+                hr_chain_steady<T, WAVES, D, P2, SK, 0, true, LITE>(prm, src, dst, rhs, partials, sh,
                                                               seg, c_out, bx, by, slot, own_end,
                                                               lane, lx);
         }

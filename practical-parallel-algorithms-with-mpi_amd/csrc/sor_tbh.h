@@ -170,7 +170,22 @@ __device__ __forceinline__ void hr_step(HrMarch<T, D>& m, d2* R, const Lane& c, 
 // residual windows sit one row higher (stage<..., SKH>).  Register ring: rows
 // n - 2K + 2 .. n + 1 + D; the row the leading register stages read last (n -
 // 2K + 2) moves to the LDS ring, which holds rows down to n - 2T + 1.
-template <int T, int D, int MODE, int Q, int PH, bool P2, bool LITE = false>
+//
+// NW >= 0: step NW of an interior warm-up (kPre, from the stream's first row
+// rs0 = rs - 1, rs = j0 - 2T the first row of the block's cone).  Stage t's
+// outputs matter from row rs + 2t + 2 on (the cone narrows by two rows per
+// iteration), which read its input rows from rs + 2t: a stage must take in
+// (A := In) every input row from there.  Its input row is rin = rs + n - 2t
+// (leading stages) or rs - 1 + n - 2t (trailing), so it matters from step 4t
+// (4t + 1); the stages are skipped before that, less a two-step margin --
+// 167 of the 410 stage steps of a T = 10 warm-up.  A skipped stage's rows
+// stay zero where the full march held values outside every cone.
+template <int T, int SKH>
+__host__ __device__ constexpr int hr_warm_start(int t) {
+    return t < SKH ? 4 * t - 2 : 4 * t - 1;
+}
+
+template <int T, int D, int MODE, int Q, int PH, bool P2, bool LITE = false, int NW = -1>
 __device__ __forceinline__ void hrs_step(HrMarch<T, D>& m, d2* R, const Lane& c, const HrIo& io,
                                          int r0, unsigned off_n, unsigned st_base) {
     using G = Hr<T, D, 1>;
@@ -221,17 +236,22 @@ __device__ __forceinline__ void hrs_step(HrMarch<T, D>& m, d2* R, const Lane& c,
                                                   rr(T - 1, true), rr(T - 1, false),
                                                   m.acc[T - 1]);
     } else {
+        // (NW: the warm-up's stages before their cone, skipped)
+        auto runs = [](int t) { return NW < 0 || NW >= hr_warm_start<T, SKH>(t); };
 #pragma unroll
         for (int t = SKH; t < T; ++t) {
+            if (!runs(t)) continue;
             if (t == T - 1) prevM2 = m.M2[t];
             u = stage<T, Q, MODE, false, P2, SKH>(c, t, true, u, r0 - 2 * t, m.A[t], m.M1[t],
                                                   m.M2[t], rr(t, true), rr(t, false), m.acc[t]);
         }
 #pragma unroll
-        for (int t = 0; t < SKH; ++t)
+        for (int t = 0; t < SKH; ++t) {
+            if (!runs(t)) continue;
             v = stage<T, 1 - Q, MODE, false, P2, SKH>(c, t, t > 0, v, r0 + 1 - 2 * t, m.A[t],
                                                       m.M1[t], m.M2[t], rr(t, true),
                                                       rr(t, false), m.acc[t]);
+        }
     }
     m.B = v;
     {
@@ -288,15 +308,16 @@ __device__ __forceinline__ void hrs_step(HrMarch<T, D>& m, d2* R, const Lane& c,
     __builtin_amdgcn_sched_barrier(0);
 }
 
-// steps NN of a chunk whose first step has ring phase P0 and colour Q0
+// steps NN of a chunk whose first step has ring phase P0 and colour Q0 (N0 >=
+// 0: an interior warm-up chunk from its step N0, hrs_step NW)
 template <int T, int D, int SK, int MODE, int Q0, bool P2, int P0 = 0, bool LITE = false,
-          int... NN>
+          int N0 = -1, int... NN>
 __device__ __forceinline__ void hr_chunk(HrMarch<T, D>& m, d2* R, const Lane& c, const HrIo& io,
                                          int r0, unsigned off_n, unsigned st_base,
                                          std::integer_sequence<int, NN...>) {
     constexpr int S = Hr<T, D, SK>::S;
     if constexpr (SK)
-        (hrs_step<T, D, MODE, Q0 ^ (NN & 1), (P0 + NN) % S, P2, LITE>(
+        (hrs_step<T, D, MODE, Q0 ^ (NN & 1), (P0 + NN) % S, P2, LITE, N0 < 0 ? -1 : N0 + NN>(
              m, R, c, io, r0 + NN, off_n + (unsigned)NN * io.row_bytes, st_base),
          ...);
     else
@@ -320,6 +341,39 @@ __device__ __forceinline__ void hr_run(HrMarch<T, D>& m, d2* R, const Lane& c, c
             m, R, c, io, rs0 + n, __builtin_amdgcn_readfirstlane((unsigned)n * io.row_bytes),
             st_base, std::make_integer_sequence<int, S>{});
     }
+}
+
+// the warm-up of a block or chained run: WU steps from the stream's first row
+// (KW whole chunks and WR steps, colour Q at step 0).  The interior warm-up
+// (kPre, skewed) is unrolled step by step and skips each stage's steps before
+// its cone (hrs_step NW); the others march the KW chunks in a loop.
+template <int T, int D, int SK, int MODE, int Q, bool P2, int... KK>
+__device__ __forceinline__ void hr_warm_chunks(HrMarch<T, D>& m, d2* R, const Lane& c,
+                                               const HrIo& io, int rs0, unsigned sb,
+                                               std::integer_sequence<int, KK...>) {
+    constexpr int S = Hr<T, D, SK>::S;
+    (hr_chunk<T, D, SK, MODE, Q, P2, 0, false, KK * S>(
+         m, R, c, io, rs0 + KK * S, __builtin_amdgcn_readfirstlane((unsigned)(KK * S) * io.row_bytes),
+         sb, std::make_integer_sequence<int, S>{}),
+     ...);
+}
+
+template <int T, int D, int SK, int MODE, int Q, bool P2>
+__device__ __forceinline__ void hr_warm(HrMarch<T, D>& m, d2* R, const Lane& c, const HrIo& io,
+                                        int rs0, unsigned sb) {
+    using G = Hr<T, D, SK>;
+    constexpr int S = G::S, KW = G::WU / S, WR = G::WR;
+    constexpr bool kSkip = MODE == kPre && SK != 0;
+    if constexpr (kSkip)
+        hr_warm_chunks<T, D, SK, MODE, Q, P2>(m, R, c, io, rs0, sb,
+                                              std::make_integer_sequence<int, KW>{});
+    else
+        hr_run<T, D, SK, MODE, Q, P2>(m, R, c, io, rs0, 0, KW, sb);
+    if constexpr (WR > 0)
+        hr_chunk<T, D, SK, MODE, Q, P2, 0, false, kSkip ? KW * S : -1>(
+            m, R, c, io, rs0 + KW * S,
+            __builtin_amdgcn_readfirstlane((unsigned)(KW * S) * io.row_bytes), sb,
+            std::make_integer_sequence<int, WR>{});
 }
 
 // the per-lane constants of the strip whose owned columns start at c_out,
@@ -444,15 +498,11 @@ __device__ __forceinline__ void hr_strip(const SweepParams& prm, const double* _
         // stores: step n finishes row rs0 + n - 2T = j0 + n - WU; the warm-up:
         // KW whole chunks and WR steps, then H / S steady chunks from phase WR
         const unsigned sb = (unsigned)WU * io.row_bytes;
-        constexpr int KW = WU / S, WR = Hr<T, D, SK>::WR;
+        constexpr int WR = Hr<T, D, SK>::WR;
         const int nsteady = (j1 - j0) / S;
         auto warm_steady = [&](auto q_c) {
             constexpr int Q = decltype(q_c)::value;
-            hr_run<T, D, SK, kPre, Q, P2>(m, R, c, io, rs0, 0, KW, sb);
-            if constexpr (WR > 0)
-                hr_chunk<T, D, SK, kPre, Q, P2, 0>(m, R, c, io, rs0 + KW * S,
-                                                   (unsigned)(KW * S) * io.row_bytes, sb,
-                                                   std::make_integer_sequence<int, WR>{});
+            hr_warm<T, D, SK, kPre, Q, P2>(m, R, c, io, rs0, sb);
             hr_run<T, D, SK, kSteady, Q, P2, WR>(m, R, c, io, rs0, 0, nsteady, sb, WU);
         };
         if (q1) warm_steady(std::integral_constant<int, 1>{});
@@ -510,7 +560,7 @@ __device__ __forceinline__ void hr_chain_steady(const SweepParams& prm,
                                                 const int bx, int by, const int slot,
                                                 int own_end, const int lane, lds_double* lx) {
     using G = Hr<T, D, SK>;
-    constexpr int S = G::S, WU = G::WU, KW = WU / S, WR = G::WR;
+    constexpr int S = G::S, WU = G::WU, WR = G::WR;
     const int c_ld = c_out - 2 * T;
     int j0, j1;
     block_rows(prm, by, j0, j1);
@@ -555,13 +605,9 @@ __device__ __forceinline__ void hr_chain_steady(const SweepParams& prm,
     for (int k = 0; k < D; ++k) m.Pq[k] = bload(io.p, io.lane, (unsigned)(k + SK) * io.row_bytes);
 #pragma unroll
     for (int k = 0; k < D + SK; ++k) R[k] = bload(io.r, io.lane, (unsigned)k * io.row_bytes);
-    // the warm-up of the run's first block: KW whole chunks and WR steps (hr_strip)
+    // the warm-up of the run's first block (hr_warm)
     const unsigned sb = (unsigned)WU * io.row_bytes;
-    hr_run<T, D, SK, WM, Q, P2>(m, R, c, io, rs0, 0, KW, sb);
-    if constexpr (WR > 0)
-        hr_chunk<T, D, SK, WM, Q, P2, 0>(m, R, c, io, rs0 + KW * S,
-                                         (unsigned)(KW * S) * io.row_bytes, sb,
-                                         std::make_integer_sequence<int, WR>{});
+    hr_warm<T, D, SK, WM, Q, P2>(m, R, c, io, rs0, sb);
     for (;;) {
         // the block's H / S steady chunks from ring phase WR (step WU stores row j0)
         hr_run<T, D, SK, SM, Q, P2, WR, LITE>(m, R, c, io, rs0, 0, (j1 - j0) / S, sb, WU);

@@ -184,6 +184,12 @@ struct SweepParams {
     unsigned long long* trace;  // diagnostics (MISOR_CHAIN_TRACE): per block L, 3 words --
                                 // start and end (wall clock, 100 MHz), workgroup | run start
     const unsigned long long* seg_tmpl;  // the initial list (device; copied per launch)
+    // the split ring's edge kernel: once its own list is done, its workgroups
+    // steal from the main list's work area (initialised before either kernel
+    // starts: no_init on the main launch); nullptr: no second list
+    int* alt_work = nullptr;
+    int alt_nseg0 = 0;
+    int no_init = 0;          // the work area is initialised already (misor_solve.hip)
 };
 
 // Chained passes: a segment word holds the next unclaimed block row (bits

@@ -351,6 +351,22 @@ int solve_rb_from(misor_grid* g, int itermax, int it0, double res0, int* iters,
                 const bool fork = has_e && has_m;
                 hipStream_t ms = fork ? g->xstream[k] : s;
                 if (fork) {
+                    // A whole pass: the edge kernel's workgroups go on to steal
+                    // from the main list once the edge list is done (its 2.5x
+                    // block cost is an estimate: its kernel ended ~2.5 ms before
+                    // the main one in a 6.6 ms 32768^2 pass, its slots idle), so
+                    // the main list's work area is initialised here, before
+                    // either kernel starts.  Not in a pipelined pass's parts:
+                    // there the edge slots, once free, are part 2's
+                    // (profiles/r06_edge_steal_ab.txt: the 8-GPU rank's loop 3%
+                    // slower with them stealing)
+                    if (part == 0) {
+                        launch_chain_init(s, g->tb_work[k], pl->main.tmpl, pl->main.nseg0,
+                                          tm.seg_cap);
+                        tm.no_init = 1;
+                        te.alt_work = g->tb_work[k];
+                        te.alt_nseg0 = pl->main.nseg0;
+                    }
                     HIPCHK(hipEventRecord(g->ev_fork[k], s));
                     HIPCHK(hipStreamWaitEvent(g->xstream[k], g->ev_fork[k], 0));
                 }

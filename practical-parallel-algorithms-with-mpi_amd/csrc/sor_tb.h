@@ -924,15 +924,17 @@ __device__ __forceinline__ unsigned long long chain_load(const unsigned long lon
 // The run a workgroup takes next, into sh[0..3] = column, block row, segment
 // slot (-1: a private range), end of the blocks it owns (own_end); sh[8] =
 // the blocks its segment had unclaimed; sh[0] = -1: no work left.  Wave 0
-// only.
+// only.  alt_n0 >= 0: another launch's list of alt_n0 initial segments (the
+// split ring's main list, taken by the edge kernel once its own is done):
+// steals only -- its tickets are that launch's workgroups'
 __device__ __forceinline__ void chain_acquire(const SweepParams& prm, int* head,
                                               unsigned long long* seg,
-                                              int* sh) {
+                                              int* sh, int alt_n0 = -1) {
     const int lane = threadIdx.x & 63;
-    const int n0 = prm.nseg0;
+    const int n0 = alt_n0 >= 0 ? alt_n0 : prm.nseg0;
     // 1. the initial segments, by ticket: the home XCD's run first
     int got = 0;
-    if (lane == 0) {
+    if (lane == 0 && alt_n0 < 0) {
         const int home = blockIdx.x % 8;
         for (int probe = 0; probe < 8;) {
             const int x = (home + probe) & 7;
@@ -961,7 +963,10 @@ __device__ __forceinline__ void chain_acquire(const SweepParams& prm, int* head,
         const int ndyn = min(__hip_atomic_load(&head[8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
                              prm.seg_cap);
         const int n = n0 + ndyn;
-        int best_r = 1, best_k = -1;
+        // (another launch's list: only ranges of 2 blocks or more are taken, a
+        // stolen run paying its warm-up once for them)
+        const int r_min = alt_n0 >= 0 ? 4 : 2;
+        int best_r = r_min - 1, best_k = -1;
         constexpr int U = 8;  // loads in flight per lane
         for (int k0 = 0; k0 < n; k0 += 64 * U) {
             unsigned long long w[U];
@@ -997,7 +1002,7 @@ __device__ __forceinline__ void chain_acquire(const SweepParams& prm, int* head,
             unsigned long long w = chain_load(seg + best_k);
             for (;;) {
                 const int N = chain_next(w), E = chain_end(w), r = E - N;
-                if (r < 2) break;
+                if (r < r_min) break;
                 const int m = E - r / 2;  // the owner keeps [N, m)
                 const unsigned long long nw =
                     chain_word(chain_col(w), N, m);

@@ -61,8 +61,9 @@ void MISOR_CAT(launch_tb_t, MISOR_TB_T)(hipStream_t s, const SweepParams& prm,
         {
             // the chained split-ring pass (sor_tbh.h rb_tbhc_kernel; configure_tb
             // keeps its passes chained and persistent): the work area gets the
-            // launch's initial segment list (as the chained pass below)
-            launch_chain_init(s, queue, prm.seg_tmpl, prm.nseg0, prm.seg_cap);
+            // launch's initial segment list (as the chained pass below), unless
+            // the caller initialised it before the edge kernel (no_init)
+            if (!prm.no_init) launch_chain_init(s, queue, prm.seg_tmpl, prm.nseg0, prm.seg_cap);
             auto gc = [&](auto kernel, int resident) {
                 const int grid = std::min(prm.chain_blocks, std::max(8, resident - prm.reserve));
                 hipLaunchKernelGGL(kernel, dim3(grid), dim3(kLanes * 4), 0, s, prm, src, dst, rhs,

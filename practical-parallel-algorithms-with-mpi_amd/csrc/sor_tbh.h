@@ -712,9 +712,15 @@ __global__ __launch_bounds__(kLanes* WAVES, 2) void rb_tbhc_kernel(
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     lds_double* lx = (lds_double*)(ring + wave * S * kStripCells);
     unsigned long long* seg = reinterpret_cast<unsigned long long*>(work + kChainHead);
+    // the edge kernel, its own list done: steals from the main list's runs
+    // (prm.alt_work), whose work area was initialised before this launch
+    bool alt = false;
     for (;;) {
         __syncthreads();  // every wave has read the last claim of the previous run
-        if (threadIdx.x < kLanes) chain_acquire(prm, work, seg, sh);
+        if (threadIdx.x < kLanes) {
+            if (alt) chain_acquire(prm, prm.alt_work, seg, sh, prm.alt_nseg0);
+            else     chain_acquire(prm, work, seg, sh);
+        }
         if (prm.trace && threadIdx.x == 0) {
             *reinterpret_cast<volatile unsigned long long*>(sh + 4) = wall_clock64();
             sh[6] = 1;
@@ -725,7 +731,12 @@ __global__ __launch_bounds__(kLanes* WAVES, 2) void rb_tbhc_kernel(
         const int slot = __builtin_amdgcn_readfirstlane(sh[2]);
         const int own_end = __builtin_amdgcn_readfirstlane(sh[3]);
         __syncthreads();  // sh is rewritten by the run's block ends
-        if (bx < 0) break;
+        if (bx < 0) {
+            if (alt || prm.alt_work == nullptr) break;
+            alt = true;
+            seg = reinterpret_cast<unsigned long long*>(prm.alt_work + kChainHead);
+            continue;
+        }
         hr_chain_run<T, WAVES, D, P2, SK, EDGE, LITE>(prm, src, dst, rhs, partials, sh, seg, bx,
                                                       by, slot, own_end, lx);
     }
